@@ -1,0 +1,57 @@
+"""Build the native libraries in-tree (they travel to the GPU box with the repo).
+
+  libsvo_rt.so    : C-ABI + gfx950 HIP kernels (include/svo_rt.h)
+  libsvo_build.so : native SVO builder (include/svo_build.h)
+
+hipcc cross-compiles gfx950 without a GPU.  Flags: -ffp-contract=off and no
+fast-math so f32 arithmetic rounds exactly like the strict-IEEE oracle.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+ARCH = os.environ.get("SVO_OFFLOAD_ARCH", "gfx950")
+
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+          "-Wno-unused-value", "-Wno-unused-result", "-I" + INCLUDE, "-I" + CSRC]
+
+TARGETS = {
+    "libsvo_rt.so": ["svo_rt.hip", "svo_kernel.hip"],
+    "libsvo_build.so": ["svo_build.hip"],
+}
+
+
+def _stale(out, srcs):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    deps = [os.path.join(CSRC, s) for s in srcs]
+    deps += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    deps += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force=False, verbose=False):
+    built = []
+    for name, srcs in TARGETS.items():
+        if not all(os.path.exists(os.path.join(CSRC, s)) for s in srcs):
+            continue
+        out = os.path.join(PKG, name)
+        if not force and not _stale(out, srcs):
+            continue
+        cmd = [HIPCC, "--offload-arch=" + ARCH] + COMMON + ["-o", out] + [os.path.join(CSRC, s) for s in srcs]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        built.append(out)
+    return built
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

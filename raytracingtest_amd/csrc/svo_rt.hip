@@ -1,0 +1,380 @@
+// svo_rt.hip -- MI355X (gfx950) sparse-voxel-octree primary-ray caster.
+//
+// C-ABI plugin (include/svo_rt.h) replacing the reference's Unity host driver
+// RaytracingMaster.cs + the HLSL compute kernel RaytraceCompute.compute /
+// NVIDIASVO.compute / AttachmentLookup.compute (reference repo paths).
+//
+// Device data layout (DESIGN.md "Data layout in HBM"):
+//   nodes : uint2[N]  .x = valid8 << 8 | nonleaf8,  .y = absolute index of the
+//           first non-leaf child.  One 8-byte load per descriptor fetch.  The
+//           reference's 16-bit RELATIVE pointer (NaiveCreator.cs:164-165) is
+//           resolved to absolute at upload, so pools deeper than 16-bit
+//           pointers allow use the same kernel.
+//   att   : uint2[N]  .x = colorA565 | colorB565 << 16, .y = choices16 | normal16 << 16
+//           (NaiveCreator.cs:189-191), one 8-byte load per hit.
+//
+// Numerics: compiled with -ffp-contract=off and correctly rounded f32 div/sqrt
+// so every expression rounds exactly as the strict-IEEE oracle (oracle/).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "svo_rt.h"
+#include "svo_traverse.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess)                                                          \
+            return fail(SVO_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct Upload {
+    size_t offset, count;
+    int depth;
+    bool external;   // has child links outside its own range (sub-SVO linking)
+};
+
+}  // namespace
+
+struct svo_ctx {
+    int device = 0;
+    size_t capacity = 0;
+    size_t n_nodes = 0;
+    uint2 *d_nodes = nullptr;
+    uint2 *d_att = nullptr;
+    int32_t *d_stage = nullptr;   // staging for V1 descriptor conversion
+    size_t stage_cap = 0;
+    hipStream_t stream = nullptr;
+    svo::Camera cam{};
+    bool cam_set = false;
+    std::vector<Upload> uploads;
+    int depth = 0;
+    // host-path output scratch
+    void *d_out_hits = nullptr;
+    void *d_out_rgba = nullptr;
+    size_t out_cap_px = 0;
+};
+
+namespace {
+
+// V1 (relative, int32) -> device node (absolute, uint2).  NaiveCreator.cs:184-187.
+__global__ void convert_v1_kernel(const int32_t *__restrict__ desc, uint2 *__restrict__ nodes,
+                                  size_t n, uint32_t base) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t cd = (uint32_t)desc[i];
+    uint32_t self = base + (uint32_t)i;
+    uint2 o;
+    o.x = cd & 0xFFFFu;
+    o.y = cd ? self + (cd >> 16) : 0u;   // node == 0 <=> descriptor word == 0 (HLSL re-fetch test)
+    nodes[base + i] = o;
+}
+
+// Host-side level walk: validates every non-leaf child index and returns the
+// number of descriptor levels reachable from the upload's first node.
+int walk_depth(const uint32_t *lo, const uint32_t *first, size_t n, size_t base, size_t pool_n,
+               int *depth_out, bool *external_out, std::string *err) {
+    std::vector<uint8_t> seen(n, 0);
+    std::vector<uint32_t> cur{0}, nxt;
+    int depth = 0;
+    bool external = false;
+    if (n == 0) { *depth_out = 0; *external_out = false; return 0; }
+    seen[0] = 1;
+    while (!cur.empty()) {
+        ++depth;
+        if (depth > 22) { *err = "node pool deeper than 22 levels (s_max = 23)"; return -1; }
+        nxt.clear();
+        for (uint32_t li : cur) {
+            uint32_t m = lo[li] & 0xFFu;
+            uint32_t f = first[li];
+            int rank = 0;
+            for (int c = 0; c < 8; ++c) {
+                if (!((m >> c) & 1u)) continue;
+                uint64_t child = (uint64_t)f + (uint64_t)rank++;
+                if (child >= pool_n) {
+                    *err = "child pointer of node " + std::to_string(base + li) + " -> " +
+                           std::to_string(child) + " outside the pool (" + std::to_string(pool_n) + ")";
+                    return -1;
+                }
+                if (child < base || child >= base + n) { external = true; continue; }
+                uint32_t cl = (uint32_t)(child - base);
+                if (seen[cl]) continue;   // shared subtrees are legal; cycles are bounded by depth
+                seen[cl] = 1;
+                nxt.push_back(cl);
+            }
+        }
+        cur.swap(nxt);
+    }
+    *depth_out = depth;
+    *external_out = external;
+    return 0;
+}
+
+void recompute_depth(svo_ctx *ctx) {
+    int root_depth = 0, other = 0;
+    bool ext = false;
+    for (const Upload &u : ctx->uploads) {
+        if (u.offset == 0) root_depth = std::max(root_depth, u.depth);
+        else other = std::max(other, u.depth);
+        ext = ext || u.external;
+    }
+    ctx->depth = root_depth + (ext ? other : 0);
+    if (ctx->depth > 22) ctx->depth = 22;
+}
+
+int record_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, size_t n, size_t base) {
+    std::string err;
+    int depth = 0;
+    bool ext = false;
+    size_t pool_n = std::max(ctx->n_nodes, base + n);
+    if (walk_depth(lo, first, n, base, pool_n, &depth, &ext, &err) != 0) return fail(SVO_ERR_FORMAT, err);
+    ctx->uploads.erase(std::remove_if(ctx->uploads.begin(), ctx->uploads.end(),
+                                      [&](const Upload &u) { return u.offset == base; }),
+                       ctx->uploads.end());
+    ctx->uploads.push_back({base, n, depth, ext});
+    ctx->n_nodes = pool_n;
+    recompute_depth(ctx);
+    return SVO_OK;
+}
+
+int ensure_out(svo_ctx *ctx, size_t px) {
+    if (px <= ctx->out_cap_px) return SVO_OK;
+    if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
+    if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
+    ctx->d_out_hits = ctx->d_out_rgba = nullptr;
+    ctx->out_cap_px = 0;
+    HIP_TRY(hipMalloc(&ctx->d_out_hits, px * sizeof(svo_hit)));
+    HIP_TRY(hipMalloc(&ctx->d_out_rgba, px * 4 * sizeof(float)));
+    ctx->out_cap_px = px;
+    return SVO_OK;
+}
+
+int band_rows_local(int height, const svo_band &b) {
+    // rows y with (y / band_rows) % band_count == band_rank
+    int rows = 0;
+    for (int y0 = b.band_rank * b.band_rows; y0 < height; y0 += b.band_rows * b.band_count)
+        rows += std::min(b.band_rows, height - y0);
+    return rows;
+}
+
+int check_band(const svo_band *band, int height, svo_band *out) {
+    svo_band b = band ? *band : svo_band{1, 0, 1};
+    if (b.band_rows <= 0 || b.band_count <= 0 || b.band_rank < 0 || b.band_rank >= b.band_count)
+        return fail(SVO_ERR_ARG, "invalid svo_band");
+    if (b.band_count == 1) b.band_rows = height > 0 ? height : 1;
+    *out = b;
+    return SVO_OK;
+}
+
+int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band,
+           void *d_rgba, void *d_hits, uint32_t *d_fetch, hipStream_t stream) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
+    if (stack_mode != SVO_STACK_HLSL && stack_mode != SVO_STACK_EXACT)
+        return fail(SVO_ERR_ARG, "unknown stack mode");
+    if (ctx->n_nodes == 0) return fail(SVO_ERR_STATE, "no node pool uploaded (svo_set_buffer)");
+    if (!ctx->cam_set) return fail(SVO_ERR_STATE, "camera not set (svo_set_camera)");
+    svo_band b;
+    int rc = check_band(band, height, &b);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    svo::LaunchParams p;
+    p.nodes = ctx->d_nodes;
+    p.att = ctx->d_att;
+    p.cam = ctx->cam;
+    p.width = width;
+    p.height = height;
+    p.band_rows = b.band_rows;
+    p.band_rank = b.band_rank;
+    p.band_count = b.band_count;
+    p.local_rows = band_rows_local(height, b);
+    p.slots = std::max(ctx->depth - 1, 1);
+    p.hits = reinterpret_cast<svo::Hit *>(d_hits);
+    p.rgba = reinterpret_cast<float4 *>(d_rgba);
+    p.fetches = d_fetch;
+    if (p.local_rows == 0) return SVO_OK;
+    hipError_t e = svo::launch_render(p, stack_mode, stream ? stream : ctx->stream);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
+    return SVO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int svo_abi_version(void) { return 1; }
+
+const char *svo_last_error(void) { return g_last_error.c_str(); }
+
+int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
+    if (!out) return fail(SVO_ERR_ARG, "out is null");
+    *out = nullptr;
+    if (capacity_nodes == 0 || capacity_nodes > (size_t)0xFFFFFFFFu)
+        return fail(SVO_ERR_ARG, "capacity_nodes must be in [1, 2^32)");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(SVO_ERR_ARG, "device index out of range");
+    HIP_TRY(hipSetDevice(device));
+    svo_ctx *ctx = new (std::nothrow) svo_ctx();
+    if (!ctx) return fail(SVO_ERR_ARG, "out of host memory");
+    ctx->device = device;
+    ctx->capacity = capacity_nodes;
+    hipError_t e = hipMalloc(&ctx->d_nodes, capacity_nodes * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_att, capacity_nodes * sizeof(uint2));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        svo_destroy(ctx);
+        return fail(SVO_ERR_HIP, std::string("svo_create: ") + hipGetErrorString(e));
+    }
+    *out = ctx;
+    return SVO_OK;
+}
+
+int svo_set_buffer(svo_ctx *ctx, const int32_t *desc, size_t n_desc, const uint32_t *att,
+                   size_t n_att, size_t dst_offset) {
+    if (!ctx || (!desc && n_desc) || (!att && n_att)) return fail(SVO_ERR_ARG, "null argument");
+    if (dst_offset + n_desc > ctx->capacity || 2 * dst_offset + n_att > 2 * ctx->capacity)
+        return fail(SVO_ERR_CAPACITY, "upload exceeds node-pool capacity");
+    if (n_att != 2 * n_desc) return fail(SVO_ERR_ARG, "attachments must hold 2 words per descriptor");
+    if (n_desc == 0) return SVO_OK;
+    // host-side validation walk on the absolute view
+    std::vector<uint32_t> lo(n_desc), first(n_desc);
+    for (size_t i = 0; i < n_desc; ++i) {
+        uint32_t cd = (uint32_t)desc[i];
+        lo[i] = cd & 0xFFFFu;
+        first[i] = cd ? (uint32_t)(dst_offset + i) + (cd >> 16) : 0u;
+    }
+    int rc = record_upload(ctx, lo.data(), first.data(), n_desc, dst_offset);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (n_desc > ctx->stage_cap) {
+        if (ctx->d_stage) hipFree(ctx->d_stage);
+        ctx->d_stage = nullptr;
+        ctx->stage_cap = 0;
+        HIP_TRY(hipMalloc(&ctx->d_stage, n_desc * sizeof(int32_t)));
+        ctx->stage_cap = n_desc;
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->d_stage, desc, n_desc * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    unsigned blocks = (unsigned)((n_desc + 255) / 256);
+    hipLaunchKernelGGL(convert_v1_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ctx->d_stage,
+                       ctx->d_nodes, n_desc, (uint32_t)dst_offset);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(ctx->d_att + dst_offset, att, n_att * sizeof(uint32_t), hipMemcpyHostToDevice,
+                           ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return SVO_OK;
+}
+
+int svo_set_buffer_v2(svo_ctx *ctx, const uint64_t *nodes, size_t n_nodes, const uint32_t *att,
+                      size_t n_att, size_t dst_offset) {
+    if (!ctx || (!nodes && n_nodes) || (!att && n_att)) return fail(SVO_ERR_ARG, "null argument");
+    if (dst_offset + n_nodes > ctx->capacity) return fail(SVO_ERR_CAPACITY, "upload exceeds node-pool capacity");
+    if (n_att != 2 * n_nodes) return fail(SVO_ERR_ARG, "attachments must hold 2 words per node");
+    if (n_nodes == 0) return SVO_OK;
+    std::vector<uint32_t> lo(n_nodes), first(n_nodes);
+    for (size_t i = 0; i < n_nodes; ++i) {
+        lo[i] = (uint32_t)nodes[i];
+        first[i] = (uint32_t)(nodes[i] >> 32);
+        if (lo[i] > 0xFFFFu) return fail(SVO_ERR_FORMAT, "v2 node low word must only hold the two masks");
+    }
+    int rc = record_upload(ctx, lo.data(), first.data(), n_nodes, dst_offset);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    static_assert(sizeof(uint2) == sizeof(uint64_t), "node layout");
+    HIP_TRY(hipMemcpyAsync(ctx->d_nodes + dst_offset, nodes, n_nodes * sizeof(uint64_t), hipMemcpyHostToDevice,
+                           ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->d_att + dst_offset, att, n_att * sizeof(uint32_t), hipMemcpyHostToDevice,
+                           ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return SVO_OK;
+}
+
+int svo_set_camera(svo_ctx *ctx, const float c2w[16], const float inv_proj[16], float px_off_x,
+                   float px_off_y, const float light[4]) {
+    if (!ctx || !c2w || !inv_proj || !light) return fail(SVO_ERR_ARG, "null argument");
+    std::memcpy(ctx->cam.c2w, c2w, sizeof(ctx->cam.c2w));
+    std::memcpy(ctx->cam.inv_proj, inv_proj, sizeof(ctx->cam.inv_proj));
+    ctx->cam.px_off[0] = px_off_x;
+    ctx->cam.px_off[1] = px_off_y;
+    std::memcpy(ctx->cam.light, light, sizeof(ctx->cam.light));
+    ctx->cam_set = true;
+    return SVO_OK;
+}
+
+int svo_render(svo_ctx *ctx, int width, int height, int stack_mode, float *rgba_out, svo_hit *hits_out) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
+    size_t px = (size_t)width * (size_t)height;
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc = ensure_out(ctx, px);
+    if (rc) return rc;
+    rc = launch(ctx, width, height, stack_mode, nullptr, rgba_out ? ctx->d_out_rgba : nullptr,
+                hits_out ? ctx->d_out_hits : nullptr, nullptr, ctx->stream);
+    if (rc) return rc;
+    if (hits_out)
+        HIP_TRY(hipMemcpyAsync(hits_out, ctx->d_out_hits, px * sizeof(svo_hit), hipMemcpyDeviceToHost, ctx->stream));
+    if (rgba_out)
+        HIP_TRY(hipMemcpyAsync(rgba_out, ctx->d_out_rgba, px * 4 * sizeof(float), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return SVO_OK;
+}
+
+int svo_render_device(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band, void *d_rgba,
+                      void *d_hits, void *stream) {
+    return launch(ctx, width, height, stack_mode, band, d_rgba, d_hits, nullptr,
+                  reinterpret_cast<hipStream_t>(stream));
+}
+
+int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band,
+                      void *d_fetches, void *stream) {
+    if (!d_fetches) return fail(SVO_ERR_ARG, "d_fetches is null");
+    return launch(ctx, width, height, stack_mode, band, nullptr, nullptr,
+                  reinterpret_cast<uint32_t *>(d_fetches), reinterpret_cast<hipStream_t>(stream));
+}
+
+int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (n_nodes) *n_nodes = ctx->n_nodes;
+    if (max_depth) *max_depth = ctx->depth;
+    if (device) *device = ctx->device;
+    return SVO_OK;
+}
+
+int svo_synchronize(svo_ctx *ctx) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return SVO_OK;
+}
+
+int svo_destroy(svo_ctx *ctx) {
+    if (!ctx) return SVO_OK;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->d_nodes) hipFree(ctx->d_nodes);
+    if (ctx->d_att) hipFree(ctx->d_att);
+    if (ctx->d_stage) hipFree(ctx->d_stage);
+    if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
+    if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return SVO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,52 @@
+// svo_traverse.h -- per-pixel SVO primary-ray kernel for gfx950 (wave64).
+//
+// Restates, for the GPU, Assets/Shaders/RaytraceCompute.compute:143-168
+// (CSMain), :129-141 (CreateCameraRay), :93-127 (Shade) and
+// Assets/Shaders/NVIDIASVO.compute:12-198 (IntersectSVO, Laine & Karras 2010)
+// of the reference.  Not a transcription of the HLSL dispatch: one wave64
+// covers an 8x8 pixel tile, the traversal stack lives in LDS laid out
+// [slot][lane] (conflict-free ds_read_b64 / ds_write_b64), a node fetch is one
+// 8-byte load, and never-written stack entries read as zero through a
+// per-lane written-slot bit mask instead of a per-ray LDS clear.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace svo {
+
+constexpr int S_MAX = 23;          // NVIDIASVO.compute:2
+constexpr int MAX_ITERS = 65536;   // safety net, identical in oracle/svo_oracle.c
+constexpr int BLOCK = 256;         // 4 waves, 16x16 pixels
+
+struct Camera {
+    float c2w[16];        // Unity Matrix4x4, column-major
+    float inv_proj[16];
+    float px_off[2];
+    float light[4];
+};
+
+struct Hit {              // == svo_hit
+    uint32_t parent;
+    uint8_t hit_idx;
+    uint8_t hit_scale;
+    uint16_t flags;
+    float t;
+    float nx, ny, nz;
+};
+static_assert(sizeof(Hit) == 24, "hit record layout");
+
+struct LaunchParams {
+    const uint2 *nodes;
+    const uint2 *att;
+    Camera cam;
+    int width, height;
+    int band_rows, band_rank, band_count, local_rows;
+    int slots;            // stack slots = depth - 1 (scales [23 - slots, 22])
+    Hit *hits;            // nullable
+    float4 *rgba;         // nullable
+    uint32_t *fetches;    // nullable (instrumented launch)
+};
+
+hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream);
+
+}  // namespace svo

@@ -1,0 +1,138 @@
+"""Host-side mirror of the reference's `RaytracingMaster` MonoBehaviour
+(Assets/Scripts/SVO/GPU/RaytracingMaster.cs) over the C-ABI of libsvo_rt.so.
+
+Same names and argument meaning as the reference:
+  InitializeSVOBuffer()          RaytracingMaster.cs:111-116
+  SetSVOBuffer(data, offset=0)   RaytracingMaster.cs:118-135 (public overload)
+  SetSVOBuffer()                 RaytracingMaster.cs:90-109  (rebuild from maxLevel / sampleType)
+  UpdateShaderParameters(...)    RaytracingMaster.cs:32-41
+  Render(width, height)          RaytracingMaster.cs:60-74   (Dispatch + result)
+Errors surface as SvoError (the C-ABI status + svo_last_error text) instead of
+Unity's silent shader failures.  There is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import HIT_DTYPE, STACK_EXACT, STACK_HLSL, SvoBand, SvoError, check
+from .camera import column_major, main_camera, main_light
+from .svo_data import SVOData
+
+# RaytracingMaster.cs:113-115: "one gibibyte of memory" / 8 elements of 4 bytes
+REFERENCE_CAPACITY = 1073741824 // 8
+
+
+class RaytracingMaster:
+    def __init__(self, device=0, capacity_nodes=REFERENCE_CAPACITY, maxLevel=5, sampleType=4):
+        self.device = device
+        self.capacity_nodes = int(capacity_nodes)
+        self.maxLevel = maxLevel        # [Range(1, 8)] in the reference (:16-17)
+        self.sampleType = sampleType    # SampleFunctions.Type.Custom1 = 4 (:18)
+        self._ctx = ctypes.c_void_p()
+        self._camera_set = False
+        self.InitializeSVOBuffer()
+
+    # ------------------------------------------------------------------ setup
+    def InitializeSVOBuffer(self):
+        L = _lib.lib()
+        if self._ctx:
+            L.svo_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+        check(L.svo_create(self.device, self.capacity_nodes, ctypes.byref(self._ctx)), "svo_create")
+
+    def SetSVOBuffer(self, data=None, offset=0):
+        """Upload an SVOData at descriptor `offset`; with no data, build one from
+        (sampleType, maxLevel) like the private reference overload."""
+        if data is None:
+            from .builder import build_svo_for_sampler
+            data = build_svo_for_sampler(self.sampleType, self.maxLevel)
+        if not isinstance(data, SVOData):
+            raise TypeError("SetSVOBuffer expects an SVOData")
+        L = _lib.lib()
+        att = np.ascontiguousarray(data.attachments, np.uint32)
+        if data.format == 1:
+            desc = np.ascontiguousarray(data.childDescriptors, np.int32)
+            check(L.svo_set_buffer(self._ctx, desc.ctypes.data, len(desc), att.ctypes.data, len(att), int(offset)),
+                  "svo_set_buffer")
+        else:
+            nodes = np.ascontiguousarray(data.nodes, np.uint64)
+            check(L.svo_set_buffer_v2(self._ctx, nodes.ctypes.data, len(nodes), att.ctypes.data, len(att),
+                                      int(offset)), "svo_set_buffer_v2")
+        return data
+
+    def UpdateShaderParameters(self, camera=None, width=1920, height=1080, pixel_offset=(0.5, 0.5), light=None):
+        """camera: raytracingtest_amd.camera.Camera, or a (c2w, inv_proj) pair of 4x4 arrays."""
+        camera = main_camera() if camera is None else camera
+        if isinstance(camera, tuple):
+            c2w, inv_proj = camera
+        else:
+            c2w, inv_proj = camera.uniforms(width, height)
+        light = main_light() if light is None else np.asarray(light, np.float32)
+        c = column_major(c2w)
+        p = column_major(inv_proj)
+        lt = np.ascontiguousarray(light, np.float32)
+        check(_lib.lib().svo_set_camera(self._ctx, c.ctypes.data, p.ctypes.data, float(pixel_offset[0]),
+                                        float(pixel_offset[1]), lt.ctypes.data), "svo_set_camera")
+        self._camera_set = True
+
+    # ----------------------------------------------------------------- render
+    def Render(self, width, height, stack_mode=STACK_HLSL, want_rgba=True, want_hits=True):
+        """Blocking render into host arrays: (rgba[H, W, 4] float32, hits[H, W] svo_hit)."""
+        rgba = np.zeros((height, width, 4), np.float32) if want_rgba else None
+        hits = np.zeros((height, width), HIT_DTYPE) if want_hits else None
+        check(_lib.lib().svo_render(self._ctx, width, height, stack_mode,
+                                    None if rgba is None else rgba.ctypes.data,
+                                    None if hits is None else hits.ctypes.data), "svo_render")
+        return rgba, hits
+
+    def render_device(self, width, height, rgba_ptr=None, hits_ptr=None, stack_mode=STACK_HLSL,
+                      band=None, stream=None):
+        """Asynchronous render into device buffers (raw device pointers, e.g. torch
+        tensor.data_ptr()), optionally only this rank's row bands."""
+        b = None if band is None else ctypes.byref(SvoBand(*band))
+        check(_lib.lib().svo_render_device(self._ctx, width, height, stack_mode, b, rgba_ptr, hits_ptr, stream),
+              "svo_render_device")
+
+    def count_fetches_device(self, width, height, fetch_ptr, stack_mode=STACK_HLSL, band=None, stream=None):
+        b = None if band is None else ctypes.byref(SvoBand(*band))
+        check(_lib.lib().svo_count_fetches(self._ctx, width, height, stack_mode, b, fetch_ptr, stream),
+              "svo_count_fetches")
+
+    def synchronize(self):
+        check(_lib.lib().svo_synchronize(self._ctx), "svo_synchronize")
+
+    def info(self):
+        n = ctypes.c_size_t()
+        d = ctypes.c_int()
+        dev = ctypes.c_int()
+        check(_lib.lib().svo_get_info(self._ctx, ctypes.byref(n), ctypes.byref(d), ctypes.byref(dev)),
+              "svo_get_info")
+        return {"n_nodes": n.value, "depth": d.value, "device": dev.value}
+
+    def close(self):
+        if self._ctx:
+            _lib.lib().svo_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def band_rows(height, band):
+    """Global row indices owned by `band` = (band_rows, band_rank, band_count), in order."""
+    rows, rank, count = band
+    ys = np.arange(height)
+    return ys[(ys // rows) % count == rank]
+
+
+__all__ = ["RaytracingMaster", "SVOData", "SvoError", "STACK_HLSL", "STACK_EXACT", "HIT_DTYPE", "band_rows"]

@@ -1,0 +1,80 @@
+"""C-ABI boundary checks that need no GPU: the library builds, loads and exports
+every symbol include/svo_rt.h declares; the header's record layout matches."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "svo_rt.h")
+
+
+@pytest.fixture(scope="module")
+def native():
+    from raytracingtest_amd import build
+    build.build()
+    from raytracingtest_amd import _lib
+    return _lib.lib()
+
+
+def declared_functions(path):
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(svo_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_exports_every_declared_symbol(native):
+    names = declared_functions(HEADER)
+    assert len(names) >= 12
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "raytracingtest_amd", "libsvo_rt.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (svo_\w+)", out))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    from raytracingtest_amd._lib import EXPORTS
+    assert set(EXPORTS) == set(names)
+
+
+def test_abi_version_and_error_text(native):
+    assert native.svo_abi_version() == 1
+    assert isinstance(native.svo_last_error(), bytes)
+
+
+def test_null_arguments_rejected_without_gpu(native):
+    assert native.svo_create(0, 16, None) == -1        # SVO_ERR_ARG, no device touched
+    assert b"null" in native.svo_last_error()
+    assert native.svo_render(None, 8, 8, 0, None, None) == -1
+    assert native.svo_destroy(None) == 0
+
+
+def test_header_layout_compiles_in_c(tmp_path):
+    src = tmp_path / "t.c"
+    src.write_text('#include "svo_rt.h"\n#include <stddef.h>\n'
+                   '_Static_assert(sizeof(svo_hit) == 24, "hit");\n'
+                   '_Static_assert(offsetof(svo_hit, t) == 8, "t");\n'
+                   '_Static_assert(offsetof(svo_hit, nz) == 20, "nz");\n'
+                   '_Static_assert(sizeof(svo_band) == 12, "band");\n'
+                   'int main(void){return 0;}\n')
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
+                    "-o", str(tmp_path / "t")], check=True)
+
+
+def test_hit_dtype_matches_header():
+    from raytracingtest_amd import HIT_DTYPE
+    assert HIT_DTYPE.itemsize == 24
+    assert HIT_DTYPE.fields["t"][1] == 8 and HIT_DTYPE.fields["nz"][1] == 20
+
+
+def test_product_has_no_oracle_dependency():
+    """The shipped package must never import or link the oracle."""
+    pkg = os.path.join(ROOT, "raytracingtest_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                text = open(os.path.join(dirpath, f)).read()
+                for pat in (r"^\s*(from|import)\s+oracle", r"liborcsvo", r"\borc_\w+\(", r"svo_oracle\.h"):
+                    assert not re.search(pat, text, flags=re.M), (f, pat)

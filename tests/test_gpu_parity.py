@@ -1,0 +1,192 @@
+"""GPU parity: the HIP path through the C-ABI vs the CPU oracle, same inputs.
+
+Bar (BASELINE.json north_star): hit voxel (parent, hit_idx, hit_scale, flags)
+bit-exact; t and normal within 1e-5 relative -- asserted bit-exact here since
+kernel and oracle share the strict-IEEE op order; RGBA of hit pixels within
+rtol 1e-5 (miss colour is the procedural sky stand-in, also compared)."""
+import numpy as np
+import pytest
+
+from raytracingtest_amd import RaytracingMaster, SVOData, SvoError, band_rows
+from raytracingtest_amd.builder import build_from_leaves, build_menger
+from raytracingtest_amd.camera import Camera, look_rotation, main_camera, main_light, overview_camera
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def rm():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    m = RaytracingMaster(device=0, capacity_nodes=1 << 22)
+    yield m
+    m.close()
+
+
+def _oracle_render(oracle_mod, svo, camera, w, h, mode=0, off=(0.5, 0.5), nodes=False):
+    c2w, inv_proj = camera.uniforms(w, h)
+    cam = oracle_mod.make_camera(c2w, inv_proj, off, main_light())
+    if nodes or svo.format == 2:
+        osvo = oracle_mod.OracleSVO(nodes=svo.to_v2(), attachments=svo.attachments)
+    else:
+        osvo = oracle_mod.OracleSVO(svo.childDescriptors, svo.attachments)
+    return oracle_mod.render(osvo, cam, w, h, mode)
+
+
+def _compare(got_hits, got_rgba, ref_hits, ref_rgba):
+    g = got_hits.reshape(-1)
+    for f in ("parent", "hit_idx", "hit_scale", "flags"):
+        bad = np.flatnonzero(g[f] != ref_hits[f])
+        assert len(bad) == 0, f"{f} differs at {len(bad)} pixels, first {bad[:5]}"
+    for f in ("t", "nx", "ny", "nz"):
+        a = g[f].astype(np.float64)
+        b = ref_hits[f].astype(np.float64)
+        fin = np.isfinite(b)
+        assert np.array_equal(np.isfinite(a), fin)
+        np.testing.assert_allclose(a[fin], b[fin], rtol=RTOL, atol=0)
+    assert g.tobytes() == ref_hits.tobytes(), "hit records not bit-identical"
+    if got_rgba is not None:
+        np.testing.assert_allclose(got_rgba.reshape(-1, 4), ref_rgba, rtol=RTOL, atol=1e-7)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("camera_name", ["main", "overview"])
+def test_text_fixture_parity(rm, oracle_mod, text_svo, mode, camera_name):
+    cam = main_camera() if camera_name == "main" else overview_camera()
+    w, h = 256, 256   # config C1
+    rm.SetSVOBuffer(text_svo)
+    rm.UpdateShaderParameters(cam, w, h)
+    rgba, hits = rm.Render(w, h, stack_mode=mode)
+    ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, text_svo, cam, w, h, mode)
+    assert np.count_nonzero(ref_hits["flags"] & 1) > 1000
+    _compare(hits, rgba, ref_hits, ref_rgba)
+
+
+def test_v1_and_v2_uploads_identical(rm, text_svo):
+    cam = overview_camera()
+    rm.SetSVOBuffer(text_svo)
+    rm.UpdateShaderParameters(cam, 320, 200)
+    r1, h1 = rm.Render(320, 200)
+    rm.SetSVOBuffer(text_svo.as_v2())
+    r2, h2 = rm.Render(320, 200)
+    assert h1.tobytes() == h2.tobytes() and r1.tobytes() == r2.tobytes()
+
+
+def test_full_hd_text_fixture(rm, oracle_mod, text_svo):
+    cam = overview_camera()
+    w, h = 1920, 1080
+    rm.SetSVOBuffer(text_svo)
+    rm.UpdateShaderParameters(cam, w, h)
+    rgba, hits = rm.Render(w, h)
+    ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, text_svo, cam, w, h)
+    _compare(hits, rgba, ref_hits, ref_rgba)
+
+
+def test_menger_depth8_parity_and_fetch_counts(rm, oracle_mod):
+    torch = pytest.importorskip("torch")
+    svo = build_menger(8)
+    assert svo.format == 2   # relative pointers overflow 16 bits at 256^3
+    cam = overview_camera()
+    w, h = 480, 270
+    rm.SetSVOBuffer(svo)
+    rm.UpdateShaderParameters(cam, w, h)
+    rgba, hits = rm.Render(w, h)
+    ref_hits, ref_rgba, ref_fetch = _oracle_render(oracle_mod, svo, cam, w, h)
+    _compare(hits, rgba, ref_hits, ref_rgba)
+    fetch = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+    rm.count_fetches_device(w, h, fetch.data_ptr())
+    rm.synchronize()
+    assert np.array_equal(fetch.cpu().numpy().view(np.uint32), ref_fetch)
+
+
+def test_band_split_reassembles_frame(rm, text_svo):
+    torch = pytest.importorskip("torch")
+    cam = overview_camera()
+    w, h = 200, 150
+    rm.SetSVOBuffer(text_svo)
+    rm.UpdateShaderParameters(cam, w, h)
+    _, full = rm.Render(w, h)
+    out = np.zeros((h, w), full.dtype)
+    for rank in range(3):
+        band = (8, rank, 3)
+        ys = band_rows(h, band)
+        buf = torch.zeros(len(ys) * w * 24, dtype=torch.uint8, device="cuda")
+        rm.render_device(w, h, hits_ptr=buf.data_ptr(), band=band)
+        rm.synchronize()
+        out[ys] = buf.cpu().numpy().view(full.dtype).reshape(len(ys), w)
+    assert out.tobytes() == full.tobytes()
+
+
+def test_jittered_pixel_offset_parity(rm, oracle_mod, text_svo):
+    from raytracingtest_amd.camera import jitter_offsets
+    cam = main_camera()
+    w, h = 128, 96
+    rm.SetSVOBuffer(text_svo)
+    for off in jitter_offsets(3):
+        rm.UpdateShaderParameters(cam, w, h, pixel_offset=tuple(off))
+        rgba, hits = rm.Render(w, h)
+        ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, text_svo, cam, w, h, off=tuple(off))
+        _compare(hits, rgba, ref_hits, ref_rgba)
+
+
+def test_random_trees_parity(rm, oracle_mod):
+    rng = np.random.default_rng(7)
+    for depth, n in ((3, 30), (7, 4000), (9, 60000)):
+        xyz = np.unique(rng.integers(0, 1 << depth, (n, 3)), axis=0)
+        nrm = rng.normal(size=(len(xyz), 3)).astype(np.float32)
+        svo = build_from_leaves(depth, xyz, nrm)
+        eye = rng.uniform(-30, 30, 3)
+        cam = Camera(position=tuple(eye), rotation=look_rotation(-eye + rng.uniform(-5, 5, 3)))
+        w, h = 160, 120
+        rm.SetSVOBuffer(svo)
+        rm.UpdateShaderParameters(cam, w, h)
+        for mode in (0, 1):
+            rgba, hits = rm.Render(w, h, stack_mode=mode)
+            ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, svo, cam, w, h, mode)
+            _compare(hits, rgba, ref_hits, ref_rgba)
+
+
+def test_camera_inside_solid_and_axis_aligned(rm, oracle_mod, text_svo):
+    # camera looking exactly down an axis: zero direction components on the centre row/column
+    cam = Camera(position=(0.0, 0.0, -40.0), rotation=np.eye(3))
+    w, h = 65, 65   # odd size: the centre pixel ray is exactly +z
+    rm.SetSVOBuffer(text_svo)
+    rm.UpdateShaderParameters(cam, w, h)
+    rgba, hits = rm.Render(w, h)
+    ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, text_svo, cam, w, h)
+    _compare(hits, rgba, ref_hits, ref_rgba)
+
+
+def test_sub_svo_offset_upload(rm, oracle_mod, text_svo):
+    """SetSVOBuffer(data, offset) (RaytracingMaster.cs:118-135): a second pool at a
+    descriptor offset; attachments land at 2*offset (documented deviation)."""
+    cam = overview_camera()
+    w, h = 96, 96
+    m = RaytracingMaster(device=0, capacity_nodes=1 << 16)
+    try:
+        m.SetSVOBuffer(text_svo, offset=0)
+        m.SetSVOBuffer(text_svo, offset=10000)
+        m.UpdateShaderParameters(cam, w, h)
+        rgba, hits = m.Render(w, h)
+        ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, text_svo, cam, w, h)
+        _compare(hits, rgba, ref_hits, ref_rgba)
+        assert m.info()["n_nodes"] == 10000 + len(text_svo)
+    finally:
+        m.close()
+
+
+def test_errors_are_loud(rm):
+    m = RaytracingMaster(device=0, capacity_nodes=64)
+    try:
+        with pytest.raises(SvoError):
+            m.Render(8, 8)                       # no pool uploaded
+        bad = SVOData(childDescriptors=np.array([(5 << 16) | 0x0101], np.int32))
+        with pytest.raises(SvoError):
+            m.SetSVOBuffer(bad)                  # child pointer outside the pool
+        with pytest.raises(SvoError):
+            m.SetSVOBuffer(build_from_leaves(4, np.argwhere(np.ones((16, 16, 16))), np.ones((4096, 3), np.float32)))
+    finally:
+        m.close()
