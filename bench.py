@@ -1,0 +1,240 @@
+"""Benchmark: SVO primary-ray throughput on MI355X (BASELINE.json metric
+"Mrays/sec + achieved HBM GB/s, 1920x1080 primary rays, depth-10 SVO").
+
+Workload (config C3 of BASELINE.json): a depth-10 (1024^3)
+SVO built from the reference's Custom1 OpenSimplex terrain sampler
+(SampleFunctions.cs:40-47, seed 7) by the native NaiveCreator restatement,
+1920x1080 primary rays from the 'overview' camera, Main.unity intrinsics and
+light.  A step = one CSMain-equivalent pass: every pixel's camera ray,
+IntersectSVO, hit decode, Shade, RGBA + 24-byte hit record written to HBM.
+Inputs (node pool, camera) are resident before the timed region.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one rank per
+GPU, SVO replicated per GPU, each rank traces one full 1920x1080 jittered
+sample per step (_PixelOffset from a seeded sequence, RaytracingMaster.cs:35):
+weak scaling, no data-path collective in the step.  `--split bands` instead
+splits ONE frame into 8-row bands across ranks and gathers the hit records to
+rank 0 over RCCL every step (strong scaling).
+
+roofline: algorithmic bytes per launch = sum over rays of
+  8 * F (8-byte node fetches) + 8 * [hit] (attachment) + 24 (hit record) + 16 (RGBA)
+with F counted per ray by the instrumented kernel; divided by the average
+kernel duration from HIP events on the launch stream.  peak = 8 TB/s HBM.
+cpu_baseline: the strict-IEEE C oracle (oracle/, "port") on the host cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+METRIC = "Mrays/sec + achieved HBM GB/s, 1920x1080 primary rays, depth-10 SVO"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--max-level", type=int, default=11, help="NaiveCreator maxLevel (depth + 1)")
+    p.add_argument("--sampler", type=int, default=4, help="SampleFunctions.Type (4 = Custom1)")
+    p.add_argument("--stack-mode", type=int, default=0, help="0 = HLSL float2 stack, 1 = exact")
+    p.add_argument("--split", choices=["samples", "bands"], default="samples")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline time budget (0 = skip)")
+    p.add_argument("--no-rgba", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from raytracingtest_amd import RaytracingMaster, band_rows
+    from raytracingtest_amd.camera import jitter_offsets, main_light, overview_camera
+    from raytracingtest_amd.native_builder import build_sampler_svo
+
+    W, H = args.width, args.height
+    t0 = time.time()
+    svo = build_sampler_svo(args.sampler, args.max_level, device=dev.index)
+    build_s = time.time() - t0
+    n_nodes = len(svo)
+
+    rm = RaytracingMaster(device=dev.index, capacity_nodes=n_nodes)
+    rm.SetSVOBuffer(svo)
+    cam = overview_camera()
+    if args.split == "samples":
+        off = (0.5, 0.5) if rank == 0 else tuple(float(v) for v in jitter_offsets(world)[rank])
+        band = None
+        rows = H
+    else:
+        off = (0.5, 0.5)
+        band = (8, rank, world)
+        rows = len(band_rows(H, band))
+    rm.UpdateShaderParameters(cam, W, H, pixel_offset=off)
+
+    n_px = W * rows
+    hits = torch.empty(n_px * 24, dtype=torch.uint8, device=dev)
+    rgba = None if args.no_rgba else torch.empty(n_px * 4, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    gathered = None
+    if args.split == "bands" and world > 1:
+        per = max(len(band_rows(H, (8, r, world))) for r in range(world)) * W * 24
+        gathered = [torch.empty(per, dtype=torch.uint8, device=dev) for _ in range(world)]
+        sendbuf = torch.zeros(per, dtype=torch.uint8, device=dev)
+
+    def step():
+        rm.render_device(W, H, rgba_ptr=None if rgba is None else rgba.data_ptr(), hits_ptr=hits.data_ptr(),
+                         stack_mode=args.stack_mode, band=band, stream=sptr)
+        if gathered is not None:
+            sendbuf[:hits.numel()].copy_(hits)
+            dist.all_gather(gathered, sendbuf)
+
+    # instrumented pass (outside the timed region): per-ray fetch counts
+    fetch = torch.zeros(n_px, dtype=torch.int32, device=dev)
+    rm.count_fetches_device(W, H, fetch.data_ptr(), stack_mode=args.stack_mode, band=band, stream=sptr)
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize(dev)
+    host_hits = hits.cpu().numpy().view(np.dtype([("parent", "<u4"), ("hit_idx", "u1"), ("hit_scale", "u1"),
+                                                  ("flags", "<u2"), ("t", "<f4"), ("nx", "<f4"), ("ny", "<f4"),
+                                                  ("nz", "<f4")]))
+    n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
+    F = int(fetch.to(torch.int64).sum().item())
+    bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if rgba is None else 16 * n_px)
+
+    # timed region: K steps between barrier + synchronize, kernel time by HIP events
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        kern_ms_max = kern_ms
+
+    rays_per_step = n_px * world
+    ms_per_step = elapsed / args.steps * 1e3
+    mrays = rays_per_step / (ms_per_step * 1e-3) / 1e6
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        cpu = cpu_baseline(args, svo, cam, off, host_hits) if (world == 1 and args.cpu_seconds > 0) else None
+        traffic = pmc_traffic()
+        out = {
+            "metric": METRIC,
+            "value": round(mrays, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if args.split == "samples" else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement",
+            "config": {"workload": f"C3 depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) Custom1 SVO, "
+                                   f"{W}x{H} primary rays, overview camera",
+                       "svo_nodes": n_nodes, "svo_format": "V%d" % svo.format, "svo_leaves": getattr(svo, "n_leaves", None),
+                       "build_s": round(build_s, 2), "stack_mode": "hlsl" if args.stack_mode == 0 else "exact",
+                       "rays_per_gpu_step": n_px, "hit_fraction": round(n_hit / n_px, 4),
+                       "fetches_per_ray": round(F / n_px, 3), "parallelism": f"{args.split}{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic,
+                         "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "bytes_formula": "8*F + 8*hits + 24*rays + 16*rays(rgba)"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    rm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def pmc_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
+    workload (profiles/pmc_summary.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(args, svo, cam, off, gpu_hits):
+    """Oracle ("port") on the host cores over the same frame, bounded by
+    --cpu-seconds; also spot-checks the GPU hit records against it."""
+    from oracle import oracle as orc
+    from raytracingtest_amd.camera import main_light
+
+    W, H = args.width, args.height
+    threads = min(16, os.cpu_count() or 1)
+    c2w, inv_proj = cam.uniforms(W, H)
+    ocam = orc.make_camera(c2w, inv_proj, off, main_light())
+    osvo = orc.OracleSVO(nodes=svo.to_v2(), attachments=svo.attachments)
+    # sample: whole rows spread over the frame, grown until the time budget is used
+    rows_total, rays, secs = 0, 0, 0.0
+    mism = 0
+    step = 8
+    t_begin = time.perf_counter()
+    y = 0
+    while time.perf_counter() - t_begin < args.cpu_seconds and rows_total < H:
+        y0 = (y * step) % H + (y * step) // H
+        t = time.perf_counter()
+        hits, _, _ = orc.render(osvo, ocam, W, H, args.stack_mode, y0=y0, y1=y0 + 1, nthreads=threads,
+                                want_rgba=True, want_fetches=False)
+        secs += time.perf_counter() - t
+        rays += W
+        rows_total += 1
+        g = gpu_hits[y0 * W:(y0 + 1) * W]
+        mism += int(g.tobytes() != hits.tobytes())
+        y += 1
+    # single-thread figure on a short sample
+    t = time.perf_counter()
+    orc.render(osvo, ocam, W, H, args.stack_mode, y0=H // 2, y1=H // 2 + 4, nthreads=1, want_fetches=False)
+    one_core = 4 * W / (time.perf_counter() - t) / 1e6
+    return {"value": round(rays / secs / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{rows_total} full rows ({rays} rays) of the same 1920x1080 frame, {threads} threads; "
+                      f"1-thread: {one_core:.3f} Mrays/s",
+            "one_core_mrays": round(one_core, 4),
+            "parity_rows_checked": rows_total, "parity_rows_mismatched": mism}
+
+
+if __name__ == "__main__":
+    main()

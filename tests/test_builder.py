@@ -1,0 +1,149 @@
+"""Builder row: NaiveCreator restatement.
+
+Pinned by: the reference's Text dump (the CompressSVOAux layout reproduces its
+4,977-descriptor topology exactly) and the digest of the reference's 3D
+OpenSimplex lookup table.  The GPU leaf classification is checked against the
+same sampler evaluated on the host."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from raytracingtest_amd import native_builder as nb
+from raytracingtest_amd.builder import (build_from_leaves, build_menger, encode_raw_normal16, menger_solid,
+                                        surface_leaves)
+from tests.conftest import GOLDEN
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from raytracingtest_amd import build
+    build.build()
+
+
+def test_opensimplex_table_matches_reference_digest():
+    ref = json.load(open(os.path.join(GOLDEN, "opensimplex3d_table.json")))
+    digest, n = nb.table_digest(nb.opensimplex_table())
+    assert n == ref["n_hashes"] == 72
+    assert digest == ref["sha256"]
+
+
+def test_layout_reproduces_text_dump_topology(text_svo):
+    leaves = text_svo.leaf_voxels()
+    nrm = np.tile(np.float32([0, 1, 0]), (len(leaves), 1))
+    ref_lo, ref_first = text_svo.masks_and_first()
+    for svo in (build_from_leaves(6, leaves[:, 3:6], nrm), nb.build_from_leaves(6, leaves[:, 3:6], nrm)):
+        lo, first = svo.masks_and_first()
+        assert len(svo) == 4977
+        assert np.array_equal(lo, ref_lo)
+        has = (lo & 0xFF) != 0
+        assert np.array_equal(first[has], ref_first[has])
+
+
+@pytest.mark.parametrize("depth,n", [(1, 3), (3, 60), (5, 2000), (7, 20000), (9, 60000)])
+def test_native_and_numpy_builders_identical(depth, n):
+    rng = np.random.default_rng(depth)
+    xyz = np.unique(rng.integers(0, 1 << depth, (n, 3)), axis=0)
+    nrm = rng.normal(size=(len(xyz), 3)).astype(np.float32)
+    a = build_from_leaves(depth, xyz, nrm)
+    b = nb.build_from_leaves(depth, xyz, nrm)
+    assert a.format == b.format
+    assert np.array_equal(a.to_v2(), b.to_v2())
+    assert np.array_equal(a.attachments, b.attachments)
+    assert a.depth() == depth
+
+
+def test_empty_and_single_leaf():
+    e = nb.build_from_leaves(4, np.zeros((0, 3), np.uint32), np.zeros((0, 3), np.float32))
+    assert len(e) == 1 and e.childDescriptors[0] == 0
+    one = nb.build_from_leaves(3, [[1, 2, 3]], [[0, 0, 1]])
+    assert one.depth() == 3 and len(one) == 3
+
+
+def test_menger_depth8_needs_wide_pointers():
+    svo = build_menger(8)
+    assert svo.format == 2 and svo.max_relative_pointer() > 0xFFFF
+    assert svo.depth() == 8
+
+
+def test_normal_code_roundtrip(oracle_mod):
+    rng = np.random.default_rng(5)
+    v = rng.normal(size=(500, 3)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    codes = encode_raw_normal16(v)
+    for n, c in zip(v, codes):
+        d = oracle_mod.decode_normal(int(c)).astype(np.float64)
+        d /= np.linalg.norm(d)
+        assert np.dot(d, n) > 0.95
+
+
+def test_samplers_on_host():
+    rng = np.random.default_rng(0)
+    p = rng.uniform(1, 2, (20000, 3)).astype(np.float32)
+    s = nb.eval_sampler(nb.SIMPLEX, p)
+    assert np.all(np.abs(s) <= 1.0) and np.std(s) > 0.05
+    c = nb.eval_sampler(nb.CUSTOM1, p)
+    np.testing.assert_array_equal(c, nb.eval_sampler(nb.CUSTOM1, p))   # deterministic
+    assert np.all(np.abs(c - (p[:, 1] - 1.5)) <= 0.65 + 1e-6)
+    np.testing.assert_array_equal(nb.eval_sampler(nb.FLAT_GROUND, p), np.float32(0.5) - p[:, 1])
+
+
+def _host_surface(sampler, max_level):
+    """Independent host classification: sample every leaf centre (+halo) with the
+    host sampler, IsEdge by 6-neighbour air test (NaiveCreator.cs:56,121-130)."""
+    d = max_level - 1
+    n = 1 << d
+    size = np.float32(2.0 ** -d)
+    c = (np.float32(1) + (np.arange(-1, n + 1, dtype=np.float32) + np.float32(0.5)) * size).astype(np.float32)
+    X, Y, Z = np.meshgrid(c, c, c, indexing="ij")
+    v = nb.eval_sampler(sampler, np.stack([X, Y, Z], -1).reshape(-1, 3)).reshape(X.shape)
+    solid = v <= 0
+    air = v > 0
+    core = solid[1:-1, 1:-1, 1:-1]
+    edge = np.zeros_like(core)
+    for ax in range(3):
+        for s in (0, 2):
+            sl = [slice(1, -1)] * 3
+            sl[ax] = slice(s, s + n)
+            edge |= air[tuple(sl)]
+    return np.argwhere(core & edge)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sampler,max_level", [(4, 5), (4, 7), (2, 6)])
+def test_gpu_classification_matches_host(sampler, max_level):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    codes, nrm = nb.surface_leaves(sampler, max_level)
+    host = _host_surface(sampler, max_level)
+    from raytracingtest_amd.builder import morton
+    assert np.array_equal(np.sort(morton(host)), codes)
+    # normals: -Normalize(finite differences), recomputed on the host
+    d = max_level - 1
+    size = np.float32(2.0 ** -d)
+    from raytracingtest_amd.builder import normalize_unity
+    xyz = host[np.argsort(morton(host))].astype(np.float32)
+    p = (np.float32(1) + xyz * size + size / np.float32(2)).astype(np.float32)
+    h = np.float32(0.001)
+    s0 = nb.eval_sampler(sampler, p)
+    diffs = []
+    for ax in range(3):
+        q = p.copy()
+        q[:, ax] = (q[:, ax] - h).astype(np.float32)
+        diffs.append((nb.eval_sampler(sampler, q) - s0).astype(np.float32))
+    ref = -normalize_unity(np.stack(diffs, 1))
+    np.testing.assert_array_equal(nrm, ref)
+
+
+@pytest.mark.gpu
+def test_gpu_build_depth10_custom1():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    svo = nb.build_sampler_svo(nb.CUSTOM1, 11)
+    assert svo.depth() == 10
+    assert svo.n_leaves > 1_000_000
+    lo, first = svo.masks_and_first()
+    assert lo[0] & 0xFF00   # root has children
