@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--split", choices=["samples", "bands"], default="samples")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--no-rgba", action="store_true")
+    p.add_argument("--camera", choices=["flyover", "overview", "main"], default="flyover")
     return p.parse_args()
 
 
@@ -69,7 +70,7 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
 
     from raytracingtest_amd import RaytracingMaster, band_rows
-    from raytracingtest_amd.camera import jitter_offsets, main_light, overview_camera
+    from raytracingtest_amd.camera import CAMERAS, jitter_offsets
     from raytracingtest_amd.native_builder import build_sampler_svo
 
     W, H = args.width, args.height
@@ -80,7 +81,7 @@ def main():
 
     rm = RaytracingMaster(device=dev.index, capacity_nodes=n_nodes)
     rm.SetSVOBuffer(svo)
-    cam = overview_camera()
+    cam = CAMERAS[args.camera]()
     if args.split == "samples":
         off = (0.5, 0.5) if rank == 0 else tuple(float(v) for v in jitter_offsets(world)[rank])
         band = None
@@ -94,7 +95,9 @@ def main():
     n_px = W * rows
     hits = torch.empty(n_px * 24, dtype=torch.uint8, device=dev)
     rgba = None if args.no_rgba else torch.empty(n_px * 4, dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream: the kernel and the timing events share it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     gathered = None
     if args.split == "bands" and world > 1:
@@ -166,7 +169,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement",
             "config": {"workload": f"C3 depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) Custom1 SVO, "
-                                   f"{W}x{H} primary rays, overview camera",
+                                   f"{W}x{H} primary rays, {args.camera} camera",
                        "svo_nodes": n_nodes, "svo_format": "V%d" % svo.format, "svo_leaves": getattr(svo, "n_leaves", None),
                        "build_s": round(build_s, 2), "stack_mode": "hlsl" if args.stack_mode == 0 else "exact",
                        "rays_per_gpu_step": n_px, "hit_fraction": round(n_hit / n_px, 4),
@@ -198,8 +201,8 @@ def pmc_traffic():
 
 
 def cpu_baseline(args, svo, cam, off, gpu_hits):
-    """Oracle ("port") on the host cores over the same frame, bounded by
-    --cpu-seconds; also spot-checks the GPU hit records against it."""
+    """Oracle ("port") on the host cores over rows of the same frame, bounded by
+    --cpu-seconds; the rows it traces are also compared with the GPU records."""
     from oracle import oracle as orc
     from raytracingtest_amd.camera import main_light
 
@@ -208,32 +211,32 @@ def cpu_baseline(args, svo, cam, off, gpu_hits):
     c2w, inv_proj = cam.uniforms(W, H)
     ocam = orc.make_camera(c2w, inv_proj, off, main_light())
     osvo = orc.OracleSVO(nodes=svo.to_v2(), attachments=svo.attachments)
-    # sample: whole rows spread over the frame, grown until the time budget is used
-    rows_total, rays, secs = 0, 0, 0.0
-    mism = 0
-    step = 8
-    t_begin = time.perf_counter()
-    y = 0
-    while time.perf_counter() - t_begin < args.cpu_seconds and rows_total < H:
-        y0 = (y * step) % H + (y * step) // H
-        t = time.perf_counter()
-        hits, _, _ = orc.render(osvo, ocam, W, H, args.stack_mode, y0=y0, y1=y0 + 1, nthreads=threads,
-                                want_rgba=True, want_fetches=False)
-        secs += time.perf_counter() - t
-        rays += W
-        rows_total += 1
-        g = gpu_hits[y0 * W:(y0 + 1) * W]
-        mism += int(g.tobytes() != hits.tobytes())
-        y += 1
-    # single-thread figure on a short sample
+    # calibrate on 8 rows spread over the frame, then one bounded call
+    ys = np.linspace(0, H - 1, 8).astype(np.int64)
+    pix = (ys[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
     t = time.perf_counter()
-    orc.render(osvo, ocam, W, H, args.stack_mode, y0=H // 2, y1=H // 2 + 4, nthreads=1, want_fetches=False)
-    one_core = 4 * W / (time.perf_counter() - t) / 1e6
-    return {"value": round(rays / secs / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{rows_total} full rows ({rays} rays) of the same 1920x1080 frame, {threads} threads; "
-                      f"1-thread: {one_core:.3f} Mrays/s",
+    orc.render_pixels(osvo, ocam, W, H, pix, args.stack_mode, nthreads=threads)
+    rate = len(pix) / (time.perf_counter() - t)
+    n_rows = int(min(H, max(8, rate * args.cpu_seconds / W)))
+    ys = np.unique(np.linspace(0, H - 1, n_rows).astype(np.int64))
+    pix = (ys[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
+    t = time.perf_counter()
+    hits, _, _ = orc.render_pixels(osvo, ocam, W, H, pix, args.stack_mode, nthreads=threads)
+    secs = time.perf_counter() - t
+    a = np.frombuffer(gpu_hits[pix].tobytes(), np.uint8).reshape(-1, 24)
+    b = np.frombuffer(hits.tobytes(), np.uint8).reshape(-1, 24)
+    mism = int(np.count_nonzero((a != b).any(axis=1)))
+    # single-thread figure on the 8 calibration rows
+    ys1 = np.linspace(0, H - 1, 8).astype(np.int64)
+    pix1 = (ys1[:, None] * W + np.arange(0, W, 4)[None, :]).reshape(-1).astype(np.uint32)
+    t = time.perf_counter()
+    orc.render_pixels(osvo, ocam, W, H, pix1, args.stack_mode, nthreads=1)
+    one_core = len(pix1) / (time.perf_counter() - t) / 1e6
+    return {"value": round(len(pix) / secs / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{len(ys)} full rows ({len(pix)} rays) spread over the same {W}x{H} frame, "
+                      f"{threads} threads, {secs:.1f} s; 1-thread rate on 8 rows: {one_core:.3f} Mrays/s",
             "one_core_mrays": round(one_core, 4),
-            "parity_rows_checked": rows_total, "parity_rows_mismatched": mism}
+            "parity_rays_checked": int(len(pix)), "parity_rays_mismatched": mism}
 
 
 if __name__ == "__main__":

@@ -1,7 +1,18 @@
-// svo_kernel.hip -- gfx950 primary-ray SVO traversal kernel (see svo_traverse.h).
+// svo_kernel.hip -- gfx950 primary-ray SVO traversal kernels (see svo_traverse.h).
 //
 // Line references are to the reference repo: NVIDIASVO.compute (N:),
 // RaytraceCompute.compute (R:), AttachmentLookup.compute (A:).
+//
+// Two launch shapes over one traversal core:
+//   * tile kernel: one lane per pixel, a wave64 = an 8x8 pixel tile;
+//   * persistent kernel (default): resident waves pull rays from a global
+//     counter in 64-ray 8x8 tiles; whenever fewer than REFILL_AT lanes of a
+//     wave are still tracing, the idle lanes take new rays (ballot + one
+//     atomicAdd per wave + mbcnt rank), so long rays no longer hold 63 idle
+//     lanes (active-ray compaction within the wave).
+// The loop body is written branch-light: PUSH and ADVANCE differ only in
+// selected addends, so divergent lanes share one instruction stream; only the
+// node fetch, the stack store, POP and termination are predicated regions.
 #include "svo_traverse.h"
 
 namespace svo {
@@ -58,27 +69,28 @@ __device__ __forceinline__ void decode_dxt(uint32_t head, uint32_t bits, int tex
     out[2] = b * (1.0f / 256.0f);
 }
 
-// HLSL float -> int (truncating, saturating; NaN -> 0) == v_cvt_i32_f32.
-__device__ __forceinline__ int32_t hlsl_f2i(float f) {
-    if (f != f) return 0;
-    if (f >= 2147483648.0f) return 2147483647;
-    if (f <= -2147483648.0f) return (int32_t)0x80000000u;
-    return (int32_t)f;
+// HLSL float -> int: truncating, saturating, NaN -> 0 == v_cvt_i32_f32 itself.
+__device__ __forceinline__ int32_t cvt_i32(float f) {
+    int32_t r;
+    asm volatile("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+    return r;
 }
 
-template <int MODE, bool COUNT>
-__global__ __launch_bounds__(BLOCK) void render_kernel(LaunchParams p) {
-    extern __shared__ uint2 stk[];   // [p.slots][BLOCK]
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    if (x >= p.width || lr >= p.local_rows) return;
-    const int band = lr / p.band_rows;
-    const int y = (band * p.band_count + p.band_rank) * p.band_rows + (lr - band * p.band_rows);
+struct Ray {
+    float tx_coef, ty_coef, tz_coef, tx_bias, ty_bias, tz_bias;
+    float t_min, t_max, h;
+    float px, py, pz, scale_exp2;
+    float dir_y;               // for the sky colour
+    uint32_t parent, cd, first;
+    uint32_t written;          // bit s: stack slot s written by this ray
+    uint32_t fetches;
+    int idx, octant_mask, scale, iters;
+    uint32_t flags;
+    bool cached;
+};
 
-    // ---- R:151 uv, R:129-141 CreateCameraRay ----
+// R:151 uv, R:129-141 CreateCameraRay, N:15-54 setup
+__device__ __forceinline__ void init_ray(const LaunchParams &p, int x, int y, Ray &r) {
     const float u = ((float)x + p.cam.px_off[0]) / (float)p.width * 2.0f - 1.0f;
     const float v = ((float)y + p.cam.px_off[1]) / (float)p.height * 2.0f - 1.0f;
     float org[3], pd[3], dir[3];
@@ -86,151 +98,162 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(LaunchParams p) {
     mul4(p.cam.inv_proj, u, v, 0.0f, 1.0f, pd);
     mul4(p.cam.c2w, pd[0], pd[1], pd[2], 0.0f, dir);
     normalize3(dir);
+    r.dir_y = dir[1];
 
-    // ---- N:15-54 setup ----
     float ox = org[0] * (1.0f / 32.0f), oy = org[1] * (1.0f / 32.0f), oz = org[2] * (1.0f / 32.0f);
     ox = ox + 1.5f; oy = oy + 1.5f; oz = oz + 1.5f;
-    const float tx_coef = 1.0f / -fabsf(dir[0]);
-    const float ty_coef = 1.0f / -fabsf(dir[1]);
-    const float tz_coef = 1.0f / -fabsf(dir[2]);
-    float tx_bias = tx_coef * ox;
-    float ty_bias = ty_coef * oy;
-    float tz_bias = tz_coef * oz;
-    int octant_mask = 7;
-    if (dir[0] > 0.0f) { octant_mask ^= 1; tx_bias = 3.0f * tx_coef - tx_bias; }
-    if (dir[1] > 0.0f) { octant_mask ^= 2; ty_bias = 3.0f * ty_coef - ty_bias; }
-    if (dir[2] > 0.0f) { octant_mask ^= 4; tz_bias = 3.0f * tz_coef - tz_bias; }
-    float t_min = fmaxf(fmaxf(2.0f * tx_coef - tx_bias, 2.0f * ty_coef - ty_bias), 2.0f * tz_coef - tz_bias);
-    float t_max = fminf(fminf(tx_coef - tx_bias, ty_coef - ty_bias), tz_coef - tz_bias);
-    float h = t_max;
-    t_min = fmaxf(t_min, 0.0f);
+    r.tx_coef = 1.0f / -fabsf(dir[0]);
+    r.ty_coef = 1.0f / -fabsf(dir[1]);
+    r.tz_coef = 1.0f / -fabsf(dir[2]);
+    r.tx_bias = r.tx_coef * ox;
+    r.ty_bias = r.ty_coef * oy;
+    r.tz_bias = r.tz_coef * oz;
+    r.octant_mask = 7;
+    if (dir[0] > 0.0f) { r.octant_mask ^= 1; r.tx_bias = 3.0f * r.tx_coef - r.tx_bias; }
+    if (dir[1] > 0.0f) { r.octant_mask ^= 2; r.ty_bias = 3.0f * r.ty_coef - r.ty_bias; }
+    if (dir[2] > 0.0f) { r.octant_mask ^= 4; r.tz_bias = 3.0f * r.tz_coef - r.tz_bias; }
+    r.t_min = fmaxf(fmaxf(2.0f * r.tx_coef - r.tx_bias, 2.0f * r.ty_coef - r.ty_bias), 2.0f * r.tz_coef - r.tz_bias);
+    r.t_max = fminf(fminf(r.tx_coef - r.tx_bias, r.ty_coef - r.ty_bias), r.tz_coef - r.tz_bias);
+    r.h = r.t_max;
+    r.t_min = fmaxf(r.t_min, 0.0f);
+    r.parent = 0; r.cd = 0; r.first = 0;
+    r.cached = false;
+    r.idx = 0;
+    r.px = 1.0f; r.py = 1.0f; r.pz = 1.0f;
+    r.scale = S_MAX - 1;
+    r.scale_exp2 = 0.5f;
+    if (1.5f * r.tx_coef - r.tx_bias > r.t_min) { r.idx ^= 1; r.px = 1.5f; }
+    if (1.5f * r.ty_coef - r.ty_bias > r.t_min) { r.idx ^= 2; r.py = 1.5f; }
+    if (1.5f * r.tz_coef - r.tz_bias > r.t_min) { r.idx ^= 4; r.pz = 1.5f; }
+    r.written = 0; r.fetches = 0; r.iters = 0; r.flags = 0;
+}
 
-    uint32_t parent = 0, cd = 0, first = 0;
-    bool cached = false;
-    int idx = 0;
-    float px = 1.0f, py = 1.0f, pz = 1.0f;
-    int scale = S_MAX - 1;
-    float scale_exp2 = 0.5f;
-    if (1.5f * tx_coef - tx_bias > t_min) { idx ^= 1; px = 1.5f; }
-    if (1.5f * ty_coef - ty_bias > t_min) { idx ^= 2; py = 1.5f; }
-    if (1.5f * tz_coef - tz_bias > t_min) { idx ^= 4; pz = 1.5f; }
+// One iteration of N:57-156.  Returns true when the ray is finished: a leaf hit
+// (r.scale < S_MAX) or a miss (r.scale >= S_MAX).
+template <int MODE, bool COUNT>
+__device__ __forceinline__ bool step(const LaunchParams &p, Ray &r, uint2 *__restrict__ stk, int scale_lo) {
+    if (r.scale >= S_MAX) return true;
+    if (++r.iters > MAX_ITERS) { r.flags |= 2u; r.scale = S_MAX; return true; }
+    if (!r.cached) {                                       // N:60-62
+        const uint2 nd = p.nodes[r.parent];
+        r.cd = nd.x;
+        r.first = nd.y;
+        r.cached = (nd.x | nd.y) != 0u;
+        if (COUNT) ++r.fetches;
+    }
+    const float tx_corner = r.px * r.tx_coef - r.tx_bias;
+    const float ty_corner = r.py * r.ty_coef - r.ty_bias;
+    const float tz_corner = r.pz * r.tz_coef - r.tz_bias;
+    const float tc_max = fminf(fminf(tx_corner, ty_corner), tz_corner);
+    const uint32_t child_masks = r.cd << (r.idx ^ r.octant_mask);
+    const float tv_max = fminf(r.t_max, tc_max);
+    const bool descend = (child_masks & 0x8000u) != 0u && r.t_min <= r.t_max && r.t_min <= tv_max;
+    if (descend && (child_masks & 0x0080u) == 0u) return true;   // leaf hit (N:93-94)
 
-    const int scale_lo = S_MAX - p.slots;   // lowest pushed scale
-    uint32_t written = 0;                    // bit s: slot s written by this ray
-    uint32_t fetches = 0;
-    int iters = 0;
-    uint32_t flags = 0;
-
-    // ---- N:57-156 ----
-    while (scale < S_MAX) {
-        if (++iters > MAX_ITERS) { flags |= 2u; scale = S_MAX; break; }
-        if (!cached) {                                     // N:60-62
-            const uint2 nd = p.nodes[parent];
-            cd = nd.x;
-            first = nd.y;
-            cached = (nd.x | nd.y) != 0u;
-            if (COUNT) ++fetches;
-        }
-        const float tx_corner = px * tx_coef - tx_bias;
-        const float ty_corner = py * ty_coef - ty_bias;
-        const float tz_corner = pz * tz_coef - tz_bias;
-        const float tc_max = fminf(fminf(tx_corner, ty_corner), tz_corner);
-
-        const uint32_t child_masks = cd << (idx ^ octant_mask);
-        if ((child_masks & 0x8000u) != 0u && t_min <= t_max) {
-            const float tv_max = fminf(t_max, tc_max);
-            const float half = scale_exp2 * 0.5f;
-            const float tx_center = half * tx_coef + tx_corner;
-            const float ty_center = half * ty_coef + ty_corner;
-            const float tz_center = half * tz_coef + tz_corner;
-            if (t_min <= tv_max) {
-                if ((child_masks & 0x0080u) == 0u) break;   // leaf hit (N:93-94)
-                if (tc_max < h) {                           // PUSH (N:97-98)
-                    const int s = scale - scale_lo;
-                    if (s < 0) { flags |= 4u; scale = S_MAX; break; }
-                    uint2 e;
-                    if (MODE == 0) {   // int2 <- float2((int)parent, asint(t_max))
-                        e.x = (uint32_t)hlsl_f2i((float)(int32_t)parent);
-                        e.y = (uint32_t)hlsl_f2i((float)__float_as_int(t_max));
-                    } else {
-                        e.x = parent;
-                        e.y = (uint32_t)__float_as_int(t_max);
-                    }
-                    stk[s * BLOCK + tid] = e;
-                    written |= 1u << s;
-                }
-                h = tc_max;
-                parent = first + (uint32_t)__builtin_popcount(child_masks & 0x7Fu);   // N:101-105
-                idx = 0;
-                scale--;
-                scale_exp2 = half;
-                if (tx_center > t_min) { idx ^= 1; px = px + scale_exp2; }
-                if (ty_center > t_min) { idx ^= 2; py = py + scale_exp2; }
-                if (tz_center > t_min) { idx ^= 4; pz = pz + scale_exp2; }
-                t_max = tv_max;
-                cached = false;
-                continue;
+    const float half = r.scale_exp2 * 0.5f;
+    int new_idx;
+    float ax, ay, az;
+    if (descend) {
+        // PUSH (N:97-117)
+        if (tc_max < r.h) {
+            const int s = r.scale - scale_lo;
+            if (s < 0) { r.flags |= 4u; r.scale = S_MAX; return true; }
+            uint2 e;
+            if (MODE == 0) {   // int2 <- float2((int)parent, asint(t_max))
+                e.x = (uint32_t)cvt_i32((float)(int32_t)r.parent);
+                e.y = (uint32_t)cvt_i32((float)__float_as_int(r.t_max));
+            } else {
+                e.x = r.parent;
+                e.y = (uint32_t)__float_as_int(r.t_max);
             }
+            stk[s * BLOCK] = e;
+            r.written |= 1u << s;
         }
+        r.h = tc_max;
+        r.parent = r.first + (uint32_t)__builtin_popcount(child_masks & 0x7Fu);
+        const float tx_center = half * r.tx_coef + tx_corner;
+        const float ty_center = half * r.ty_coef + ty_corner;
+        const float tz_center = half * r.tz_coef + tz_corner;
+        new_idx = (tx_center > r.t_min ? 1 : 0) | (ty_center > r.t_min ? 2 : 0) | (tz_center > r.t_min ? 4 : 0);
+        ax = (new_idx & 1) ? half : 0.0f;
+        ay = (new_idx & 2) ? half : 0.0f;
+        az = (new_idx & 4) ? half : 0.0f;
+        r.scale -= 1;
+        r.scale_exp2 = half;
+        r.t_max = tv_max;
+        r.cached = false;
+    } else {
         // ADVANCE (N:122-128)
-        int step_mask = 0;
-        if (tx_corner <= tc_max) { step_mask ^= 1; px = px - scale_exp2; }
-        if (ty_corner <= tc_max) { step_mask ^= 2; py = py - scale_exp2; }
-        if (tz_corner <= tc_max) { step_mask ^= 4; pz = pz - scale_exp2; }
-        t_min = tc_max;
-        idx ^= step_mask;
-        if ((idx & step_mask) != 0) {
-            // POP (N:134-154)
+        const int step_mask = (tx_corner <= tc_max ? 1 : 0) | (ty_corner <= tc_max ? 2 : 0) |
+                              (tz_corner <= tc_max ? 4 : 0);
+        ax = (step_mask & 1) ? -r.scale_exp2 : 0.0f;
+        ay = (step_mask & 2) ? -r.scale_exp2 : 0.0f;
+        az = (step_mask & 4) ? -r.scale_exp2 : 0.0f;
+        r.t_min = tc_max;
+        new_idx = r.idx ^ step_mask;
+        if ((new_idx & step_mask) != 0) {
+            // POP (N:134-154): positions after the step, then the highest differing bit
+            const float qx = r.px + ax, qy = r.py + ay, qz = r.pz + az;
             uint32_t differing = 0;
-            if (step_mask & 1) differing |= (uint32_t)(__float_as_int(px) ^ __float_as_int(px + scale_exp2));
-            if (step_mask & 2) differing |= (uint32_t)(__float_as_int(py) ^ __float_as_int(py + scale_exp2));
-            if (step_mask & 4) differing |= (uint32_t)(__float_as_int(pz) ^ __float_as_int(pz + scale_exp2));
-            scale = (__float_as_int((float)differing) >> 23) - 127;
-            scale_exp2 = __int_as_float((scale - S_MAX + 127) << 23);
+            if (step_mask & 1) differing |= (uint32_t)(__float_as_int(qx) ^ __float_as_int(qx + r.scale_exp2));
+            if (step_mask & 2) differing |= (uint32_t)(__float_as_int(qy) ^ __float_as_int(qy + r.scale_exp2));
+            if (step_mask & 4) differing |= (uint32_t)(__float_as_int(qz) ^ __float_as_int(qz + r.scale_exp2));
+            const int scale = (__float_as_int((float)differing) >> 23) - 127;
+            r.scale = scale;
+            r.scale_exp2 = __int_as_float((scale - S_MAX + 127) << 23);
             const int s = scale - scale_lo;
             uint2 e = make_uint2(0u, 0u);
-            if (s >= 0 && s < 32 && ((written >> s) & 1u)) e = stk[s * BLOCK + tid];
-            parent = e.x;
-            t_max = __int_as_float((int32_t)e.y);
-            const int32_t shx = __float_as_int(px) >> scale;
-            const int32_t shy = __float_as_int(py) >> scale;
-            const int32_t shz = __float_as_int(pz) >> scale;
-            px = __int_as_float((int32_t)((uint32_t)shx << scale));
-            py = __int_as_float((int32_t)((uint32_t)shy << scale));
-            pz = __int_as_float((int32_t)((uint32_t)shz << scale));
-            idx = (shx & 1) | ((shy & 1) << 1) | ((shz & 1) << 2);
-            h = 0.0f;
-            cached = false;
+            if (s >= 0 && s < 32 && ((r.written >> s) & 1u)) e = stk[s * BLOCK];
+            r.parent = e.x;
+            r.t_max = __int_as_float((int32_t)e.y);
+            const int32_t shx = __float_as_int(qx) >> scale;
+            const int32_t shy = __float_as_int(qy) >> scale;
+            const int32_t shz = __float_as_int(qz) >> scale;
+            r.px = __int_as_float((int32_t)((uint32_t)shx << scale));
+            r.py = __int_as_float((int32_t)((uint32_t)shy << scale));
+            r.pz = __int_as_float((int32_t)((uint32_t)shz << scale));
+            r.idx = (shx & 1) | ((shy & 1) << 1) | ((shz & 1) << 2);
+            r.h = 0.0f;
+            r.cached = false;
+            return r.scale >= S_MAX;
         }
     }
+    r.px = r.px + ax;
+    r.py = r.py + ay;
+    r.pz = r.pz + az;
+    r.idx = new_idx;
+    return false;
+}
 
-    const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
-    if (COUNT) {
-        p.fetches[out] = fetches;
-        return;
-    }
-    // ---- N:158-186 hit decode; R:93-127 Shade; R:167 store ----
-    Hit hr;
-    float rgb[3];
-    if (scale >= S_MAX) {
-        hr.parent = 0xFFFFFFFFu; hr.hit_idx = 0; hr.hit_scale = 0; hr.flags = (uint16_t)flags;
-        hr.t = __int_as_float(0x7F800000); hr.nx = 0.0f; hr.ny = 0.0f; hr.nz = 0.0f;
+// N:158-186 hit decode; R:93-127 Shade; R:167 store
+__device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r_in, size_t out) {
+    Ray r = r_in;
+    uint32_t w0, w1, w2, w3, w4, w5;
+    float rgb0, rgb1, rgb2;
+    if (r.scale >= S_MAX) {
+        w0 = 0xFFFFFFFFu;
+        w1 = (r.flags & 0xFFFFu) << 16;
+        w2 = 0x7F800000u;
+        w3 = 0u; w4 = 0u; w5 = 0u;
         // procedural sky (the reference's skybox assets are missing), == orc_sky
-        const float k = 0.5f * dir[1] + 0.5f;
-        rgb[0] = 0.25f + 0.5f * k;
-        rgb[1] = 0.35f + 0.55f * k;
-        rgb[2] = 0.6f + 0.4f * k;
+        const float k = 0.5f * r.dir_y + 0.5f;
+        rgb0 = 0.25f + 0.5f * k;
+        rgb1 = 0.35f + 0.55f * k;
+        rgb2 = 0.6f + 0.4f * k;
     } else {
-        t_min = t_min * 32.0f;
-        const int hit_idx = idx ^ octant_mask ^ 7;
-        const uint2 a = p.att[parent];
+        const float t_min = r.t_min * 32.0f;
+        const int hit_idx = r.idx ^ r.octant_mask ^ 7;
+        const uint2 a = p.att[r.parent];
         float n[3];
         decode_normal(a.y >> 16, n);
         normalize3(n);
-        hr.parent = parent; hr.hit_idx = (uint8_t)hit_idx; hr.hit_scale = (uint8_t)scale;
-        hr.flags = (uint16_t)(flags | 1u);
-        hr.t = t_min * 64.0f;
-        hr.nx = n[0]; hr.ny = n[1]; hr.nz = n[2];
+        w0 = r.parent;
+        w1 = (uint32_t)hit_idx | ((uint32_t)r.scale << 8) | (((r.flags | 1u) & 0xFFFFu) << 16);
+        w2 = (uint32_t)__float_as_int(t_min * 64.0f);
+        w3 = (uint32_t)__float_as_int(n[0]);
+        w4 = (uint32_t)__float_as_int(n[1]);
+        w5 = (uint32_t)__float_as_int(n[2]);
+        rgb0 = rgb1 = rgb2 = 0.0f;
         if (p.rgba) {
             float alb[3];
             decode_dxt(a.x, a.y, hit_idx, alb);
@@ -240,32 +263,137 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(LaunchParams p) {
             float s = d * -1.0f;
             s = fminf(fmaxf(s, 0.0f), 1.0f);
             s = s * p.cam.light[3];
-            rgb[0] = s * alb[0]; rgb[1] = s * alb[1]; rgb[2] = s * alb[2];
+            rgb0 = s * alb[0]; rgb1 = s * alb[1]; rgb2 = s * alb[2];
         }
     }
     if (p.hits) {
         uint2 *dst = reinterpret_cast<uint2 *>(p.hits + out);
-        dst[0] = make_uint2(hr.parent, (uint32_t)hr.hit_idx | ((uint32_t)hr.hit_scale << 8) | ((uint32_t)hr.flags << 16));
-        dst[1] = make_uint2((uint32_t)__float_as_int(hr.t), (uint32_t)__float_as_int(hr.nx));
-        dst[2] = make_uint2((uint32_t)__float_as_int(hr.ny), (uint32_t)__float_as_int(hr.nz));
+        dst[0] = make_uint2(w0, w1);
+        dst[1] = make_uint2(w2, w3);
+        dst[2] = make_uint2(w4, w5);
     }
-    if (p.rgba) p.rgba[out] = make_float4(rgb[0], rgb[1], rgb[2], 1.0f);
+    if (p.rgba) p.rgba[out] = make_float4(rgb0, rgb1, rgb2, 1.0f);
+}
+
+__device__ __forceinline__ int global_row(const LaunchParams &p, int lr) {
+    const int band = lr / p.band_rows;
+    return (band * p.band_count + p.band_rank) * p.band_rows + (lr - band * p.band_rows);
+}
+
+// ------------------------------------------------------------- tile kernel
+template <int MODE, bool COUNT>
+__global__ __launch_bounds__(BLOCK) void render_tile_kernel(LaunchParams p) {
+    extern __shared__ uint2 stk_base[];   // [p.slots][BLOCK]
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    if (x >= p.width || lr >= p.local_rows) return;
+    Ray r;
+    init_ray(p, x, global_row(p, lr), r);
+    const int scale_lo = S_MAX - p.slots;
+    uint2 *stk = stk_base + tid;
+    while (!step<MODE, COUNT>(p, r, stk, scale_lo)) {
+    }
+    const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
+    if (COUNT) { p.fetches[out] = r.fetches; return; }
+    finish(p, r, out);
+}
+
+// ------------------------------------------------------- persistent kernel
+constexpr int REFILL_AT = 40;   // refill the idle lanes when fewer lanes than this trace
+
+template <int MODE, bool COUNT>
+__global__ __launch_bounds__(BLOCK) void render_persistent_kernel(LaunchParams p, uint32_t *__restrict__ counter,
+                                                                  uint32_t total_rays, int tiles_x) {
+    extern __shared__ uint2 stk_base[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    uint2 *stk = stk_base + tid;
+    const int scale_lo = S_MAX - p.slots;
+    Ray r;
+    bool active = false;
+    int x = 0, lr = 0;
+    bool exhausted = false;
+    for (;;) {
+        // ---- refill idle lanes (wave-uniform control flow) ----
+        const uint64_t idle = __ballot(!active);
+        if (!exhausted && idle != 0ull) {
+            const uint32_t n_idle = (uint32_t)__popcll(idle);
+            const int leader = __ffsll((long long)idle) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(counter, n_idle);
+            base = (uint32_t)__shfl((int)base, leader);
+            if (base >= total_rays) exhausted = true;
+            if (!active) {
+                const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                const uint32_t ray = base + rank;
+                if (ray < total_rays) {
+                    const uint32_t tile = ray >> 6;
+                    x = (int)(tile % (uint32_t)tiles_x) * 8 + (int)(ray & 7u);
+                    lr = (int)(tile / (uint32_t)tiles_x) * 8 + (int)((ray >> 3) & 7u);
+                    if (x < p.width && lr < p.local_rows) {
+                        init_ray(p, x, global_row(p, lr), r);
+                        active = true;
+                    }
+                }
+            }
+        }
+        if (__ballot(active) == 0ull) {
+            if (exhausted) break;
+            continue;
+        }
+        // ---- trace until too few lanes remain busy ----
+        for (;;) {
+            if (active) {
+                if (step<MODE, COUNT>(p, r, stk, scale_lo)) {
+                    const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
+                    if (COUNT) p.fetches[out] = r.fetches;
+                    else finish(p, r, out);
+                    active = false;
+                }
+            }
+            const int busy = __popcll(__ballot(active));
+            if (busy == 0 || (!exhausted && busy < REFILL_AT)) break;
+        }
+    }
 }
 
 }  // namespace
 
-hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream) {
-    dim3 grid((unsigned)((p.width + 15) / 16), (unsigned)((p.local_rows + 15) / 16));
-    size_t lds = (size_t)p.slots * BLOCK * sizeof(uint2);
-    const bool count = p.fetches != nullptr;
-    if (stack_mode == 0) {
-        if (count) hipLaunchKernelGGL((render_kernel<0, true>), grid, dim3(BLOCK), lds, stream, p);
-        else hipLaunchKernelGGL((render_kernel<0, false>), grid, dim3(BLOCK), lds, stream, p);
-    } else {
-        if (count) hipLaunchKernelGGL((render_kernel<1, true>), grid, dim3(BLOCK), lds, stream, p);
-        else hipLaunchKernelGGL((render_kernel<1, false>), grid, dim3(BLOCK), lds, stream, p);
+template <int MODE, bool COUNT>
+static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int kernel, uint32_t *counter,
+                                 int max_blocks) {
+    const size_t lds = (size_t)p.slots * BLOCK * sizeof(uint2);
+    if (kernel == 0) {
+        dim3 grid((unsigned)((p.width + 15) / 16), (unsigned)((p.local_rows + 15) / 16));
+        hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT>), grid, dim3(BLOCK), lds, stream, p);
+        return hipGetLastError();
     }
+    const int tiles_x = (p.width + 7) / 8;
+    const int tiles_y = (p.local_rows + 7) / 8;
+    const uint32_t total = (uint32_t)tiles_x * (uint32_t)tiles_y * 64u;
+    hipError_t e = hipMemsetAsync(counter, 0, 16, stream);
+    if (e != hipSuccess) return e;
+    int occ = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, render_persistent_kernel<MODE, COUNT>, BLOCK, lds);
+    if (e != hipSuccess || occ < 1) occ = 1;
+    int blocks = std::min<long long>((long long)max_blocks * occ, ((long long)total + BLOCK - 1) / BLOCK);
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((render_persistent_kernel<MODE, COUNT>), dim3(blocks), dim3(BLOCK), lds, stream, p, counter,
+                       total, tiles_x);
     return hipGetLastError();
+}
+
+hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel, uint32_t *counter,
+                         int num_cus) {
+    const bool count = p.fetches != nullptr;
+    if (stack_mode == 0)
+        return count ? launch_variant<0, true>(p, stream, kernel, counter, num_cus)
+                     : launch_variant<0, false>(p, stream, kernel, counter, num_cus);
+    return count ? launch_variant<1, true>(p, stream, kernel, counter, num_cus)
+                 : launch_variant<1, false>(p, stream, kernel, counter, num_cus);
 }
 
 }  // namespace svo

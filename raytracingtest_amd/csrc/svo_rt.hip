@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -68,6 +69,9 @@ struct svo_ctx {
     void *d_out_hits = nullptr;
     void *d_out_rgba = nullptr;
     size_t out_cap_px = 0;
+    uint32_t *d_counter = nullptr;   // persistent-kernel work counter (16 B, zeroed per launch)
+    int num_cus = 256;
+    int kernel = 1;                  // 1 = persistent (default), 0 = tile; env SVO_KERNEL=tile|persistent
 };
 
 namespace {
@@ -208,7 +212,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.rgba = reinterpret_cast<float4 *>(d_rgba);
     p.fetches = d_fetch;
     if (p.local_rows == 0) return SVO_OK;
-    hipError_t e = svo::launch_render(p, stack_mode, stream ? stream : ctx->stream);
+    hipError_t e = svo::launch_render(p, stack_mode, stream ? stream : ctx->stream, ctx->kernel, ctx->d_counter,
+                                      ctx->num_cus);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
     return SVO_OK;
 }
@@ -237,6 +242,10 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     hipError_t e = hipMalloc(&ctx->d_nodes, capacity_nodes * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&ctx->d_att, capacity_nodes * sizeof(uint2));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_counter, 256);
+    if (e == hipSuccess) e = hipMemset(ctx->d_counter, 0, 256);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "tile") == 0 ? 0 : 1;
     if (e != hipSuccess) {
         svo_destroy(ctx);
         return fail(SVO_ERR_HIP, std::string("svo_create: ") + hipGetErrorString(e));
@@ -372,6 +381,7 @@ int svo_destroy(svo_ctx *ctx) {
     if (ctx->d_stage) hipFree(ctx->d_stage);
     if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
+    if (ctx->d_counter) hipFree(ctx->d_counter);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return SVO_OK;

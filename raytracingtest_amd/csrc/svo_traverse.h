@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 namespace svo {
 
 constexpr int S_MAX = 23;          // NVIDIASVO.compute:2
@@ -47,6 +49,9 @@ struct LaunchParams {
     uint32_t *fetches;    // nullable (instrumented launch)
 };
 
-hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream);
+// kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).
+// counter: 16-byte device work counter (persistent kernel), num_cus: CU count.
+hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel,
+                         uint32_t *counter, int num_cus);
 
 }  // namespace svo

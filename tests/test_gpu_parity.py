@@ -190,3 +190,24 @@ def test_errors_are_loud(rm):
             m.SetSVOBuffer(build_from_leaves(4, np.argwhere(np.ones((16, 16, 16))), np.ones((4096, 3), np.float32)))
     finally:
         m.close()
+
+
+def test_tile_and_persistent_kernels_identical(oracle_mod, text_svo, monkeypatch):
+    """Both launch shapes (SVO_KERNEL=tile / persistent) give the same records."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    svo = build_menger(7)
+    cam = overview_camera()
+    outs = []
+    for k in ("tile", "persistent"):
+        monkeypatch.setenv("SVO_KERNEL", k)
+        m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+        try:
+            m.SetSVOBuffer(svo)
+            m.UpdateShaderParameters(cam, 333, 177)
+            outs.append(m.Render(333, 177))
+        finally:
+            m.close()
+    assert outs[0][1].tobytes() == outs[1][1].tobytes()
+    assert outs[0][0].tobytes() == outs[1][0].tobytes()
