@@ -302,7 +302,6 @@ __global__ __launch_bounds__(BLOCK) void render_tile_kernel(LaunchParams p) {
 }
 
 // ------------------------------------------------------- persistent kernel
-constexpr int REFILL_AT = 40;   // refill the idle lanes when fewer lanes than this trace
 
 template <int MODE, bool COUNT>
 __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(LaunchParams p, uint32_t *__restrict__ counter,
@@ -355,7 +354,7 @@ __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(LaunchParams p
                 }
             }
             const int busy = __popcll(__ballot(active));
-            if (busy == 0 || (!exhausted && busy < REFILL_AT)) break;
+            if (busy == 0 || (!exhausted && busy < p.refill_at)) break;
         }
     }
 }
@@ -376,10 +375,9 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
     const uint32_t total = (uint32_t)tiles_x * (uint32_t)tiles_y * 64u;
     hipError_t e = hipMemsetAsync(counter, 0, 16, stream);
     if (e != hipSuccess) return e;
-    int occ = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, render_persistent_kernel<MODE, COUNT>, BLOCK, lds);
-    if (e != hipSuccess || occ < 1) occ = 1;
-    int blocks = std::min<long long>((long long)max_blocks * occ, ((long long)total + BLOCK - 1) / BLOCK);
+    // Over-subscribe: blocks beyond the resident set start when others retire and
+    // find the counter drained (no inter-block dependency, so residency is free).
+    int blocks = (int)std::min<long long>((long long)max_blocks * p.blocks_per_cu, ((long long)total + BLOCK - 1) / BLOCK);
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL((render_persistent_kernel<MODE, COUNT>), dim3(blocks), dim3(BLOCK), lds, stream, p, counter,
                        total, tiles_x);

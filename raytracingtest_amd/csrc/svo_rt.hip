@@ -72,6 +72,8 @@ struct svo_ctx {
     uint32_t *d_counter = nullptr;   // persistent-kernel work counter (16 B, zeroed per launch)
     int num_cus = 256;
     int kernel = 1;                  // 1 = persistent (default), 0 = tile; env SVO_KERNEL=tile|persistent
+    int refill_at = 40;              // env SVO_REFILL
+    int blocks_per_cu = 8;           // env SVO_BLOCKS_PER_CU
 };
 
 namespace {
@@ -211,6 +213,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.hits = reinterpret_cast<svo::Hit *>(d_hits);
     p.rgba = reinterpret_cast<float4 *>(d_rgba);
     p.fetches = d_fetch;
+    p.refill_at = ctx->refill_at;
+    p.blocks_per_cu = ctx->blocks_per_cu;
     if (p.local_rows == 0) return SVO_OK;
     hipError_t e = svo::launch_render(p, stack_mode, stream ? stream : ctx->stream, ctx->kernel, ctx->d_counter,
                                       ctx->num_cus);
@@ -246,6 +250,8 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (e == hipSuccess) e = hipMemset(ctx->d_counter, 0, 256);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "tile") == 0 ? 0 : 1;
+    if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
+    if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));
     if (e != hipSuccess) {
         svo_destroy(ctx);
         return fail(SVO_ERR_HIP, std::string("svo_create: ") + hipGetErrorString(e));

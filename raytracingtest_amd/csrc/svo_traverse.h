@@ -47,6 +47,8 @@ struct LaunchParams {
     Hit *hits;            // nullable
     float4 *rgba;         // nullable
     uint32_t *fetches;    // nullable (instrumented launch)
+    int refill_at;        // persistent kernel: refill idle lanes when fewer than this still trace
+    int blocks_per_cu;    // persistent kernel: grid = CUs x this
 };
 
 // kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).
