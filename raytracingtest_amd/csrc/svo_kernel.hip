@@ -4,12 +4,15 @@
 // RaytraceCompute.compute (R:), AttachmentLookup.compute (A:).
 //
 // Two launch shapes over one traversal core:
-//   * tile kernel: one lane per pixel, a wave64 = an 8x8 pixel tile;
-//   * persistent kernel (default): resident waves pull rays from a global
-//     counter in 64-ray 8x8 tiles; whenever fewer than REFILL_AT lanes of a
-//     wave are still tracing, the idle lanes take new rays (ballot + one
-//     atomicAdd per wave + mbcnt rank), so long rays no longer hold 63 idle
-//     lanes (active-ray compaction within the wave).
+//   * tile kernel (default): one lane per pixel, a wave64 = an 8x8 pixel tile;
+//   * persistent kernel: resident waves pull rays from a global counter in
+//     64-ray 8x8 tiles; whenever fewer than p.refill_at lanes of a wave are
+//     still tracing, the idle lanes take new rays (ballot + one atomicAdd per
+//     wave + mbcnt rank) -- active-ray compaction within the wave.
+//     Measured on MI355X (C3 flyover): 8x8 primary-ray tiles are
+//     already ~90% SIMD-efficient and one global counter serialises at ~88
+//     dequeues/us, so this shape is 2-8x SLOWER here; it is kept for
+//     incoherent ray sets (secondary rays) and as the A/B reference.
 // The loop body is written branch-light: PUSH and ADVANCE differ only in
 // selected addends, so divergent lanes share one instruction stream; only the
 // node fetch, the stack store, POP and termination are predicated regions.

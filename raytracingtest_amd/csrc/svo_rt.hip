@@ -71,7 +71,7 @@ struct svo_ctx {
     size_t out_cap_px = 0;
     uint32_t *d_counter = nullptr;   // persistent-kernel work counter (16 B, zeroed per launch)
     int num_cus = 256;
-    int kernel = 1;                  // 1 = persistent (default), 0 = tile; env SVO_KERNEL=tile|persistent
+    int kernel = 0;                  // 0 = tile (default), 1 = persistent; env SVO_KERNEL=tile|persistent
     int refill_at = 40;              // env SVO_REFILL
     int blocks_per_cu = 8;           // env SVO_BLOCKS_PER_CU
 };
@@ -249,7 +249,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (e == hipSuccess) e = hipMalloc(&ctx->d_counter, 256);
     if (e == hipSuccess) e = hipMemset(ctx->d_counter, 0, 256);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "tile") == 0 ? 0 : 1;
+    if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "persistent") == 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));
     if (e != hipSuccess) {
