@@ -228,6 +228,102 @@ __device__ __forceinline__ bool step(const LaunchParams &p, Ray &r, uint2 *__res
     return false;
 }
 
+// Branch-flattened iteration (default): identical results to step(), but PUSH
+// and ADVANCE are both evaluated and selected per lane, and the stack store is
+// unconditional (non-pushing lanes write a per-lane dummy slot), leaving only
+// the node fetch, POP and termination as divergent regions.  This removes most
+// of the exec-mask SALU traffic that dominated the branchy loop (SQ_INSTS_SALU
+// ~0.73 x SQ_INSTS_VALU on MI355X).
+template <int MODE, bool COUNT>
+__device__ __forceinline__ bool step_flat(const LaunchParams &p, Ray &r, uint2 *__restrict__ stk, int scale_lo,
+                                          int dummy) {
+    if (++r.iters > MAX_ITERS) { r.flags |= 2u; r.scale = S_MAX; return true; }
+    if (!r.cached) {                                       // N:60-62
+        const uint2 nd = p.nodes[r.parent];
+        r.cd = nd.x;
+        r.first = nd.y;
+        r.cached = (nd.x | nd.y) != 0u;
+        if (COUNT) ++r.fetches;
+    }
+    const float tx_corner = r.px * r.tx_coef - r.tx_bias;
+    const float ty_corner = r.py * r.ty_coef - r.ty_bias;
+    const float tz_corner = r.pz * r.tz_coef - r.tz_bias;
+    const float tc_max = fminf(fminf(tx_corner, ty_corner), tz_corner);
+    const uint32_t child_masks = r.cd << (r.idx ^ r.octant_mask);
+    const float tv_max = fminf(r.t_max, tc_max);
+    const bool descend = (child_masks & 0x8000u) != 0u && r.t_min <= r.t_max && r.t_min <= tv_max;
+    const bool do_store = descend && tc_max < r.h;
+    const int s_push = r.scale - scale_lo;
+    if ((descend && (child_masks & 0x0080u) == 0u) || (do_store && s_push < 0)) {
+        if (!(descend && (child_masks & 0x0080u) == 0u)) { r.flags |= 4u; r.scale = S_MAX; }
+        return true;                                       // leaf hit (N:93-94) or stack overflow
+    }
+    const float half = r.scale_exp2 * 0.5f;
+    // PUSH candidate (N:83-117)
+    const float tx_center = half * r.tx_coef + tx_corner;
+    const float ty_center = half * r.ty_coef + ty_corner;
+    const float tz_center = half * r.tz_coef + tz_corner;
+    const int cidx = (tx_center > r.t_min ? 1 : 0) | (ty_center > r.t_min ? 2 : 0) | (tz_center > r.t_min ? 4 : 0);
+    // ADVANCE candidate (N:122-128)
+    const int step_mask = (tx_corner <= tc_max ? 1 : 0) | (ty_corner <= tc_max ? 2 : 0) | (tz_corner <= tc_max ? 4 : 0);
+    // stack store (N:97-98); lanes that do not push write their dummy slot
+    uint2 e;
+    if (MODE == 0) {   // int2 <- float2((int)parent, asint(t_max))
+        e.x = (uint32_t)cvt_i32((float)(int32_t)r.parent);
+        e.y = (uint32_t)cvt_i32((float)__float_as_int(r.t_max));
+    } else {
+        e.x = r.parent;
+        e.y = (uint32_t)__float_as_int(r.t_max);
+    }
+    stk[(do_store ? s_push : dummy) * BLOCK] = e;
+    r.written |= do_store ? (1u << s_push) : 0u;
+
+    const int mx = descend ? (cidx & 1) : (step_mask & 1);
+    const int my = descend ? (cidx & 2) : (step_mask & 2);
+    const int mz = descend ? (cidx & 4) : (step_mask & 4);
+    const float delta = descend ? half : -r.scale_exp2;
+    const float qx = r.px + (mx ? delta : 0.0f);
+    const float qy = r.py + (my ? delta : 0.0f);
+    const float qz = r.pz + (mz ? delta : 0.0f);
+    const int new_idx = descend ? cidx : (r.idx ^ step_mask);
+    const uint32_t child = r.first + (uint32_t)__builtin_popcount(child_masks & 0x7Fu);
+    r.h = descend ? tc_max : r.h;
+    r.parent = descend ? child : r.parent;
+    r.t_max = descend ? tv_max : r.t_max;
+    r.t_min = descend ? r.t_min : tc_max;
+    r.cached = descend ? false : r.cached;
+    if (!descend && (new_idx & step_mask) != 0) {
+        // POP (N:134-154)
+        uint32_t differing = 0;
+        if (step_mask & 1) differing |= (uint32_t)(__float_as_int(qx) ^ __float_as_int(qx + r.scale_exp2));
+        if (step_mask & 2) differing |= (uint32_t)(__float_as_int(qy) ^ __float_as_int(qy + r.scale_exp2));
+        if (step_mask & 4) differing |= (uint32_t)(__float_as_int(qz) ^ __float_as_int(qz + r.scale_exp2));
+        const int scale = (__float_as_int((float)differing) >> 23) - 127;
+        r.scale = scale;
+        r.scale_exp2 = __int_as_float((scale - S_MAX + 127) << 23);
+        const int s = scale - scale_lo;   // in [0, slots]; slots == dummy only when leaving the root
+        const uint2 se = stk[s * BLOCK];
+        const bool ok = (r.written >> s) & 1u;
+        r.parent = ok ? se.x : 0u;
+        r.t_max = __int_as_float(ok ? (int32_t)se.y : 0);
+        const int32_t shx = __float_as_int(qx) >> scale;
+        const int32_t shy = __float_as_int(qy) >> scale;
+        const int32_t shz = __float_as_int(qz) >> scale;
+        r.px = __int_as_float((int32_t)((uint32_t)shx << scale));
+        r.py = __int_as_float((int32_t)((uint32_t)shy << scale));
+        r.pz = __int_as_float((int32_t)((uint32_t)shz << scale));
+        r.idx = (shx & 1) | ((shy & 1) << 1) | ((shz & 1) << 2);
+        r.h = 0.0f;
+        r.cached = false;
+        return r.scale >= S_MAX;
+    }
+    r.scale = descend ? r.scale - 1 : r.scale;
+    r.scale_exp2 = descend ? half : r.scale_exp2;
+    r.px = qx; r.py = qy; r.pz = qz;
+    r.idx = new_idx;
+    return false;
+}
+
 // N:158-186 hit decode; R:93-127 Shade; R:167 store
 __device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r_in, size_t out) {
     Ray r = r_in;
@@ -284,20 +380,39 @@ __device__ __forceinline__ int global_row(const LaunchParams &p, int lr) {
 }
 
 // ------------------------------------------------------------- tile kernel
-template <int MODE, bool COUNT>
-__global__ __launch_bounds__(BLOCK) void render_tile_kernel(LaunchParams p) {
+// 1-D grid of 16x16-pixel blocks (4 waves x 8x8).  Blocks are dealt round-robin
+// over the 8 XCDs (b and b + 8 share one, MI355X_MICROARCH.md "Workgroup
+// dispatch"); with xcd_remap the blocks that share an XCD cover one contiguous
+// band of screen tiles, so each XCD's private 4 MB L2 holds the SVO nodes of
+// its own screen band instead of every XCD caching the whole visible tree.
+// Placement only changes speed, never results.
+__device__ __forceinline__ int tile_of_block(int b, int nb, bool remap) {
+    if (!remap) return b;
+    const int q = nb / 8, rem = nb % 8, xcd = b % 8;   // bijective for any nb
+    return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / 8;
+}
+
+template <int MODE, bool COUNT, bool FLAT>
+__global__ __launch_bounds__(BLOCK) void render_tile_kernel(LaunchParams p, int blocks_x, int remap) {
     extern __shared__ uint2 stk_base[];   // [p.slots][BLOCK]
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int t = tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
+    const int bx = t % blocks_x, by = t / blocks_x;
+    const int x = bx * 16 + (wave & 1) * 8 + (lane & 7);
+    const int lr = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     if (x >= p.width || lr >= p.local_rows) return;
     Ray r;
     init_ray(p, x, global_row(p, lr), r);
     const int scale_lo = S_MAX - p.slots;
     uint2 *stk = stk_base + tid;
-    while (!step<MODE, COUNT>(p, r, stk, scale_lo)) {
+    if (FLAT) {
+        while (!step_flat<MODE, COUNT>(p, r, stk, scale_lo, p.slots)) {
+        }
+    } else {
+        while (!step<MODE, COUNT>(p, r, stk, scale_lo)) {
+        }
     }
     const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
     if (COUNT) { p.fetches[out] = r.fetches; return; }
@@ -349,7 +464,7 @@ __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(LaunchParams p
         // ---- trace until too few lanes remain busy ----
         for (;;) {
             if (active) {
-                if (step<MODE, COUNT>(p, r, stk, scale_lo)) {
+                if (step_flat<MODE, COUNT>(p, r, stk, scale_lo, p.slots)) {
                     const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
                     if (COUNT) p.fetches[out] = r.fetches;
                     else finish(p, r, out);
@@ -367,10 +482,15 @@ __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(LaunchParams p
 template <int MODE, bool COUNT>
 static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int kernel, uint32_t *counter,
                                  int max_blocks) {
-    const size_t lds = (size_t)p.slots * BLOCK * sizeof(uint2);
+    const size_t lds = (size_t)(p.slots + 1) * BLOCK * sizeof(uint2);   // + the dummy slot
     if (kernel == 0) {
-        dim3 grid((unsigned)((p.width + 15) / 16), (unsigned)((p.local_rows + 15) / 16));
-        hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT>), grid, dim3(BLOCK), lds, stream, p);
+        const int bx = (p.width + 15) / 16, by = (p.local_rows + 15) / 16;
+        if (p.flat)
+            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, true>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
+                               stream, p, bx, p.xcd_remap);
+        else
+            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, false>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
+                               stream, p, bx, p.xcd_remap);
         return hipGetLastError();
     }
     const int tiles_x = (p.width + 7) / 8;

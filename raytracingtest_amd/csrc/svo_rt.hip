@@ -74,6 +74,8 @@ struct svo_ctx {
     int kernel = 0;                  // 0 = tile (default), 1 = persistent; env SVO_KERNEL=tile|persistent
     int refill_at = 40;              // env SVO_REFILL
     int blocks_per_cu = 8;           // env SVO_BLOCKS_PER_CU
+    int xcd_remap = 0;               // env SVO_XCD_REMAP (measured slower: XCD load imbalance)
+    int flat = 1;                    // env SVO_FLAT
 };
 
 namespace {
@@ -215,6 +217,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.fetches = d_fetch;
     p.refill_at = ctx->refill_at;
     p.blocks_per_cu = ctx->blocks_per_cu;
+    p.xcd_remap = ctx->xcd_remap;
+    p.flat = ctx->flat;
     if (p.local_rows == 0) return SVO_OK;
     hipError_t e = svo::launch_render(p, stack_mode, stream ? stream : ctx->stream, ctx->kernel, ctx->d_counter,
                                       ctx->num_cus);
@@ -251,6 +255,8 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "persistent") == 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
+    if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));
     if (e != hipSuccess) {
         svo_destroy(ctx);

@@ -49,6 +49,8 @@ struct LaunchParams {
     uint32_t *fetches;    // nullable (instrumented launch)
     int refill_at;        // persistent kernel: refill idle lanes when fewer than this still trace
     int blocks_per_cu;    // persistent kernel: grid = CUs x this
+    int xcd_remap;        // tile kernel: give each XCD a contiguous screen band
+    int flat;             // 1: branch-flattened iteration (default), 0: branchy reference form
 };
 
 // kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).
