@@ -133,7 +133,7 @@ __device__ __forceinline__ void init_ray(const LaunchParams &p, int x, int y, Ra
 
 // One iteration of N:57-156.  Returns true when the ray is finished: a leaf hit
 // (r.scale < S_MAX) or a miss (r.scale >= S_MAX).
-template <int MODE, bool COUNT>
+template <int MODE, bool COUNT, int STRIDE = BLOCK>
 __device__ __forceinline__ bool step(const LaunchParams &p, Ray &r, uint2 *__restrict__ stk, int scale_lo) {
     if (r.scale >= S_MAX) return true;
     if (++r.iters > MAX_ITERS) { r.flags |= 2u; r.scale = S_MAX; return true; }
@@ -169,7 +169,7 @@ __device__ __forceinline__ bool step(const LaunchParams &p, Ray &r, uint2 *__res
                 e.x = r.parent;
                 e.y = (uint32_t)__float_as_int(r.t_max);
             }
-            stk[s * BLOCK] = e;
+            stk[s * STRIDE] = e;
             r.written |= 1u << s;
         }
         r.h = tc_max;
@@ -206,7 +206,7 @@ __device__ __forceinline__ bool step(const LaunchParams &p, Ray &r, uint2 *__res
             r.scale_exp2 = __int_as_float((scale - S_MAX + 127) << 23);
             const int s = scale - scale_lo;
             uint2 e = make_uint2(0u, 0u);
-            if (s >= 0 && s < 32 && ((r.written >> s) & 1u)) e = stk[s * BLOCK];
+            if (s >= 0 && s < 32 && ((r.written >> s) & 1u)) e = stk[s * STRIDE];
             r.parent = e.x;
             r.t_max = __int_as_float((int32_t)e.y);
             const int32_t shx = __float_as_int(qx) >> scale;
@@ -234,7 +234,7 @@ __device__ __forceinline__ bool step(const LaunchParams &p, Ray &r, uint2 *__res
 // the node fetch, POP and termination as divergent regions.  This removes most
 // of the exec-mask SALU traffic that dominated the branchy loop (SQ_INSTS_SALU
 // ~0.73 x SQ_INSTS_VALU on MI355X).
-template <int MODE, bool COUNT>
+template <int MODE, bool COUNT, int STRIDE = BLOCK>
 __device__ __forceinline__ bool step_flat(const LaunchParams &p, Ray &r, uint2 *__restrict__ stk, int scale_lo,
                                           int dummy) {
     if (++r.iters > MAX_ITERS) { r.flags |= 2u; r.scale = S_MAX; return true; }
@@ -275,7 +275,7 @@ __device__ __forceinline__ bool step_flat(const LaunchParams &p, Ray &r, uint2 *
         e.x = r.parent;
         e.y = (uint32_t)__float_as_int(r.t_max);
     }
-    stk[(do_store ? s_push : dummy) * BLOCK] = e;
+    stk[(do_store ? s_push : dummy) * STRIDE] = e;
     r.written |= do_store ? (1u << s_push) : 0u;
 
     const int mx = descend ? (cidx & 1) : (step_mask & 1);
@@ -302,7 +302,7 @@ __device__ __forceinline__ bool step_flat(const LaunchParams &p, Ray &r, uint2 *
         r.scale = scale;
         r.scale_exp2 = __int_as_float((scale - S_MAX + 127) << 23);
         const int s = scale - scale_lo;   // in [0, slots]; slots == dummy only when leaving the root
-        const uint2 se = stk[s * BLOCK];
+        const uint2 se = stk[s * STRIDE];
         const bool ok = (r.written >> s) & 1u;
         r.parent = ok ? se.x : 0u;
         r.t_max = __int_as_float(ok ? (int32_t)se.y : 0);
@@ -392,26 +392,27 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, bool remap) {
     return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / 8;
 }
 
-template <int MODE, bool COUNT, bool FLAT>
-__global__ __launch_bounds__(BLOCK) void render_tile_kernel(LaunchParams p, int blocks_x, int remap) {
-    extern __shared__ uint2 stk_base[];   // [p.slots][BLOCK]
+template <int MODE, bool COUNT, bool FLAT, int BS>
+__global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blocks_x, int remap) {
+    // BS = 256: a block is 16x16 pixels (4 waves of 8x8); BS = 64: one 8x8 wave.
+    extern __shared__ uint2 stk_base[];   // [p.slots + 1][BS]
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int t = tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
     const int bx = t % blocks_x, by = t / blocks_x;
-    const int x = bx * 16 + (wave & 1) * 8 + (lane & 7);
-    const int lr = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int x = BS == 256 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
+    const int lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
     if (x >= p.width || lr >= p.local_rows) return;
     Ray r;
     init_ray(p, x, global_row(p, lr), r);
     const int scale_lo = S_MAX - p.slots;
     uint2 *stk = stk_base + tid;
     if (FLAT) {
-        while (!step_flat<MODE, COUNT>(p, r, stk, scale_lo, p.slots)) {
+        while (!step_flat<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
         }
     } else {
-        while (!step<MODE, COUNT>(p, r, stk, scale_lo)) {
+        while (!step<MODE, COUNT, BS>(p, r, stk, scale_lo)) {
         }
     }
     const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
@@ -484,13 +485,24 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
                                  int max_blocks) {
     const size_t lds = (size_t)(p.slots + 1) * BLOCK * sizeof(uint2);   // + the dummy slot
     if (kernel == 0) {
+        if (p.block == 64) {
+            const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
+            const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
+            if (p.flat)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, true, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                                   lds64, stream, p, bx, p.xcd_remap);
+            else
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, false, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                                   lds64, stream, p, bx, p.xcd_remap);
+            return hipGetLastError();
+        }
         const int bx = (p.width + 15) / 16, by = (p.local_rows + 15) / 16;
         if (p.flat)
-            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, true>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
+            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, true, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
                                stream, p, bx, p.xcd_remap);
         else
-            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, false>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
-                               stream, p, bx, p.xcd_remap);
+            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, false, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK),
+                               lds, stream, p, bx, p.xcd_remap);
         return hipGetLastError();
     }
     const int tiles_x = (p.width + 7) / 8;

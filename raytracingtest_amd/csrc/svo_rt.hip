@@ -76,6 +76,7 @@ struct svo_ctx {
     int blocks_per_cu = 8;           // env SVO_BLOCKS_PER_CU
     int xcd_remap = 0;               // env SVO_XCD_REMAP (measured slower: XCD load imbalance)
     int flat = 1;                    // env SVO_FLAT
+    int block = 64;                  // env SVO_BLOCK (64 | 256)
 };
 
 namespace {
@@ -219,6 +220,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.blocks_per_cu = ctx->blocks_per_cu;
     p.xcd_remap = ctx->xcd_remap;
     p.flat = ctx->flat;
+    p.block = ctx->block;
     if (p.local_rows == 0) return SVO_OK;
     hipError_t e = svo::launch_render(p, stack_mode, stream ? stream : ctx->stream, ctx->kernel, ctx->d_counter,
                                       ctx->num_cus);
@@ -257,6 +259,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
     if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_BLOCK")) ctx->block = std::atoi(k) == 256 ? 256 : 64;
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));
     if (e != hipSuccess) {
         svo_destroy(ctx);
