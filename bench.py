@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--no-rgba", action="store_true")
     p.add_argument("--camera", choices=["flyover", "overview", "main"], default="flyover")
+    p.add_argument("--accumulate", action="store_true",
+                   help="samples mode: all-reduce the RGBA samples (progressive accumulation) every step")
     return p.parse_args()
 
 
@@ -62,12 +64,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL; SVO_BENCH_BACKEND=gloo + ranks sharing a GPU is
+    # only for rehearsing the N>1 plumbing on a one-GPU box
+    backend = os.environ.get("SVO_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from raytracingtest_amd import RaytracingMaster, band_rows
     from raytracingtest_amd.camera import CAMERAS, jitter_offsets
@@ -89,7 +95,7 @@ def main():
     else:
         off = (0.5, 0.5)
         band = (8, rank, world)
-        rows = len(band_rows(H, band))
+        rows = len(band_rows(H, band))   # == D.rank_band(rank, world)
     rm.UpdateShaderParameters(cam, W, H, pixel_offset=off)
 
     n_px = W * rows
@@ -99,18 +105,17 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
-    gathered = None
-    if args.split == "bands" and world > 1:
-        per = max(len(band_rows(H, (8, r, world))) for r in range(world)) * W * 24
-        gathered = [torch.empty(per, dtype=torch.uint8, device=dev) for _ in range(world)]
-        sendbuf = torch.zeros(per, dtype=torch.uint8, device=dev)
+    from raytracingtest_amd import distributed as D
+    gather = args.split == "bands" and world > 1
+    accumulate = args.split == "samples" and args.accumulate and world > 1 and rgba is not None
 
     def step():
         rm.render_device(W, H, rgba_ptr=None if rgba is None else rgba.data_ptr(), hits_ptr=hits.data_ptr(),
                          stack_mode=args.stack_mode, band=band, stream=sptr)
-        if gathered is not None:
-            sendbuf[:hits.numel()].copy_(hits)
-            dist.all_gather(gathered, sendbuf)
+        if gather:       # hit-record bands -> every rank (RCCL all_gather over xGMI)
+            D.gather_bands(hits, H, W, world, rank, 24, dist=dist)
+        if accumulate:   # AddShader progressive accumulation across the ranks' samples
+            D.accumulate_samples(rgba, world, dist=dist)
 
     # instrumented pass (outside the timed region): per-ray fetch counts
     fetch = torch.zeros(n_px, dtype=torch.int32, device=dev)
@@ -173,7 +178,7 @@ def main():
                        "svo_nodes": n_nodes, "svo_format": "V%d" % svo.format, "svo_leaves": getattr(svo, "n_leaves", None),
                        "build_s": round(build_s, 2), "stack_mode": "hlsl" if args.stack_mode == 0 else "exact",
                        "rays_per_gpu_step": n_px, "hit_fraction": round(n_hit / n_px, 4),
-                       "fetches_per_ray": round(F / n_px, 3), "parallelism": f"{args.split}{world}"},
+                       "fetches_per_ray": round(F / n_px, 3), "parallelism": f"{args.split}{world}" + ("+allreduce" if accumulate else "") + ("+allgather" if gather else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,

@@ -1,0 +1,98 @@
+"""World-size-2 gloo tests of the multi-GPU path on CPU.
+
+The per-rank renderer is the CPU oracle (test infrastructure) standing in for
+the HIP kernel, so the band split, the all-gather and the re-interleave of
+raytracingtest_amd.distributed are exercised exactly as bench.py uses them on
+RCCL; the GPU path of the band split itself is covered by
+test_gpu_parity.py::test_band_split_reassembles_frame."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from tests.conftest import GOLDEN, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, mode, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as orc
+    from raytracingtest_amd import SVOData, band_rows
+    from raytracingtest_amd import distributed as D
+    from raytracingtest_amd.camera import jitter_offsets, main_light, overview_camera
+    z = np.load(os.path.join(GOLDEN, "text_svo.npz"))
+    svo = SVOData.from_absolute(z["abs_child_ptr"], z["valid_mask"], z["nonleaf_mask"], z["normal_code"])
+    W, H = 96, 70
+    c2w, inv_proj = overview_camera().uniforms(W, H)
+    osvo = orc.OracleSVO(svo.childDescriptors, svo.attachments)
+    if mode == "bands":
+        cam = orc.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
+        band = D.rank_band(rank, world)
+        ys = band_rows(H, band)
+        pix = (ys[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
+        hits, _, _ = orc.render_pixels(osvo, cam, W, H, pix, nthreads=2)
+        local = torch.from_numpy(np.frombuffer(hits.tobytes(), np.uint8).copy())
+        parts = D.gather_bands(local, H, W, world, rank, 24)
+        if rank == 0:
+            frame = D.assemble([p.numpy() for p in parts], H, W, orc.HIT_DTYPE)
+            np.save(os.path.join(out_dir, "frame.npy"), frame)
+    else:
+        off = (0.5, 0.5) if rank == 0 else tuple(float(v) for v in jitter_offsets(world)[rank])
+        cam = orc.make_camera(c2w, inv_proj, off, main_light())
+        _, rgba, _ = orc.render(osvo, cam, W, H, nthreads=2)
+        t = torch.from_numpy(rgba.copy())
+        D.accumulate_samples(t, world)
+        if rank == 0:
+            np.save(os.path.join(out_dir, "accum.npy"), t.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["bands", "samples"])
+def test_two_rank_gloo(tmp_path, oracle_mod, text_svo, mode):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), mode, str(tmp_path)), nprocs=world, join=True)
+    from raytracingtest_amd.camera import jitter_offsets, main_light, overview_camera
+    W, H = 96, 70
+    c2w, inv_proj = overview_camera().uniforms(W, H)
+    osvo = oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments)
+    if mode == "bands":
+        cam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
+        ref, _, _ = oracle_mod.render(osvo, cam, W, H)
+        got = np.load(tmp_path / "frame.npy")
+        assert got.reshape(-1).tobytes() == ref.tobytes()
+    else:
+        acc = np.zeros((W * H, 4), np.float64)
+        for r in range(world):
+            off = (0.5, 0.5) if r == 0 else tuple(float(v) for v in jitter_offsets(world)[r])
+            cam = oracle_mod.make_camera(c2w, inv_proj, off, main_light())
+            _, rgba, _ = oracle_mod.render(osvo, cam, W, H)
+            acc += rgba
+        np.testing.assert_allclose(np.load(tmp_path / "accum.npy"), acc / world, rtol=1e-6, atol=1e-7)
+
+
+def test_band_helpers_cover_frame():
+    from raytracingtest_amd import band_rows
+    from raytracingtest_amd.distributed import assemble, max_band_len
+    for H, world in ((1080, 8), (1080, 3), (70, 2), (5, 4)):
+        seen = np.concatenate([band_rows(H, (8, r, world)) for r in range(world)])
+        assert np.array_equal(np.sort(seen), np.arange(H))
+        assert max_band_len(H, world) == max(len(band_rows(H, (8, r, world))) for r in range(world))
+    parts = [np.arange(len(band_rows(20, (8, r, 2))) * 3, dtype=np.int32) + 1000 * r for r in range(2)]
+    f = assemble(parts, 20, 3, np.int32)
+    assert f.shape == (20, 3) and f[0, 0] == 0 and f[8, 0] == 1000
