@@ -1,0 +1,87 @@
+// RaytracingMasterNative.cs -- Unity-side drop-in for Assets/Scripts/SVO/GPU/RaytracingMaster.cs
+// that drives the MI355X plugin (libsvo_rt.so, include/svo_rt.h) through P/Invoke instead of
+// ComputeShader.Dispatch.  NOT compiled in this repository (no C# toolchain in the build image);
+// it is the binding a Unity maintainer adds next to the reference script (see INTEGRATION.md).
+using System;
+using System.Runtime.InteropServices;
+using UnityEngine;
+
+public static class SvoNative {
+    const string Lib = "svo_rt";   // libsvo_rt.so in Assets/Plugins/x86_64
+
+    [StructLayout(LayoutKind.Sequential)]
+    public struct SvoHit { public uint parent; public byte hitIdx; public byte hitScale; public ushort flags;
+                           public float t, nx, ny, nz; }                          // 24 bytes == svo_hit
+
+    [DllImport(Lib)] public static extern int svo_create(int device, UIntPtr capacityNodes, out IntPtr ctx);
+    [DllImport(Lib)] public static extern int svo_set_buffer(IntPtr ctx, int[] desc, UIntPtr nDesc,
+                                                             uint[] att, UIntPtr nAtt, UIntPtr dstOffset);
+    [DllImport(Lib)] public static extern int svo_set_camera(IntPtr ctx, float[] c2w, float[] invProj,
+                                                             float pxOffX, float pxOffY, float[] light);
+    [DllImport(Lib)] public static extern int svo_render(IntPtr ctx, int width, int height, int stackMode,
+                                                         float[] rgbaOut, [Out] SvoHit[] hitsOut);
+    [DllImport(Lib)] public static extern int svo_destroy(IntPtr ctx);
+    [DllImport(Lib)] public static extern IntPtr svo_last_error();
+
+    public static void Check(int rc, string what) {
+        if (rc != 0) throw new InvalidOperationException(what + ": " + Marshal.PtrToStringAnsi(svo_last_error()));
+    }
+
+    // Unity Matrix4x4 is column-major in memory (m00, m10, m20, m30, m01, ...), which is the C-ABI order.
+    public static float[] ToArray(Matrix4x4 m) {
+        var a = new float[16];
+        for (int i = 0; i < 16; i++) a[i] = m[i];   // Matrix4x4 indexer is column-major
+        return a;
+    }
+}
+
+public class RaytracingMasterNative : MonoBehaviour {
+    public Light DirectionalLight;
+    [Range(1, 8)] public int maxLevel = 5;
+    public SampleFunctions.Type sampleType = SampleFunctions.Type.Custom1;
+
+    IntPtr _ctx;
+    Camera _camera;
+    Texture2D _frame;
+    float[] _rgba;
+
+    void Awake() {
+        _camera = GetComponent<Camera>();
+        InitializeSVOBuffer();
+    }
+
+    // RaytracingMaster.cs:111-116
+    public void InitializeSVOBuffer() {
+        SvoNative.Check(SvoNative.svo_create(0, (UIntPtr)(1073741824 / 8), out _ctx), "svo_create");
+    }
+
+    // RaytracingMaster.cs:118-135 (attachments land at 2*offset: the reference's offset bug is fixed)
+    public void SetSVOBuffer(RT.SVOData data, int offset = 0) {
+        var desc = data.childDescriptors.ToArray();
+        var att = data.attachments.ToArray();
+        SvoNative.Check(SvoNative.svo_set_buffer(_ctx, desc, (UIntPtr)desc.Length, att, (UIntPtr)att.Length,
+                                                 (UIntPtr)offset), "svo_set_buffer");
+    }
+
+    // RaytracingMaster.cs:32-41 + 60-74
+    void OnRenderImage(RenderTexture source, RenderTexture destination) {
+        Vector3 l = DirectionalLight.transform.forward;
+        SvoNative.Check(SvoNative.svo_set_camera(_ctx, SvoNative.ToArray(_camera.cameraToWorldMatrix),
+                                                 SvoNative.ToArray(_camera.projectionMatrix.inverse),
+                                                 UnityEngine.Random.value, UnityEngine.Random.value,
+                                                 new[] { l.x, l.y, l.z, DirectionalLight.intensity }), "svo_set_camera");
+        int w = Screen.width, h = Screen.height;
+        if (_frame == null || _frame.width != w || _frame.height != h) {
+            _frame = new Texture2D(w, h, TextureFormat.RGBAFloat, false, true);
+            _rgba = new float[w * h * 4];
+        }
+        SvoNative.Check(SvoNative.svo_render(_ctx, w, h, 0, _rgba, null), "svo_render");
+        _frame.SetPixelData(_rgba, 0);
+        _frame.Apply(false);
+        Graphics.Blit(_frame, destination);
+    }
+
+    void OnDestroy() {
+        if (_ctx != IntPtr.Zero) SvoNative.svo_destroy(_ctx);
+    }
+}
