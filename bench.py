@@ -159,7 +159,9 @@ def main():
 
     if rank == 0:
         cpu = cpu_baseline(args, svo, cam, off, host_hits) if (world == 1 and args.cpu_seconds > 0) else None
-        traffic = pmc_traffic()
+        workload = (f"C3 depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) Custom1 SVO, "
+                    f"{W}x{H} primary rays, {args.camera} camera")
+        traffic = pmc_traffic(workload)
         out = {
             "metric": METRIC,
             "value": round(mrays, 2),
@@ -173,8 +175,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement",
-            "config": {"workload": f"C3 depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) Custom1 SVO, "
-                                   f"{W}x{H} primary rays, {args.camera} camera",
+            "config": {"workload": workload,
                        "svo_nodes": n_nodes, "svo_format": "V%d" % svo.format, "svo_leaves": getattr(svo, "n_leaves", None),
                        "build_s": round(build_s, 2), "stack_mode": "hlsl" if args.stack_mode == 0 else "exact",
                        "rays_per_gpu_step": n_px, "hit_fraction": round(n_hit / n_px, 4),
@@ -193,16 +194,17 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
-    workload (profiles/pmc_summary.json), or None."""
+def pmc_traffic(workload):
+    """HBM bytes per launch of the render kernel from the committed rocprofv3 PMC
+    summary (profiles/pmc_summary.json, tools/pmc_summary.py) when it was taken
+    on this same workload, else None."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+    return d.get("hbm_bytes_per_launch") if d.get("workload") == workload else None
 
 
 def cpu_baseline(args, svo, cam, off, gpu_hits):
