@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--no-rgba", action="store_true")
     p.add_argument("--camera", choices=["flyover", "overview", "main"], default="flyover")
+    p.add_argument("--shadows", action="store_true", help="C3 '+1 shadow ray' pass after the primary rays")
     p.add_argument("--accumulate", action="store_true",
                    help="samples mode: all-reduce the RGBA samples (progressive accumulation) every step")
     return p.parse_args()
@@ -97,6 +98,8 @@ def main():
         band = (8, rank, world)
         rows = len(band_rows(H, band))   # == D.rank_band(rank, world)
     rm.UpdateShaderParameters(cam, W, H, pixel_offset=off)
+    if args.shadows:
+        rm.SetShadowRays(True)
 
     n_px = W * rows
     hits = torch.empty(n_px * 24, dtype=torch.uint8, device=dev)
@@ -160,7 +163,8 @@ def main():
     if rank == 0:
         cpu = cpu_baseline(args, svo, cam, off, host_hits) if (world == 1 and args.cpu_seconds > 0) else None
         workload = (f"C3 depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) Custom1 SVO, "
-                    f"{W}x{H} primary rays, {args.camera} camera")
+                    f"{W}x{H} primary rays" + (" + 1 shadow ray per hit" if args.shadows else "") +
+                    f", {args.camera} camera")
         traffic = pmc_traffic(workload)
         out = {
             "metric": METRIC,
@@ -185,7 +189,8 @@ def main():
                          "traffic": traffic,
                          "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
                          "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "bytes_formula": "8*F + 8*hits + 24*rays + 16*rays(rgba)"},
+                         "bytes_formula": "8*F + 8*hits + 24*rays + 16*rays(rgba)" +
+                                          (" (primary pass only; kernel_ms covers both passes)" if args.shadows else "")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -43,7 +43,7 @@ typedef struct svo_hit {
     uint32_t parent;     /* descriptor holding the hit leaf (NVIDIASVO.compute:177); 0xFFFFFFFF = miss */
     uint8_t  hit_idx;    /* child slot of the hit leaf = idx ^ octant_mask ^ 7 (:176) */
     uint8_t  hit_scale;  /* leaf scale, 23 - depth */
-    uint16_t flags;      /* bit0 hit, bit1 iteration cap, bit2 stack overflow */
+    uint16_t flags;      /* bit0 hit, bit1 iteration cap, bit2 stack overflow, bit3 in shadow */
     float    t;          /* bestHit.distance = 2048 * t_min (:163,171); +inf on miss */
     float    nx, ny, nz; /* normalize(decodeNormal(att[2*parent+1] >> 16)) (:177-182) */
 } svo_hit;
@@ -101,6 +101,14 @@ int svo_render_device(svo_ctx *ctx, int width, int height, int stack_mode,
  * of the roofline.  Same arguments as svo_render_device plus d_fetches. */
 int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode,
                       const svo_band *band, void *d_fetches, void *stream);
+
+/* Render options (bit set).  SVO_OPT_SHADOW_RAYS: after the primary pass,
+ * trace one shadow ray per hit toward -_DirectionalLight (SURVEY.md 8(d) C3;
+ * the reference's shadow test is commented out at RaytraceCompute.compute:105-112):
+ * origin = world hit point + 0.001 * normal; an occluded pixel gets hit flag
+ * bit 3 and a black Result. */
+enum { SVO_OPT_SHADOW_RAYS = 1 };
+int svo_set_options(svo_ctx *ctx, uint32_t options);
 
 /* Information about the uploaded pool. */
 int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device);

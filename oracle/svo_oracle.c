@@ -291,6 +291,24 @@ static void shade_pixel(const orc_camera *cam, const orc_hit *hit, const float a
     out[3] = 1.0f;
 }
 
+/* Shadow ray of a primary hit (the reference's commented-out
+ * test RaytraceCompute.compute:105-112 with a corrected origin): world hit point
+ * P = o + (t / 64) * d (t = 2048 * t_svo, world distance = 32 * t_svo), origin
+ * P + 0.001 * n, direction -L.  Returns 1 when the shadow ray hits a voxel. */
+int orc_shadow_ray(const orc_svo *svo, const orc_camera *cam, const float o[3], const float d[3],
+                   const orc_hit *h, int mode) {
+    const float tw = h->t * (1.0f / 64.0f);
+    const float n[3] = { h->nx, h->ny, h->nz };
+    float so[3], sd[3];
+    for (int k = 0; k < 3; ++k) {
+        float pk = o[k] + tw * d[k];
+        so[k] = pk + n[k] * 0.001f;
+        sd[k] = -cam->light[k];
+    }
+    orc_hit sh;
+    return orc_intersect(svo, so, sd, mode & 0xFF, &sh, NULL, NULL, NULL);
+}
+
 static void trace_pixel(const orc_svo *svo, const orc_camera *cam, int width, int height,
                         uint32_t x, uint32_t y, int mode, orc_hit *hit_out, float *rgba_out,
                         uint32_t *fetch_out) {
@@ -298,9 +316,17 @@ static void trace_pixel(const orc_svo *svo, const orc_camera *cam, int width, in
     orc_hit h;
     uint32_t f = 0;
     orc_camera_ray(cam, x, y, width, height, o, d);
-    orc_intersect(svo, o, d, mode, &h, alb, &f, NULL);
+    orc_intersect(svo, o, d, mode & 0xFF, &h, alb, &f, NULL);
+    int shadowed = 0;
+    if ((mode & ORC_SHADOW_RAYS) && (h.flags & 1)) {
+        shadowed = orc_shadow_ray(svo, cam, o, d, &h, mode);
+        if (shadowed) h.flags |= 8;   /* bit3: in shadow */
+    }
     if (hit_out) *hit_out = h;
-    if (rgba_out) shade_pixel(cam, &h, alb, d, rgba_out);
+    if (rgba_out) {
+        shade_pixel(cam, &h, alb, d, rgba_out);
+        if (shadowed) { rgba_out[0] = 0.0f; rgba_out[1] = 0.0f; rgba_out[2] = 0.0f; }   /* :109-111 */
+    }
     if (fetch_out) *fetch_out = f;
 }
 

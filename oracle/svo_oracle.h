@@ -40,13 +40,15 @@ enum { ORC_FMT_V1 = 1, ORC_FMT_V2 = 2 };
  *  HLSL : stack entries round-trip through float2 as in NVIDIASVO.compute:98.
  *  EXACT: exact (parent, t_max) entries (Laine-Karras / C# tracer). */
 enum { ORC_STACK_HLSL = 0, ORC_STACK_EXACT = 1 };
+/* OR-ed into the render mode: trace one shadow ray per primary hit. */
+#define ORC_SHADOW_RAYS 0x100
 
 /* Per-pixel hit record: identical layout to svo_hit in include/svo_rt.h. */
 typedef struct orc_hit {
     uint32_t parent;    /* descriptor index holding the hit leaf, 0xFFFFFFFF = miss */
     uint8_t  hit_idx;   /* child slot of the leaf inside `parent` (NVIDIASVO.compute:176) */
     uint8_t  hit_scale; /* leaf scale (23 - depth) */
-    uint16_t flags;     /* bit0 hit, bit1 iteration cap reached */
+    uint16_t flags;     /* bit0 hit, bit1 iteration cap, bit2 stack overflow, bit3 in shadow */
     float    t;         /* bestHit.distance = 2048 * t_min (NVIDIASVO.compute:163,171); +inf on miss */
     float    nx, ny, nz;/* normalize(decodeNormal(att[2p+1] >> 16)) (NVIDIASVO.compute:177-182) */
 } orc_hit;
@@ -79,6 +81,10 @@ int  orc_intersect(const orc_svo *svo, const float origin[3], const float dir[3]
                    orc_hit *hit, float albedo[3], uint32_t *fetches, uint32_t *iters);
 
 void orc_sky(const float dir[3], float out[3]);
+
+/* Shadow ray toward -L from a primary hit; 1 if occluded (see svo_oracle.c). */
+int  orc_shadow_ray(const orc_svo *svo, const orc_camera *cam, const float o[3], const float d[3],
+                    const orc_hit *hit, int stack_mode);
 
 /* Render rows [y0, y1) of a width x height frame with `nthreads` threads.
  * hits / rgba / fetches are indexed by (y - y0) * width + x and are nullable. */

@@ -92,17 +92,20 @@ struct Ray {
     bool cached;
 };
 
-// R:151 uv, R:129-141 CreateCameraRay, N:15-54 setup
-__device__ __forceinline__ void init_ray(const LaunchParams &p, int x, int y, Ray &r) {
+// R:151 uv, R:129-141 CreateCameraRay
+__device__ __forceinline__ void camera_ray(const LaunchParams &p, int x, int y, float org[3], float dir[3]) {
     const float u = ((float)x + p.cam.px_off[0]) / (float)p.width * 2.0f - 1.0f;
     const float v = ((float)y + p.cam.px_off[1]) / (float)p.height * 2.0f - 1.0f;
-    float org[3], pd[3], dir[3];
+    float pd[3];
     mul4(p.cam.c2w, 0.0f, 0.0f, 0.0f, 1.0f, org);
     mul4(p.cam.inv_proj, u, v, 0.0f, 1.0f, pd);
     mul4(p.cam.c2w, pd[0], pd[1], pd[2], 0.0f, dir);
     normalize3(dir);
-    r.dir_y = dir[1];
+}
 
+// N:15-54 setup for a ray (origin, direction) in world space
+__device__ __forceinline__ void setup_ray(const float org[3], const float dir[3], Ray &r) {
+    r.dir_y = dir[1];
     float ox = org[0] * (1.0f / 32.0f), oy = org[1] * (1.0f / 32.0f), oz = org[2] * (1.0f / 32.0f);
     ox = ox + 1.5f; oy = oy + 1.5f; oz = oz + 1.5f;
     r.tx_coef = 1.0f / -fabsf(dir[0]);
@@ -129,6 +132,12 @@ __device__ __forceinline__ void init_ray(const LaunchParams &p, int x, int y, Ra
     if (1.5f * r.ty_coef - r.ty_bias > r.t_min) { r.idx ^= 2; r.py = 1.5f; }
     if (1.5f * r.tz_coef - r.tz_bias > r.t_min) { r.idx ^= 4; r.pz = 1.5f; }
     r.written = 0; r.fetches = 0; r.iters = 0; r.flags = 0;
+}
+
+__device__ __forceinline__ void init_ray(const LaunchParams &p, int x, int y, Ray &r) {
+    float org[3], dir[3];
+    camera_ray(p, x, y, org, dir);
+    setup_ray(org, dir, r);
 }
 
 // One iteration of N:57-156.  Returns true when the ray is finished: a leaf hit
@@ -420,6 +429,48 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     finish(p, r, out);
 }
 
+// ------------------------------------------------------------- shadow pass
+// One shadow ray per primary hit (the reference's test is
+// commented out at RaytraceCompute.compute:105-112): world hit point
+// P = o + (t / 64) d, origin P + 0.001 n, direction -L.  An occluded pixel gets
+// flag bit 3 and a black Result (:109-111).  Runs over the same 8x8 tiles as
+// the primary pass: sky tiles retire at once, so no compaction pass is needed.
+template <int MODE, int BS>
+__global__ __launch_bounds__(BS) void shadow_tile_kernel(LaunchParams p, int blocks_x) {
+    extern __shared__ uint2 stk_base[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int t = (int)blockIdx.x;
+    const int x = (t % blocks_x) * 8 + (lane & 7);
+    const int lr = (t / blocks_x) * 8 + (lane >> 3);
+    if (x >= p.width || lr >= p.local_rows) return;
+    const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
+    uint2 *rec = reinterpret_cast<uint2 *>(p.hits + out);
+    const uint2 w01 = rec[0], w23 = rec[1], w45 = rec[2];
+    if (!((w01.y >> 16) & 1u)) return;
+    float org[3], dir[3];
+    camera_ray(p, x, global_row(p, lr), org, dir);
+    const float tw = __int_as_float((int32_t)w23.x) * (1.0f / 64.0f);
+    const float n[3] = { __int_as_float((int32_t)w23.y), __int_as_float((int32_t)w45.x), __int_as_float((int32_t)w45.y) };
+    float so[3], sd[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float pk = org[k] + tw * dir[k];
+        so[k] = pk + n[k] * 0.001f;
+        sd[k] = -p.cam.light[k];
+    }
+    Ray r;
+    setup_ray(so, sd, r);
+    const int scale_lo = S_MAX - p.slots;
+    uint2 *stk = stk_base + tid;
+    while (!step_flat<MODE, false, BS>(p, r, stk, scale_lo, p.slots)) {
+    }
+    if (r.scale < S_MAX) {   // occluded
+        rec[0] = make_uint2(w01.x, w01.y | (8u << 16));
+        if (p.rgba) p.rgba[out] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+    }
+}
+
 // ------------------------------------------------------- persistent kernel
 
 template <int MODE, bool COUNT>
@@ -519,9 +570,23 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
     return hipGetLastError();
 }
 
+template <int MODE>
+static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
+    const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
+    const size_t lds = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
+    hipLaunchKernelGGL((shadow_tile_kernel<MODE, 64>), dim3((unsigned)(bx * by)), dim3(64), lds, stream, p, bx);
+    return hipGetLastError();
+}
+
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel, uint32_t *counter,
                          int num_cus) {
     const bool count = p.fetches != nullptr;
+    if (!count && p.shadows && p.hits) {
+        hipError_t e = stack_mode == 0 ? launch_variant<0, false>(p, stream, kernel, counter, num_cus)
+                                       : launch_variant<1, false>(p, stream, kernel, counter, num_cus);
+        if (e != hipSuccess) return e;
+        return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
+    }
     if (stack_mode == 0)
         return count ? launch_variant<0, true>(p, stream, kernel, counter, num_cus)
                      : launch_variant<0, false>(p, stream, kernel, counter, num_cus);

@@ -77,6 +77,7 @@ struct svo_ctx {
     int xcd_remap = 0;               // env SVO_XCD_REMAP (measured slower: XCD load imbalance)
     int flat = 1;                    // env SVO_FLAT
     int block = 64;                  // env SVO_BLOCK (64 | 256)
+    uint32_t options = 0;            // svo_set_options
 };
 
 namespace {
@@ -221,7 +222,13 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.xcd_remap = ctx->xcd_remap;
     p.flat = ctx->flat;
     p.block = ctx->block;
+    p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? 1 : 0;
     if (p.local_rows == 0) return SVO_OK;
+    if (p.shadows && !p.hits && !p.fetches) {   // the shadow pass reads the primary hit records
+        int rc2 = ensure_out(ctx, (size_t)p.local_rows * (size_t)width);
+        if (rc2) return rc2;
+        p.hits = reinterpret_cast<svo::Hit *>(ctx->d_out_hits);
+    }
     hipError_t e = svo::launch_render(p, stack_mode, stream ? stream : ctx->stream, ctx->kernel, ctx->d_counter,
                                       ctx->num_cus);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
@@ -370,6 +377,13 @@ int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode, const
     if (!d_fetches) return fail(SVO_ERR_ARG, "d_fetches is null");
     return launch(ctx, width, height, stack_mode, band, nullptr, nullptr,
                   reinterpret_cast<uint32_t *>(d_fetches), reinterpret_cast<hipStream_t>(stream));
+}
+
+int svo_set_options(svo_ctx *ctx, uint32_t options) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (options & ~(uint32_t)SVO_OPT_SHADOW_RAYS) return fail(SVO_ERR_ARG, "unknown option bits");
+    ctx->options = options;
+    return SVO_OK;
 }
 
 int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device) {

@@ -52,6 +52,7 @@ struct LaunchParams {
     int xcd_remap;        // tile kernel: give each XCD a contiguous screen band
     int flat;             // 1: branch-flattened iteration (default), 0: branchy reference form
     int block;            // tile kernel workgroup size: 64 (one 8x8 wave) or 256 (16x16 pixels)
+    int shadows;          // 1: second pass, one shadow ray per primary hit (needs hits)
 };
 
 // kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).

@@ -76,6 +76,11 @@ class RaytracingMaster:
                                         float(pixel_offset[1]), lt.ctypes.data), "svo_set_camera")
         self._camera_set = True
 
+    def SetShadowRays(self, enable=True):
+        """Trace one shadow ray per primary hit toward -_DirectionalLight (the
+        reference's commented-out test, RaytraceCompute.compute:105-112)."""
+        check(_lib.lib().svo_set_options(self._ctx, _lib.SVO_OPT_SHADOW_RAYS if enable else 0), "svo_set_options")
+
     # ----------------------------------------------------------------- render
     def Render(self, width, height, stack_mode=STACK_HLSL, want_rgba=True, want_hits=True):
         """Blocking render into host arrays: (rgba[H, W, 4] float32, hits[H, W] svo_hit)."""

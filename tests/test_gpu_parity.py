@@ -26,14 +26,14 @@ def rm():
     m.close()
 
 
-def _oracle_render(oracle_mod, svo, camera, w, h, mode=0, off=(0.5, 0.5), nodes=False):
+def _oracle_render(oracle_mod, svo, camera, w, h, mode=0, off=(0.5, 0.5), nodes=False, shadows=False):
     c2w, inv_proj = camera.uniforms(w, h)
     cam = oracle_mod.make_camera(c2w, inv_proj, off, main_light())
     if nodes or svo.format == 2:
         osvo = oracle_mod.OracleSVO(nodes=svo.to_v2(), attachments=svo.attachments)
     else:
         osvo = oracle_mod.OracleSVO(svo.childDescriptors, svo.attachments)
-    return oracle_mod.render(osvo, cam, w, h, mode)
+    return oracle_mod.render(osvo, cam, w, h, mode | (oracle_mod.SHADOW_RAYS if shadows else 0))
 
 
 def _compare(got_hits, got_rgba, ref_hits, ref_rgba):
@@ -211,3 +211,23 @@ def test_tile_and_persistent_kernels_identical(oracle_mod, text_svo, monkeypatch
             m.close()
     assert outs[0][1].tobytes() == outs[1][1].tobytes()
     assert outs[0][0].tobytes() == outs[1][0].tobytes()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_shadow_rays_parity(rm, oracle_mod, mode):
+    """C3's '+1 shadow ray' pass: occlusion flag and black
+    Result identical to the oracle, on the 256^3 Menger and random terrain."""
+    svo = build_menger(8)
+    cam = overview_camera()
+    w, h = 400, 240
+    rm.SetSVOBuffer(svo)
+    rm.UpdateShaderParameters(cam, w, h)
+    rm.SetShadowRays(True)
+    try:
+        rgba, hits = rm.Render(w, h, stack_mode=mode)
+    finally:
+        rm.SetShadowRays(False)
+    ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, svo, cam, w, h, mode, shadows=True)
+    n_sh = int(np.count_nonzero(ref_hits["flags"] & 8))
+    assert 0 < n_sh < np.count_nonzero(ref_hits["flags"] & 1)
+    _compare(hits, rgba, ref_hits, ref_rgba)
