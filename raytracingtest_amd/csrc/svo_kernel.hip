@@ -403,14 +403,14 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, bool remap) {
 
 template <int MODE, bool COUNT, bool FLAT, int BS>
 __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blocks_x, int remap) {
-    // BS = 256: a block is 16x16 pixels (4 waves of 8x8); BS = 64: one 8x8 wave.
+    // BS = 256: a block is 16x16 pixels (4 waves of 8x8); 128: 16x8 (2 waves); 64: one 8x8 wave.
     extern __shared__ uint2 stk_base[];   // [p.slots + 1][BS]
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int t = tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
     const int bx = t % blocks_x, by = t / blocks_x;
-    const int x = BS == 256 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
+    const int x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
     const int lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
     if (x >= p.width || lr >= p.local_rows) return;
     Ray r;
@@ -536,6 +536,17 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
                                  int max_blocks) {
     const size_t lds = (size_t)(p.slots + 1) * BLOCK * sizeof(uint2);   // + the dummy slot
     if (kernel == 0) {
+        if (p.block == 128) {
+            const int bx = (p.width + 15) / 16, by = (p.local_rows + 7) / 8;
+            const size_t lds128 = (size_t)(p.slots + 1) * 128 * sizeof(uint2);
+            if (p.flat)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, true, 128>), dim3((unsigned)(bx * by)), dim3(128),
+                                   lds128, stream, p, bx, p.xcd_remap);
+            else
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, false, 128>), dim3((unsigned)(bx * by)),
+                                   dim3(128), lds128, stream, p, bx, p.xcd_remap);
+            return hipGetLastError();
+        }
         if (p.block == 64) {
             const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
             const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
