@@ -90,6 +90,7 @@ struct Ray {
     int idx, octant_mask, scale, iters;
     uint32_t flags;
     bool cached;
+    uint2 nd;                  // prefetched node (step_pf): issued when the parent changes
 };
 
 // R:151 uv, R:129-141 CreateCameraRay
@@ -333,6 +334,97 @@ __device__ __forceinline__ bool step_flat(const LaunchParams &p, Ray &r, uint2 *
     return false;
 }
 
+template <int MODE, bool COUNT, int STRIDE = BLOCK>
+__device__ __forceinline__ bool step_pf(const LaunchParams &p, Ray &r, uint2 *__restrict__ stk, int scale_lo,
+                                          int dummy) {
+    if (++r.iters > MAX_ITERS) { r.flags |= 2u; r.scale = S_MAX; return true; }
+    if (!r.cached) {                                       // N:60-62 (load issued one step early)
+        r.cd = r.nd.x;
+        r.first = r.nd.y;
+        r.cached = (r.nd.x | r.nd.y) != 0u;
+        if (COUNT) ++r.fetches;
+    }
+    const float tx_corner = r.px * r.tx_coef - r.tx_bias;
+    const float ty_corner = r.py * r.ty_coef - r.ty_bias;
+    const float tz_corner = r.pz * r.tz_coef - r.tz_bias;
+    const float tc_max = fminf(fminf(tx_corner, ty_corner), tz_corner);
+    const uint32_t child_masks = r.cd << (r.idx ^ r.octant_mask);
+    const float tv_max = fminf(r.t_max, tc_max);
+    const bool descend = (child_masks & 0x8000u) != 0u && r.t_min <= r.t_max && r.t_min <= tv_max;
+    const bool do_store = descend && tc_max < r.h;
+    const int s_push = r.scale - scale_lo;
+    if ((descend && (child_masks & 0x0080u) == 0u) || (do_store && s_push < 0)) {
+        if (!(descend && (child_masks & 0x0080u) == 0u)) { r.flags |= 4u; r.scale = S_MAX; }
+        return true;                                       // leaf hit (N:93-94) or stack overflow
+    }
+    const float half = r.scale_exp2 * 0.5f;
+    // PUSH candidate (N:83-117)
+    const float tx_center = half * r.tx_coef + tx_corner;
+    const float ty_center = half * r.ty_coef + ty_corner;
+    const float tz_center = half * r.tz_coef + tz_corner;
+    const int cidx = (tx_center > r.t_min ? 1 : 0) | (ty_center > r.t_min ? 2 : 0) | (tz_center > r.t_min ? 4 : 0);
+    // ADVANCE candidate (N:122-128)
+    const int step_mask = (tx_corner <= tc_max ? 1 : 0) | (ty_corner <= tc_max ? 2 : 0) | (tz_corner <= tc_max ? 4 : 0);
+    // stack store (N:97-98); lanes that do not push write their dummy slot
+    uint2 e;
+    if (MODE == 0) {   // int2 <- float2((int)parent, asint(t_max))
+        e.x = (uint32_t)cvt_i32((float)(int32_t)r.parent);
+        e.y = (uint32_t)cvt_i32((float)__float_as_int(r.t_max));
+    } else {
+        e.x = r.parent;
+        e.y = (uint32_t)__float_as_int(r.t_max);
+    }
+    stk[(do_store ? s_push : dummy) * STRIDE] = e;
+    r.written |= do_store ? (1u << s_push) : 0u;
+
+    const int mx = descend ? (cidx & 1) : (step_mask & 1);
+    const int my = descend ? (cidx & 2) : (step_mask & 2);
+    const int mz = descend ? (cidx & 4) : (step_mask & 4);
+    const float delta = descend ? half : -r.scale_exp2;
+    const float qx = r.px + (mx ? delta : 0.0f);
+    const float qy = r.py + (my ? delta : 0.0f);
+    const float qz = r.pz + (mz ? delta : 0.0f);
+    const int new_idx = descend ? cidx : (r.idx ^ step_mask);
+    const uint32_t child = r.first + (uint32_t)__builtin_popcount(child_masks & 0x7Fu);
+    r.h = descend ? tc_max : r.h;
+    r.parent = descend ? child : r.parent;
+    r.t_max = descend ? tv_max : r.t_max;
+    r.t_min = descend ? r.t_min : tc_max;
+    r.cached = descend ? false : r.cached;
+    if (!descend && (new_idx & step_mask) != 0) {
+        // POP (N:134-154)
+        uint32_t differing = 0;
+        if (step_mask & 1) differing |= (uint32_t)(__float_as_int(qx) ^ __float_as_int(qx + r.scale_exp2));
+        if (step_mask & 2) differing |= (uint32_t)(__float_as_int(qy) ^ __float_as_int(qy + r.scale_exp2));
+        if (step_mask & 4) differing |= (uint32_t)(__float_as_int(qz) ^ __float_as_int(qz + r.scale_exp2));
+        const int scale = (__float_as_int((float)differing) >> 23) - 127;
+        r.scale = scale;
+        r.scale_exp2 = __int_as_float((scale - S_MAX + 127) << 23);
+        const int s = scale - scale_lo;   // in [0, slots]; slots == dummy only when leaving the root
+        const uint2 se = stk[s * STRIDE];
+        const bool ok = (r.written >> s) & 1u;
+        r.parent = ok ? se.x : 0u;
+        r.t_max = __int_as_float(ok ? (int32_t)se.y : 0);
+        const int32_t shx = __float_as_int(qx) >> scale;
+        const int32_t shy = __float_as_int(qy) >> scale;
+        const int32_t shz = __float_as_int(qz) >> scale;
+        r.px = __int_as_float((int32_t)((uint32_t)shx << scale));
+        r.py = __int_as_float((int32_t)((uint32_t)shy << scale));
+        r.pz = __int_as_float((int32_t)((uint32_t)shz << scale));
+        r.idx = (shx & 1) | ((shy & 1) << 1) | ((shz & 1) << 2);
+        r.h = 0.0f;
+        r.cached = false;
+        if (r.scale < S_MAX) r.nd = p.nodes[r.parent];   // prefetch the popped parent
+        return r.scale >= S_MAX;
+    }
+    r.scale = descend ? r.scale - 1 : r.scale;
+    r.scale_exp2 = descend ? half : r.scale_exp2;
+    r.px = qx; r.py = qy; r.pz = qz;
+    r.idx = new_idx;
+    if (!r.cached) r.nd = p.nodes[r.parent];             // prefetch the child (or re-fetch an empty root)
+    return false;
+}
+
 // N:158-186 hit decode; R:93-127 Shade; R:167 store
 __device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r_in, size_t out) {
     Ray r = r_in;
@@ -401,7 +493,7 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, bool remap) {
     return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / 8;
 }
 
-template <int MODE, bool COUNT, bool FLAT, int BS>
+template <int MODE, bool COUNT, int STEP, int BS>
 __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blocks_x, int remap) {
     // BS = 256: a block is 16x16 pixels (4 waves of 8x8); 128: 16x8 (2 waves); 64: one 8x8 wave.
     extern __shared__ uint2 stk_base[];   // [p.slots + 1][BS]
@@ -417,7 +509,11 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     init_ray(p, x, global_row(p, lr), r);
     const int scale_lo = S_MAX - p.slots;
     uint2 *stk = stk_base + tid;
-    if (FLAT) {
+    if (STEP == 2) {
+        r.nd = p.nodes[0];
+        while (!step_pf<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
+        }
+    } else if (STEP == 1) {
         while (!step_flat<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
         }
     } else {
@@ -540,30 +636,33 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
             const int bx = (p.width + 15) / 16, by = (p.local_rows + 7) / 8;
             const size_t lds128 = (size_t)(p.slots + 1) * 128 * sizeof(uint2);
             if (p.flat)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, true, 128>), dim3((unsigned)(bx * by)), dim3(128),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 128>), dim3((unsigned)(bx * by)), dim3(128),
                                    lds128, stream, p, bx, p.xcd_remap);
             else
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, false, 128>), dim3((unsigned)(bx * by)),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 128>), dim3((unsigned)(bx * by)),
                                    dim3(128), lds128, stream, p, bx, p.xcd_remap);
             return hipGetLastError();
         }
         if (p.block == 64) {
             const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
             const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
-            if (p.flat)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, true, 64>), dim3((unsigned)(bx * by)), dim3(64),
+            if (p.flat == 2)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 2, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                                   lds64, stream, p, bx, p.xcd_remap);
+            else if (p.flat)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 64>), dim3((unsigned)(bx * by)), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, false, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 64>), dim3((unsigned)(bx * by)), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             return hipGetLastError();
         }
         const int bx = (p.width + 15) / 16, by = (p.local_rows + 15) / 16;
         if (p.flat)
-            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, true, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
+            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
                                stream, p, bx, p.xcd_remap);
         else
-            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, false, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK),
+            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK),
                                lds, stream, p, bx, p.xcd_remap);
         return hipGetLastError();
     }

@@ -265,7 +265,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "persistent") == 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
     if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(2, std::atoi(k)));
     if (const char *k = std::getenv("SVO_BLOCK")) { const int b = std::atoi(k); ctx->block = (b == 256 || b == 128) ? b : 64; }
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));
     if (e != hipSuccess) {
