@@ -656,6 +656,19 @@ int surface_leaves_gpu(int device, int type, int max_level, std::vector<uint64_t
     return SVOB_OK;
 }
 
+// Empty tree: CompressSVO's placeholder descriptor 0 stays 0; the root's
+// attachment still encodes its default normal Vector3.up (Node ctor, Util.cs)
+// with no children (NaiveCreator.cs:132-136, 195-257).
+int empty_tree(int depth, svob_result *out) {
+    out->n_nodes = 1; out->depth = depth; out->v1_ok = 1; out->n_leaves = 0;
+    out->nodes = (uint64_t *)std::calloc(1, sizeof(uint64_t));
+    out->attachments = (uint32_t *)std::calloc(2, sizeof(uint32_t));
+    out->descriptors = (int32_t *)std::calloc(1, sizeof(int32_t));
+    if (!out->nodes || !out->attachments || !out->descriptors) return fail(SVOB_ERR_MEM, "out of host memory");
+    out->attachments[1] = encode_normal16({ 0.0f, 1.0f, 0.0f }) << 16;
+    return SVOB_OK;
+}
+
 int check_sampler(int type, int max_level) {
     if (type == 3) return fail(SVOB_ERR_ARG, "RotatedCuboid sampler is not supported yet");
     if (type < 0 || type > 4) return fail(SVOB_ERR_ARG, "unknown sampler");
@@ -746,13 +759,7 @@ int svob_build_from_leaves(int depth, size_t n_leaves, const uint32_t *xyz, cons
     std::sort(order.begin(), order.end());
     for (size_t i = 1; i < n_leaves; ++i)
         if (order[i].first == order[i - 1].first) return fail(SVOB_ERR_ARG, "duplicate leaf coordinates");
-    if (n_leaves == 0) {   // empty tree: a single zero descriptor (CompressSVO placeholder)
-        out->n_nodes = 1; out->depth = depth; out->v1_ok = 1;
-        out->nodes = (uint64_t *)std::calloc(1, sizeof(uint64_t));
-        out->attachments = (uint32_t *)std::calloc(2, sizeof(uint32_t));
-        out->descriptors = (int32_t *)std::calloc(1, sizeof(int32_t));
-        return SVOB_OK;
-    }
+    if (n_leaves == 0) return empty_tree(depth, out);
     std::vector<uint64_t> codes(n_leaves);
     std::vector<V3> nrm(n_leaves), col(n_leaves);
     const float inv = std::ldexp(1.0f, -depth);
@@ -776,13 +783,7 @@ int svob_build_sampler(int device, int sampler, int max_level, svob_result *out)
     rc = surface_leaves_gpu(device, sampler, max_level, codes, normals);
     if (rc) return rc;
     const int depth = max_level - 1;
-    if (codes.empty()) {
-        out->n_nodes = 1; out->depth = depth; out->v1_ok = 1;
-        out->nodes = (uint64_t *)std::calloc(1, sizeof(uint64_t));
-        out->attachments = (uint32_t *)std::calloc(2, sizeof(uint32_t));
-        out->descriptors = (int32_t *)std::calloc(1, sizeof(int32_t));
-        return SVOB_OK;
-    }
+    if (codes.empty()) return empty_tree(depth, out);
     std::vector<V3> col(codes.size());
     const float inv = std::ldexp(1.0f, -depth);
     for (size_t i = 0; i < codes.size(); ++i)   // node.color = position - 1 (NaiveCreator.cs:66)
