@@ -425,6 +425,190 @@ __device__ __forceinline__ bool step_pf(const LaunchParams &p, Ray &r, uint2 *__
     return false;
 }
 
+// ------------------------------------------------------- lean traversal
+// The default tile-kernel loop.  Same results as step()/step_flat() (the GPU
+// parity tests compare them all against the oracle), restructured for VALU
+// issue, which is what bounds this kernel at 8 waves/SIMD:
+//   * per-lane booleans (child index bits, octant mask, PUSH/ADVANCE/POP,
+//     node cached) are held explicitly as 64-bit lane masks in SGPRs
+//     (ballot / inverse_ballot), so the index algebra of N:83-154 is SALU
+//     work that issues in parallel with other waves' VALU; the loop runs
+//     while any lane is active (wave-uniform exit: finished lanes stay in
+//     exec with every update gated off), so no lane-exit bookkeeping;
+//   * scale is implied by scale_exp2 (an exact power of two);
+//   * the stack is zeroed once per ray (never-written entries read as zero),
+//     so no written-slot mask is kept, and entries are stored raw: the HLSL
+//     float2 round trip (N:98) is applied when an entry is popped -- the same
+//     function of the same bits, once per POP instead of once per PUSH;
+//   * the iteration cap uses the wave-uniform trip count: all lanes of a tile
+//     start together, so a lane still tracing after n trips has iterated n
+//     times, exactly the per-ray count of the oracle;
+//   * "t_min <= t_max" (N:79) is implied by "t_min <= min(t_max, tc_max)":
+//     t_max is never NaN (a min over corner values of which at most two are
+//     NaN, a popped stack value -- the round trip cannot create a NaN
+//     pattern -- or zero).
+typedef uint64_t lmask;
+
+// fminf without the sNaN-quieting canonicalize LLVM adds for operands it
+// cannot prove non-signalling (LDS-loaded t_max): every value here comes out
+// of f32 arithmetic, so it is never a signalling NaN and v_min_f32 alone has
+// fminf's semantics (NaN operand -> the other operand).
+__device__ __forceinline__ float vmin(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// 3-bit per-lane integer b0 | b1 << 1 | b2 << 2 from three lane masks: one
+// v_cndmask and two add-with-carry (2r + carry-in bit) instead of three
+// selects and an or.
+__device__ __forceinline__ int lanes_to_idx(uint64_t b0, uint64_t b1, uint64_t b2) {
+    int r = __builtin_amdgcn_inverse_ballot_w64(b2) ? 1 : 0;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(r), "s"(b1));
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(r), "s"(b0));
+    return r;
+}
+#define LM_OF(c) __builtin_amdgcn_ballot_w64(c)
+#define LM_ON(m) __builtin_amdgcn_inverse_ballot_w64(m)
+
+struct FRay {
+    float px, py, pz, cx, cy, cz, bx, by, bz;
+    float t_min, t_max, h, sexp, dir_y;
+    uint32_t parent, cd16, first, flags;
+    int idx, octant_mask;   // only at entry / exit
+    int trips;              // wave-uniform loop trip count (diagnostics)
+};
+
+__device__ __forceinline__ void to_fray(const Ray &r, FRay &f) {
+    f.px = r.px; f.py = r.py; f.pz = r.pz;
+    f.cx = r.tx_coef; f.cy = r.ty_coef; f.cz = r.tz_coef;
+    f.bx = r.tx_bias; f.by = r.ty_bias; f.bz = r.tz_bias;
+    f.t_min = r.t_min; f.t_max = r.t_max; f.h = r.h; f.sexp = r.scale_exp2; f.dir_y = r.dir_y;
+    f.parent = 0; f.cd16 = 0; f.first = 0; f.flags = 0;
+    f.idx = r.idx; f.octant_mask = r.octant_mask;
+}
+
+// Back to the Ray fields finish() reads.
+__device__ __forceinline__ void from_fray(const FRay &f, Ray &r) {
+    const bool miss = f.sexp >= 1.0f || (f.flags & 6u) != 0u;
+    r.scale = miss ? S_MAX : (int)(__float_as_uint(f.sexp) >> 23) - 104;
+    r.idx = f.idx;
+    r.octant_mask = f.octant_mask;
+    r.t_min = f.t_min; r.parent = f.parent; r.flags = f.flags; r.dir_y = f.dir_y;
+}
+
+template <int MODE, int STRIDE>
+__device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk) {
+    const int slots = p.slots;
+    for (int s = 0; s < slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
+    const int scale_lo = S_MAX - slots;
+    const float sexp_lo = __int_as_float((scale_lo - S_MAX + 127) << 23);   // push below scale_lo overflows
+    lmask act = LM_OF(true);
+    lmask ix = LM_OF(r.idx & 1), iy = LM_OF(r.idx & 2), iz = LM_OF(r.idx & 4);
+    const lmask ox = LM_OF(r.octant_mask & 1), oy = LM_OF(r.octant_mask & 2), oz = LM_OF(r.octant_mask & 4);
+    lmask cached = 0, capped = 0, ovf = 0;
+    const uint32_t push_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk -
+                               (uint32_t)(104 + scale_lo) * (uint32_t)(STRIDE * sizeof(uint2));
+    int it = 0;
+    while (act != 0) {
+        // wave-uniform trip count kept in an SGPR (LLVM otherwise counts down in a VGPR)
+        asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
+        if (it > MAX_ITERS) { capped = act; break; }
+        const lmask need = act & ~cached;
+        if (LM_ON(need)) {                               // N:60-62
+            const uint2 nd = p.nodes[r.parent];
+            r.cd16 = nd.x << 16;
+            r.first = nd.y;
+        }
+        cached |= need;
+        const float tx = r.px * r.cx - r.bx;             // N:67-70
+        const float ty = r.py * r.cy - r.by;
+        const float tz = r.pz * r.cz - r.bz;
+        const float tc_max = fminf(fminf(tx, ty), tz);
+        const int k = lanes_to_idx(ix ^ ox, iy ^ oy, iz ^ oz);
+        const uint32_t cm = r.cd16 << k;                 // valid bit -> bit 31, leaf bit -> bit 23
+        const float tv_max = vmin(r.t_max, tc_max);
+        const lmask descend = act & LM_OF((int32_t)cm < 0) & LM_OF(r.t_min <= tv_max);
+        const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
+        const lmask hit = descend & leaf;                // N:93-94
+        const lmask store = descend & ~leaf & LM_OF(tc_max < r.h);
+        const lmask of = store & LM_OF(r.sexp < sexp_lo);
+        const lmask push = descend & ~leaf & ~of;
+        const lmask adv = act & ~descend;
+        if (LM_ON(store & ~of)) {                        // N:97-98 (raw; round trip on POP)
+            // slot = scale - scale_lo = (bits(scale_exp2) >> 23) - 104 - scale_lo; two dwords by
+            // ds_write2_b32: no copy into an aligned register pair
+            const uint32_t a = push_base + (__float_as_uint(r.sexp) >> 23) * (uint32_t)(STRIDE * sizeof(uint2));
+            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(r.t_max) : "memory");
+        }
+        const float half = r.sexp * 0.5f;                // N:111-116
+        const lmask cx = LM_OF(half * r.cx + tx > r.t_min);
+        const lmask cy = LM_OF(half * r.cy + ty > r.t_min);
+        const lmask cz = LM_OF(half * r.cz + tz > r.t_min);
+        const lmask sx = adv & LM_OF(tx <= tc_max);      // N:122-125
+        const lmask sy = adv & LM_OF(ty <= tc_max);
+        const lmask sz = adv & LM_OF(tz <= tc_max);
+        const float se = r.sexp;
+        const float delta = LM_ON(push) ? half : -se;
+        const float qx = r.px + (LM_ON((push & cx) | sx) ? delta : 0.0f);
+        const float qy = r.py + (LM_ON((push & cy) | sy) ? delta : 0.0f);
+        const float qz = r.pz + (LM_ON((push & cz) | sz) ? delta : 0.0f);
+        const lmask pop = (sx & ~ix) | (sy & ~iy) | (sz & ~iz);   // N:130-131
+        const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
+        if (LM_ON(push)) {
+            r.parent = child;
+            r.h = tc_max;
+            r.t_max = tv_max;
+            r.sexp = half;
+        }
+        r.t_min = LM_ON(adv) ? tc_max : r.t_min;
+        ix = (push & cx) | (~push & (ix ^ sx));
+        iy = (push & cy) | (~push & (iy ^ sy));
+        iz = (push & cz) | (~push & (iz ^ sz));
+        cached &= ~push;
+        r.px = qx; r.py = qy; r.pz = qz;
+        lmask out = 0;
+        if (pop != 0) {
+            uint32_t bit = 0;
+            if (LM_ON(pop)) {                            // N:134-154
+                uint32_t differing = 0;
+                if (LM_ON(sx)) differing |= __float_as_uint(qx) ^ __float_as_uint(qx + se);
+                if (LM_ON(sy)) differing |= __float_as_uint(qy) ^ __float_as_uint(qy + se);
+                if (LM_ON(sz)) differing |= __float_as_uint(qz) ^ __float_as_uint(qz + se);
+                const uint32_t fd = __float_as_uint((float)differing);
+                const int scale = (int)(fd >> 23) - 127;
+                r.sexp = __uint_as_float((fd & 0x7F800000u) - (23u << 23));
+                const uint2 e = stk[(scale - scale_lo) * STRIDE];   // slot == slots only when leaving the root
+                uint32_t pa = e.x, tm = e.y;
+                if (MODE == 0) {                         // int2 <- float2((int)parent, asint(t_max))
+                    pa = (uint32_t)cvt_i32((float)(int32_t)pa);
+                    tm = (uint32_t)cvt_i32((float)(int32_t)tm);
+                }
+                r.parent = pa;
+                r.t_max = __uint_as_float(tm);
+                const uint32_t keep = 0xFFFFFFFFu << scale;
+                bit = 1u << scale;
+                r.px = __uint_as_float(__float_as_uint(qx) & keep);
+                r.py = __uint_as_float(__float_as_uint(qy) & keep);
+                r.pz = __uint_as_float(__float_as_uint(qz) & keep);
+                r.h = 0.0f;
+            }
+            ix = (ix & ~pop) | (pop & LM_OF((__float_as_uint(qx) & bit) != 0u));
+            iy = (iy & ~pop) | (pop & LM_OF((__float_as_uint(qy) & bit) != 0u));
+            iz = (iz & ~pop) | (pop & LM_OF((__float_as_uint(qz) & bit) != 0u));
+            cached &= ~pop;
+            out = pop & LM_OF(r.sexp >= 1.0f);
+        }
+        ovf |= of;
+        act &= ~(hit | of | out);
+    }
+    r.idx = (LM_ON(ix) ? 1 : 0) | (LM_ON(iy) ? 2 : 0) | (LM_ON(iz) ? 4 : 0);
+    r.trips = it;
+    if (LM_ON(capped)) r.flags |= 2u;
+    if (LM_ON(ovf)) r.flags |= 4u;
+}
+
 // N:158-186 hit decode; R:93-127 Shade; R:167 store
 __device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r_in, size_t out) {
     Ray r = r_in;
@@ -500,7 +684,8 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int t = tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
+    const int t = (STEP == 3 && BS == 64 && p.tile_order) ? (int)p.tile_order[blockIdx.x]
+                                                         : tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
     const int bx = t % blocks_x, by = t / blocks_x;
     const int x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
     const int lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
@@ -509,11 +694,26 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     init_ray(p, x, global_row(p, lr), r);
     const int scale_lo = S_MAX - p.slots;
     uint2 *stk = stk_base + tid;
-    if (STEP == 2) {
+    if (STEP == 3 && !COUNT) {
+        uint32_t t0 = 0;
+        if (p.wave_log) t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        FRay f;
+        to_fray(r, f);
+        trace_lean<MODE, BS>(p, f, stk);
+        from_fray(f, r);
+        if (BS == 64 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every lane
+        if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
+            uint32_t *w = p.wave_log + 4 * ((size_t)blockIdx.x * (BS / 64) + wave);
+            w[0] = t0;
+            w[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            w[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+            w[3] = ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFFu) | ((uint32_t)f.trips << 8);
+        }
+    } else if (STEP == 2) {
         r.nd = p.nodes[0];
         while (!step_pf<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
         }
-    } else if (STEP == 1) {
+    } else if (STEP == 1 || STEP == 3) {
         while (!step_flat<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
         }
     } else {
@@ -635,7 +835,10 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
         if (p.block == 128) {
             const int bx = (p.width + 15) / 16, by = (p.local_rows + 7) / 8;
             const size_t lds128 = (size_t)(p.slots + 1) * 128 * sizeof(uint2);
-            if (p.flat)
+            if (p.flat == 3)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 128>), dim3((unsigned)(bx * by)), dim3(128),
+                                   lds128, stream, p, bx, p.xcd_remap);
+            else if (p.flat)
                 hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 128>), dim3((unsigned)(bx * by)), dim3(128),
                                    lds128, stream, p, bx, p.xcd_remap);
             else
@@ -646,7 +849,10 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
         if (p.block == 64) {
             const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
             const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
-            if (p.flat == 2)
+            if (p.flat == 3)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                                   lds64, stream, p, bx, p.xcd_remap);
+            else if (p.flat == 2)
                 hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 2, 64>), dim3((unsigned)(bx * by)), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat)
@@ -658,7 +864,10 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
             return hipGetLastError();
         }
         const int bx = (p.width + 15) / 16, by = (p.local_rows + 15) / 16;
-        if (p.flat)
+        if (p.flat == 3)
+            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
+                               stream, p, bx, p.xcd_remap);
+        else if (p.flat)
             hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
                                stream, p, bx, p.xcd_remap);
         else
@@ -677,6 +886,43 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL((render_persistent_kernel<MODE, COUNT>), dim3(blocks), dim3(BLOCK), lds, stream, p, counter,
                        total, tiles_x);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------- tile order
+__global__ __launch_bounds__(1024) void order_tiles_kernel(const uint16_t *__restrict__ cost,
+                                                           uint32_t *__restrict__ order, int n) {
+    constexpr int NB = 1024;
+    __shared__ uint32_t cnt[NB];
+    __shared__ uint32_t part[NB / 64];
+    const int tid = threadIdx.x;
+    cnt[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += NB) atomicAdd(&cnt[NB - 1 - min((int)cost[i], NB - 1)], 1u);
+    __syncthreads();
+    // exclusive scan of cnt: wave-level inclusive scan, then the 16 wave totals
+    const uint32_t v = cnt[tid];
+    uint32_t x = v;
+    const int lane = tid & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) part[tid >> 6] = x;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int w = 0; w < (tid >> 6); ++w) base += part[w];
+    cnt[tid] = base + x - v;
+    __syncthreads();
+    for (int i = tid; i < n; i += NB) {
+        const uint32_t pos = atomicAdd(&cnt[NB - 1 - min((int)cost[i], NB - 1)], 1u);
+        order[pos] = (uint32_t)i;
+    }
+}
+
+hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream) {
+    hipLaunchKernelGGL(order_tiles_kernel, dim3(1), dim3(1024), 0, stream, cost, order, n_tiles);
     return hipGetLastError();
 }
 

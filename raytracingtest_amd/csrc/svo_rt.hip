@@ -75,9 +75,21 @@ struct svo_ctx {
     int refill_at = 40;              // env SVO_REFILL
     int blocks_per_cu = 8;           // env SVO_BLOCKS_PER_CU
     int xcd_remap = 0;               // env SVO_XCD_REMAP (measured slower: XCD load imbalance)
-    int flat = 1;                    // env SVO_FLAT
+    int flat = 3;                    // env SVO_FLAT: 3 lean (default), 1 flat, 0 branchy, 2 prefetch
     int block = 64;                  // env SVO_BLOCK (64 | 256)
     uint32_t options = 0;            // svo_set_options
+    uint32_t *d_wave_log = nullptr;  // diagnostics: env SVO_WAVE_LOG=<file> (tile kernel, SVO_FLAT=3)
+    size_t wave_log_cap = 0;
+    // cost-ordered tile dispatch: per 8x8 tile, the trip count of the
+    // previous launch at the same geometry and the resulting most-expensive-first order
+    int tile_order = 1;              // env SVO_TILE_ORDER=0 disables
+    uint16_t *d_tile_cost = nullptr;
+    uint32_t *d_tile_order = nullptr;
+    size_t tile_cap = 0;
+    long long tile_key = -1;         // (width, local_rows, band) the recorded costs belong to
+    bool order_valid = false;
+    hipEvent_t order_event = nullptr;   // last order-kernel launch: ordered renders on any stream wait on it
+    bool order_event_recorded = false;
 };
 
 namespace {
@@ -229,9 +241,66 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         if (rc2) return rc2;
         p.hits = reinterpret_cast<svo::Hit *>(ctx->d_out_hits);
     }
-    hipError_t e = svo::launch_render(p, stack_mode, stream ? stream : ctx->stream, ctx->kernel, ctx->d_counter,
-                                      ctx->num_cus);
+    p.wave_log = nullptr;
+    p.tile_order = nullptr;
+    p.tile_cost = nullptr;
+    const bool ordered = ctx->tile_order && ctx->kernel == 0 && ctx->flat == 3 && ctx->block == 64 && !p.fetches;
+    const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
+    if (ordered) {
+        const long long key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^
+                              ((long long)b.band_rows << 8) ^ (long long)b.band_rank ^ ((long long)b.band_count << 4);
+        if (ctx->tile_cap < (size_t)n_tiles) {
+            if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
+            if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
+            ctx->d_tile_cost = nullptr;
+            ctx->d_tile_order = nullptr;
+            ctx->tile_cap = 0;
+            HIP_TRY(hipMalloc(&ctx->d_tile_cost, (size_t)n_tiles * sizeof(uint16_t)));
+            HIP_TRY(hipMalloc(&ctx->d_tile_order, (size_t)n_tiles * sizeof(uint32_t)));
+            ctx->tile_cap = (size_t)n_tiles;
+            ctx->order_valid = false;
+        }
+        if (key != ctx->tile_key) ctx->order_valid = false;
+        ctx->tile_key = key;
+        p.tile_order = ctx->order_valid ? ctx->d_tile_order : nullptr;
+        p.tile_cost = ctx->d_tile_cost;
+    }
+    const char *log_path = std::getenv("SVO_WAVE_LOG");
+    const size_t n_wave = (size_t)((width + 15) / 16) * (size_t)((p.local_rows + 15) / 16) * 4;   // >= any tiling
+    if (log_path && !p.fetches) {
+        if (ctx->wave_log_cap < n_wave) {
+            if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
+            ctx->d_wave_log = nullptr;
+            ctx->wave_log_cap = 0;
+            HIP_TRY(hipMalloc(&ctx->d_wave_log, n_wave * 16));
+            ctx->wave_log_cap = n_wave;
+        }
+        HIP_TRY(hipMemset(ctx->d_wave_log, 0, n_wave * 16));
+        p.wave_log = ctx->d_wave_log;
+    }
+    hipStream_t s = stream ? stream : ctx->stream;
+    // the cost/order buffers are shared by every launch of this context: chain
+    // ordered launches (render, then order kernel) across streams
+    if (p.tile_cost && ctx->order_event_recorded) HIP_TRY(hipStreamWaitEvent(s, ctx->order_event, 0));
+    hipError_t e = svo::launch_render(p, stack_mode, s, ctx->kernel, ctx->d_counter, ctx->num_cus);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
+    if (p.tile_cost) {   // next launch at this geometry dispatches the most expensive tiles first
+        e = svo::launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, s);
+        if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
+        ctx->order_valid = true;
+        if (!ctx->order_event) HIP_TRY(hipEventCreateWithFlags(&ctx->order_event, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ctx->order_event, s));
+        ctx->order_event_recorded = true;
+    }
+    if (p.wave_log) {   // blocking dump of the last launch's per-wave record
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<uint32_t> h(n_wave * 4);
+        HIP_TRY(hipMemcpy(h.data(), ctx->d_wave_log, n_wave * 16, hipMemcpyDeviceToHost));
+        if (FILE *f = std::fopen(log_path, "wb")) {
+            std::fwrite(h.data(), 16, n_wave, f);
+            std::fclose(f);
+        }
+    }
     return SVO_OK;
 }
 
@@ -265,7 +334,8 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "persistent") == 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
     if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(2, std::atoi(k)));
+    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(3, std::atoi(k)));
+    if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_BLOCK")) { const int b = std::atoi(k); ctx->block = (b == 256 || b == 128) ? b : 64; }
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));
     if (e != hipSuccess) {
@@ -411,6 +481,10 @@ int svo_destroy(svo_ctx *ctx) {
     if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
     if (ctx->d_counter) hipFree(ctx->d_counter);
+    if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
+    if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
+    if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
+    if (ctx->order_event) hipEventDestroy(ctx->order_event);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return SVO_OK;

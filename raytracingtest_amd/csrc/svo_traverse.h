@@ -53,7 +53,17 @@ struct LaunchParams {
     int flat;             // 1: branch-flattened iteration (default), 0: branchy reference form
     int block;            // tile kernel workgroup size: 64 (one 8x8 wave) or 256 (16x16 pixels)
     int shadows;          // 1: second pass, one shadow ray per primary hit (needs hits)
+    uint32_t *wave_log;   // diagnostics (env SVO_WAVE_LOG): per wave {t0, t1, HW_ID, XCC_ID | trips << 8}
+    // Cost-ordered dispatch (64-thread tile kernel): block b traces 8x8 tile
+    // tile_order[b] (null = b) and records its wave trip count in tile_cost.
+    const uint32_t *tile_order;
+    uint16_t *tile_cost;
 };
+
+// Sort the tiles by recorded cost, most expensive first, into `order` (one
+// workgroup; counting sort on min(cost, 1023)).  Placement only: any order
+// gives identical results.
+hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream);
 
 // kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).
 // counter: 16-byte device work counter (persistent kernel), num_cus: CU count.

@@ -1,0 +1,87 @@
+"""Per-wave timing of one render of the bench workload (diagnostics).
+
+Runs the tile kernel once with SVO_WAVE_LOG set (svo_rt.hip writes, per wave:
+s_memrealtime at trace start / end (100 MHz), HW_ID, XCC_ID | trip count << 8)
+and prints the kernel span, the wave-duration distribution, the mean number
+of resident waves over the span and a coarse occupancy timeline.
+
+  python tools/wave_log.py [--camera flyover] [--max-level 11] [--order ...]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--camera", default="flyover")
+    ap.add_argument("--max-level", type=int, default=11)
+    ap.add_argument("--out", default="gpurun_out/wave_log.bin")
+    args = ap.parse_args()
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    os.environ["SVO_WAVE_LOG"] = os.path.abspath(args.out)
+    import torch
+    from raytracingtest_amd import RaytracingMaster
+    from raytracingtest_amd.camera import CAMERAS
+    from raytracingtest_amd.native_builder import build_sampler_svo
+
+    W, H = 1920, 1080
+    svo = build_sampler_svo(4, args.max_level)
+    rm = RaytracingMaster(capacity_nodes=len(svo))
+    rm.SetSVOBuffer(svo)
+    rm.UpdateShaderParameters(CAMERAS[args.camera](), W, H)
+    hits = torch.empty(W * H * 24, dtype=torch.uint8, device="cuda")
+    rgba = torch.empty(W * H * 4, dtype=torch.float32, device="cuda")
+    for _ in range(3):
+        rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr())
+    rm.synchronize()
+    log = np.fromfile(args.out, np.uint32).reshape(-1, 4)
+    log = log[(log[:, 0] != 0) | (log[:, 1] != 0)]
+    t0 = log[:, 0].astype(np.int64)
+    t1 = log[:, 1].astype(np.int64)
+    t1 = np.where(t1 < t0, t1 + (1 << 32), t1)
+    base = t0.min()
+    t0 -= base
+    t1 -= base
+    dur = (t1 - t0) * 10e-3    # us
+    trips = log[:, 3] >> 8
+    span = t1.max() * 10e-3
+    print(f"waves {len(log)}  span {span:.1f} us  (100 MHz clock)")
+    q = np.percentile(dur, [0, 10, 50, 90, 99, 100])
+    print("wave duration us  min/p10/p50/p90/p99/max", np.round(q, 2))
+    q = np.percentile(trips, [0, 10, 50, 90, 99, 100])
+    print("trips             min/p10/p50/p90/p99/max", q)
+    print(f"sum of wave time {dur.sum():.0f} us -> mean resident waves {dur.sum() / span:.0f}"
+          f" (chip max 256 CUs x 32 = 8192)")
+    # resident-wave timeline (20 bins)
+    nb = 20
+    edges = np.linspace(0, t1.max(), nb + 1)
+    res = []
+    for a, b in zip(edges[:-1], edges[1:]):
+        ov = np.clip(np.minimum(t1, b) - np.maximum(t0, a), 0, None).sum() / (b - a)
+        res.append(ov)
+    print("resident waves per 5% of span:", " ".join(f"{int(v)}" for v in res))
+    # start times: how fast the dispatcher issues
+    ts = np.sort(t0) * 10e-3
+    print("wave starts by t(us): 25%/50%/75%/100% of waves started at",
+          np.round([ts[int(len(ts) * f) - 1] for f in (0.25, 0.5, 0.75, 1.0)], 1))
+    # duration vs screen position (block order = row-major tiles)
+    ntx = W // 8
+    ty = np.arange(len(log)) // ntx
+    rows = [dur[ty == y].mean() for y in range(0, ty.max() + 1, 15)]
+    print("mean wave us per 15 tile-rows (top->bottom):", " ".join(f"{v:.1f}" for v in rows))
+    hw = log[:, 2]
+    xcc = log[:, 3] & 0xFF
+    print("waves per XCC:", np.bincount(xcc, minlength=8)[:8])
+    for x in range(8):
+        m = xcc == x
+        print(f"  xcc {x}: busy-sum {dur[m].sum():.0f} us, last end {t1[m].max() * 10e-3:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
