@@ -890,39 +890,107 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
 }
 
 // ---------------------------------------------------------- tile order
-__global__ __launch_bounds__(1024) void order_tiles_kernel(const uint16_t *__restrict__ cost,
-                                                           uint32_t *__restrict__ order, int n) {
-    constexpr int NB = 1024;
-    __shared__ uint32_t cnt[NB];
-    __shared__ uint32_t part[NB / 64];
-    const int tid = threadIdx.x;
-    cnt[tid] = 0;
-    __syncthreads();
-    for (int i = tid; i < n; i += NB) atomicAdd(&cnt[NB - 1 - min((int)cost[i], NB - 1)], 1u);
-    __syncthreads();
-    // exclusive scan of cnt: wave-level inclusive scan, then the 16 wave totals
-    const uint32_t v = cnt[tid];
-    uint32_t x = v;
-    const int lane = tid & 63;
+// Stable-free 4-class partition of the tiles by recorded cost, heaviest class
+// first: class 0 = cost >= max/2, 1 = >= max/4, 2 = >= max/8, 3 = the rest.
+// Only the start order of the heavy tiles matters (they bound the launch; the
+// light ones fill in behind), so a partition does what a sort would
+// (tools/wave_log.py: any order that dispatches the >= max/2 tiles first
+// reaches the longest-wave bound).  One workgroup; every tile's cost is read
+// with 16-byte loads into registers (32 per thread per chunk), classes are
+// counted with ballots, positions come from mbcnt ranks: no atomics.
+constexpr int ORDER_THREADS = 1024, ORDER_PER = 32, ORDER_CHUNK = ORDER_THREADS * ORDER_PER;
+
+__device__ __forceinline__ void order_load(const uint16_t *cost, int chunk, int tid, uint32_t v[ORDER_PER / 2]) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(cost + (size_t)chunk * ORDER_CHUNK + (size_t)tid * ORDER_PER);
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-        if (lane >= d) x += y;
-    }
-    if (lane == 63) part[tid >> 6] = x;
-    __syncthreads();
-    uint32_t base = 0;
-    for (int w = 0; w < (tid >> 6); ++w) base += part[w];
-    cnt[tid] = base + x - v;
-    __syncthreads();
-    for (int i = tid; i < n; i += NB) {
-        const uint32_t pos = atomicAdd(&cnt[NB - 1 - min((int)cost[i], NB - 1)], 1u);
-        order[pos] = (uint32_t)i;
+    for (int q = 0; q < ORDER_PER / 8; ++q) {
+        const uint4 w = src[q];
+        v[4 * q + 0] = w.x; v[4 * q + 1] = w.y; v[4 * q + 2] = w.z; v[4 * q + 3] = w.w;
     }
 }
 
+__global__ __launch_bounds__(ORDER_THREADS) void order_tiles_kernel(const uint16_t *__restrict__ cost,
+                                                                    uint32_t *__restrict__ order, int n) {
+    constexpr int NW = ORDER_THREADS / 64, NC = 4;
+    __shared__ uint32_t red[NW];
+    __shared__ uint32_t cnt[NC][NW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n_chunks = (n + ORDER_CHUNK - 1) / ORDER_CHUNK;
+    uint32_t v[ORDER_PER / 2];   // two 16-bit costs per word
+    // ---- max cost
+    uint32_t mx = 0;
+    for (int c = 0; c < n_chunks; ++c) {
+        order_load(cost, c, tid, v);
+#pragma unroll
+        for (int e = 0; e < ORDER_PER; ++e) {
+            const int i = c * ORDER_CHUNK + tid * ORDER_PER + e;
+            const uint32_t k = (v[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu;
+            if (i < n) mx = max(mx, k);
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+    if (lane == 0) red[wave] = mx;
+    __syncthreads();
+    mx = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) mx = max(mx, red[w]);
+    // class of a cost (NC = invalid element)
+    auto cls = [mx](uint32_t k) { return 2 * k >= mx ? 0 : 4 * k >= mx ? 1 : 8 * k >= mx ? 2 : 3; };
+    // ---- per-wave class counts
+    uint32_t count[NC] = {0, 0, 0, 0};
+    for (int c = 0; c < n_chunks; ++c) {
+        if (n_chunks > 1) order_load(cost, c, tid, v);
+#pragma unroll
+        for (int e = 0; e < ORDER_PER; ++e) {
+            const int i = c * ORDER_CHUNK + tid * ORDER_PER + e;
+            const int k = i < n ? cls((v[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu) : NC;
+#pragma unroll
+            for (int q = 0; q < NC; ++q) count[q] += (uint32_t)__popcll(__ballot(k == q));
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < NC; ++q) cnt[q][wave] = count[q];
+    }
+    __syncthreads();
+    uint32_t run[NC];
+    uint32_t before = 0;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+        uint32_t mine = before;
+        for (int w = 0; w < NW; ++w) {
+            if (w < wave) mine += cnt[q][w];
+            before += cnt[q][w];
+        }
+        run[q] = mine;
+    }
+    // ---- scatter
+    for (int c = 0; c < n_chunks; ++c) {
+        if (n_chunks > 1) order_load(cost, c, tid, v);
+#pragma unroll
+        for (int e = 0; e < ORDER_PER; ++e) {
+            const int i = c * ORDER_CHUNK + tid * ORDER_PER + e;
+            const int k = i < n ? cls((v[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu) : NC;
+            uint32_t pos = 0;
+#pragma unroll
+            for (int q = 0; q < NC; ++q) {
+                const uint64_t m = __ballot(k == q);
+                if (k == q) pos = run[q] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                run[q] += (uint32_t)__popcll(m);
+            }
+            if (k < NC) order[pos] = (uint32_t)i;
+        }
+    }
+}
+
+size_t order_cost_capacity(int n_tiles) {
+    return ((size_t)n_tiles + ORDER_CHUNK - 1) / ORDER_CHUNK * ORDER_CHUNK;
+}
+
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream) {
-    hipLaunchKernelGGL(order_tiles_kernel, dim3(1), dim3(1024), 0, stream, cost, order, n_tiles);
+    if (n_tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(order_tiles_kernel, dim3(1), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles);
     return hipGetLastError();
 }
 

@@ -80,16 +80,18 @@ struct svo_ctx {
     uint32_t options = 0;            // svo_set_options
     uint32_t *d_wave_log = nullptr;  // diagnostics: env SVO_WAVE_LOG=<file> (tile kernel, SVO_FLAT=3)
     size_t wave_log_cap = 0;
-    // cost-ordered tile dispatch: per 8x8 tile, the trip count of the
-    // previous launch at the same geometry and the resulting most-expensive-first order
+    // Cost-ordered tile dispatch: every launch records each 8x8 tile's trip
+    // count; the order kernel, enqueued right behind it, turns them into the
+    // heaviest-first dispatch order of the next launch at the same geometry.
     int tile_order = 1;              // env SVO_TILE_ORDER=0 disables
+    int order_every = 8;             // env SVO_ORDER_EVERY: rebuild the order every k-th launch (~20 us one-CU kernel)
+    unsigned long long order_launches = 0;
     uint16_t *d_tile_cost = nullptr;
     uint32_t *d_tile_order = nullptr;
     size_t tile_cap = 0;
-    long long tile_key = -1;         // (width, local_rows, band) the recorded costs belong to
-    bool order_valid = false;
-    hipEvent_t order_event = nullptr;   // last order-kernel launch: ordered renders on any stream wait on it
-    bool order_event_recorded = false;
+    long long order_key = -1;        // geometry d_tile_order was built for (-1: none)
+    hipStream_t order_stream = nullptr;   // stream of the last order kernel (a launch elsewhere syncs it first)
+    bool order_pending = false;
 };
 
 namespace {
@@ -246,23 +248,25 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.tile_cost = nullptr;
     const bool ordered = ctx->tile_order && ctx->kernel == 0 && ctx->flat == 3 && ctx->block == 64 && !p.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
+    long long key = -1;
     if (ordered) {
-        const long long key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^
-                              ((long long)b.band_rows << 8) ^ (long long)b.band_rank ^ ((long long)b.band_count << 4);
+        key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^ ((long long)b.band_rows << 8) ^
+              (long long)b.band_rank ^ ((long long)b.band_count << 4);
         if (ctx->tile_cap < (size_t)n_tiles) {
+            HIP_TRY(hipDeviceSynchronize());   // a pending launch may still use the old buffers
             if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
             if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
             ctx->d_tile_cost = nullptr;
             ctx->d_tile_order = nullptr;
             ctx->tile_cap = 0;
-            HIP_TRY(hipMalloc(&ctx->d_tile_cost, (size_t)n_tiles * sizeof(uint16_t)));
+            ctx->order_key = -1;
+            const size_t cap = svo::order_cost_capacity(n_tiles);
+            HIP_TRY(hipMalloc(&ctx->d_tile_cost, cap * sizeof(uint16_t)));
+            HIP_TRY(hipMemset(ctx->d_tile_cost, 0, cap * sizeof(uint16_t)));
             HIP_TRY(hipMalloc(&ctx->d_tile_order, (size_t)n_tiles * sizeof(uint32_t)));
             ctx->tile_cap = (size_t)n_tiles;
-            ctx->order_valid = false;
         }
-        if (key != ctx->tile_key) ctx->order_valid = false;
-        ctx->tile_key = key;
-        p.tile_order = ctx->order_valid ? ctx->d_tile_order : nullptr;
+        p.tile_order = ctx->order_key == key ? ctx->d_tile_order : nullptr;
         p.tile_cost = ctx->d_tile_cost;
     }
     const char *log_path = std::getenv("SVO_WAVE_LOG");
@@ -279,18 +283,21 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         p.wave_log = ctx->d_wave_log;
     }
     hipStream_t s = stream ? stream : ctx->stream;
-    // the cost/order buffers are shared by every launch of this context: chain
-    // ordered launches (render, then order kernel) across streams
-    if (p.tile_cost && ctx->order_event_recorded) HIP_TRY(hipStreamWaitEvent(s, ctx->order_event, 0));
+    // the cost/order buffers are shared by all launches of the context: launches
+    // on one stream are ordered; switching streams waits for the last order kernel
+    if (p.tile_cost && ctx->order_pending && ctx->order_stream != s) {
+        HIP_TRY(hipStreamSynchronize(ctx->order_stream));
+        ctx->order_pending = false;
+    }
     hipError_t e = svo::launch_render(p, stack_mode, s, ctx->kernel, ctx->d_counter, ctx->num_cus);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
-    if (p.tile_cost) {   // next launch at this geometry dispatches the most expensive tiles first
+    const bool refresh = p.tile_cost && (ctx->order_key != key || ctx->order_launches++ % ctx->order_every == 0);
+    if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
         e = svo::launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, s);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
-        ctx->order_valid = true;
-        if (!ctx->order_event) HIP_TRY(hipEventCreateWithFlags(&ctx->order_event, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(ctx->order_event, s));
-        ctx->order_event_recorded = true;
+        ctx->order_stream = s;
+        ctx->order_pending = true;
+        ctx->order_key = key;
     }
     if (p.wave_log) {   // blocking dump of the last launch's per-wave record
         HIP_TRY(hipStreamSynchronize(s));
@@ -336,6 +343,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(3, std::atoi(k)));
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_BLOCK")) { const int b = std::atoi(k); ctx->block = (b == 256 || b == 128) ? b : 64; }
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));
     if (e != hipSuccess) {
@@ -484,7 +492,6 @@ int svo_destroy(svo_ctx *ctx) {
     if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
     if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
     if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
-    if (ctx->order_event) hipEventDestroy(ctx->order_event);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return SVO_OK;

@@ -60,10 +60,12 @@ struct LaunchParams {
     uint16_t *tile_cost;
 };
 
-// Sort the tiles by recorded cost, most expensive first, into `order` (one
-// workgroup; counting sort on min(cost, 1023)).  Placement only: any order
-// gives identical results.
+// Order the tiles by recorded cost, most expensive class first, into `order`
+// (one workgroup, no atomics).  Placement only: any order gives identical
+// results.  `cost` must hold order_cost_capacity(n_tiles) entries (the tail
+// beyond n_tiles is read, never used).
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream);
+size_t order_cost_capacity(int n_tiles);
 
 // kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).
 // counter: 16-byte device work counter (persistent kernel), num_cus: CU count.
