@@ -498,8 +498,14 @@ __device__ __forceinline__ void from_fray(const FRay &f, Ray &r) {
     r.t_min = f.t_min; r.parent = f.parent; r.flags = f.flags; r.dir_y = f.dir_y;
 }
 
-template <int MODE, int STRIDE>
-__device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk) {
+struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
+    uint64_t fetch_cycles = 0, loop_cycles = 0;
+    uint32_t fetch_trips = 0, pop_trips = 0;
+};
+
+template <int MODE, int STRIDE, bool DIAG = false>
+__device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk,
+                                           LeanDiag *diag = nullptr) {
     const int slots = p.slots;
     for (int s = 0; s < slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
     const int scale_lo = S_MAX - slots;
@@ -511,15 +517,24 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     const uint32_t push_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk -
                                (uint32_t)(104 + scale_lo) * (uint32_t)(STRIDE * sizeof(uint2));
     int it = 0;
+    uint64_t tl0 = 0;
+    if (DIAG) tl0 = __builtin_amdgcn_s_memtime();
     while (act != 0) {
         // wave-uniform trip count kept in an SGPR (LLVM otherwise counts down in a VGPR)
         asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
         if (it > MAX_ITERS) { capped = act; break; }
         const lmask need = act & ~cached;
+        uint64_t tf0 = 0;
+        if (DIAG && need) tf0 = __builtin_amdgcn_s_memtime();
         if (LM_ON(need)) {                               // N:60-62
             const uint2 nd = p.nodes[r.parent];
             r.cd16 = nd.x << 16;
             r.first = nd.y;
+        }
+        if (DIAG && need) {                              // wait for the data, then stamp
+            asm volatile("v_mov_b32 %0, %0" : "+v"(r.first));
+            diag->fetch_cycles += __builtin_amdgcn_s_memtime() - tf0;
+            diag->fetch_trips += 1;
         }
         cached |= need;
         const float tx = r.px * r.cx - r.bx;             // N:67-70
@@ -570,6 +585,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         r.px = qx; r.py = qy; r.pz = qz;
         lmask out = 0;
         if (pop != 0) {
+            if (DIAG) diag->pop_trips += 1;
             uint32_t bit = 0;
             if (LM_ON(pop)) {                            // N:134-154
                 uint32_t differing = 0;
@@ -603,6 +619,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         ovf |= of;
         act &= ~(hit | of | out);
     }
+    if (DIAG) diag->loop_cycles = __builtin_amdgcn_s_memtime() - tl0;
     r.idx = (LM_ON(ix) ? 1 : 0) | (LM_ON(iy) ? 2 : 0) | (LM_ON(iz) ? 4 : 0);
     r.trips = it;
     if (LM_ON(capped)) r.flags |= 2u;
@@ -690,6 +707,14 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     const int x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
     const int lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
     if (x >= p.width || lr >= p.local_rows) return;
+    if (STEP == 3 && BS == 64 && p.tile_order && p.prio) {
+        // issue priority by the previous launch's cost class: the heaviest tiles
+        // bound the launch, so their waves win issue arbitration on a busy SIMD
+        const uint32_t b = blockIdx.x, n = gridDim.x;
+        if (b < p.tile_order[n]) __builtin_amdgcn_s_setprio(3);
+        else if (b < p.tile_order[n + 1]) __builtin_amdgcn_s_setprio(2);
+        else if (b < p.tile_order[n + 2]) __builtin_amdgcn_s_setprio(1);
+    }
     Ray r;
     init_ray(p, x, global_row(p, lr), r);
     const int scale_lo = S_MAX - p.slots;
@@ -699,15 +724,21 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
         if (p.wave_log) t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
         FRay f;
         to_fray(r, f);
-        trace_lean<MODE, BS>(p, f, stk);
+        LeanDiag dg;
+        if (p.wave_log) trace_lean<MODE, BS, true>(p, f, stk, &dg);
+        else trace_lean<MODE, BS>(p, f, stk);
         from_fray(f, r);
         if (BS == 64 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every lane
         if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
-            uint32_t *w = p.wave_log + 4 * ((size_t)blockIdx.x * (BS / 64) + wave);
+            uint32_t *w = p.wave_log + 8 * ((size_t)blockIdx.x * (BS / 64) + wave);
             w[0] = t0;
             w[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
             w[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
             w[3] = ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFFu) | ((uint32_t)f.trips << 8);
+            w[4] = (uint32_t)dg.loop_cycles;
+            w[5] = (uint32_t)dg.fetch_cycles;
+            w[6] = dg.fetch_trips;
+            w[7] = dg.pop_trips;
         }
     } else if (STEP == 2) {
         r.nd = p.nodes[0];
@@ -964,6 +995,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_tiles_kernel(const uint16
             before += cnt[q][w];
         }
         run[q] = mine;
+        if (tid == 0) order[n + q] = before;   // class boundaries: end of class q in the order
     }
     // ---- scatter
     for (int c = 0; c < n_chunks; ++c) {

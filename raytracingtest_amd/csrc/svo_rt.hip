@@ -84,6 +84,7 @@ struct svo_ctx {
     // count; the order kernel, enqueued right behind it, turns them into the
     // heaviest-first dispatch order of the next launch at the same geometry.
     int tile_order = 1;              // env SVO_TILE_ORDER=0 disables
+    int prio = 1;                    // env SVO_PRIO=0: no issue priority by cost class
     int order_every = 8;             // env SVO_ORDER_EVERY: rebuild the order every k-th launch (~20 us one-CU kernel)
     unsigned long long order_launches = 0;
     uint16_t *d_tile_cost = nullptr;
@@ -246,6 +247,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.wave_log = nullptr;
     p.tile_order = nullptr;
     p.tile_cost = nullptr;
+    p.prio = ctx->prio;
     const bool ordered = ctx->tile_order && ctx->kernel == 0 && ctx->flat == 3 && ctx->block == 64 && !p.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
     long long key = -1;
@@ -263,11 +265,31 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             const size_t cap = svo::order_cost_capacity(n_tiles);
             HIP_TRY(hipMalloc(&ctx->d_tile_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(ctx->d_tile_cost, 0, cap * sizeof(uint16_t)));
-            HIP_TRY(hipMalloc(&ctx->d_tile_order, (size_t)n_tiles * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&ctx->d_tile_order, ((size_t)n_tiles + 4) * sizeof(uint32_t)));
             ctx->tile_cap = (size_t)n_tiles;
         }
-        p.tile_order = ctx->order_key == key ? ctx->d_tile_order : nullptr;
-        p.tile_cost = ctx->d_tile_cost;
+        if (const char *f = std::getenv("SVO_ORDER_FILE")) {   // experiments: a fixed host-made order
+            if (ctx->order_key != key) {
+                std::vector<uint32_t> h((size_t)n_tiles + 4, 0u);
+                FILE *fp = std::fopen(f, "rb");
+                if (!fp) return fail(SVO_ERR_ARG, std::string("SVO_ORDER_FILE: cannot open ") + f);
+                const size_t got = std::fread(h.data(), sizeof(uint32_t), (size_t)n_tiles, fp);
+                std::fclose(fp);
+                if (got != (size_t)n_tiles) return fail(SVO_ERR_ARG, "SVO_ORDER_FILE: short file");
+                std::vector<uint8_t> seen((size_t)n_tiles, 0);
+                for (size_t i = 0; i < (size_t)n_tiles; ++i) {
+                    if (h[i] >= (uint32_t)n_tiles || seen[h[i]]) return fail(SVO_ERR_ARG, "SVO_ORDER_FILE: not a permutation");
+                    seen[h[i]] = 1;
+                }
+                HIP_TRY(hipMemcpy(ctx->d_tile_order, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+                ctx->order_key = key;
+            }
+            p.tile_order = ctx->d_tile_order;
+            p.tile_cost = nullptr;
+        } else {
+            p.tile_order = ctx->order_key == key ? ctx->d_tile_order : nullptr;
+        }
+        if (!std::getenv("SVO_ORDER_FILE")) p.tile_cost = ctx->d_tile_cost;
     }
     const char *log_path = std::getenv("SVO_WAVE_LOG");
     const size_t n_wave = (size_t)((width + 15) / 16) * (size_t)((p.local_rows + 15) / 16) * 4;   // >= any tiling
@@ -276,10 +298,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
             ctx->d_wave_log = nullptr;
             ctx->wave_log_cap = 0;
-            HIP_TRY(hipMalloc(&ctx->d_wave_log, n_wave * 16));
+            HIP_TRY(hipMalloc(&ctx->d_wave_log, n_wave * 32));
             ctx->wave_log_cap = n_wave;
         }
-        HIP_TRY(hipMemset(ctx->d_wave_log, 0, n_wave * 16));
+        HIP_TRY(hipMemset(ctx->d_wave_log, 0, n_wave * 32));
         p.wave_log = ctx->d_wave_log;
     }
     hipStream_t s = stream ? stream : ctx->stream;
@@ -301,10 +323,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     }
     if (p.wave_log) {   // blocking dump of the last launch's per-wave record
         HIP_TRY(hipStreamSynchronize(s));
-        std::vector<uint32_t> h(n_wave * 4);
-        HIP_TRY(hipMemcpy(h.data(), ctx->d_wave_log, n_wave * 16, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> h(n_wave * 8);
+        HIP_TRY(hipMemcpy(h.data(), ctx->d_wave_log, n_wave * 32, hipMemcpyDeviceToHost));
         if (FILE *f = std::fopen(log_path, "wb")) {
-            std::fwrite(h.data(), 16, n_wave, f);
+            std::fwrite(h.data(), 32, n_wave, f);
             std::fclose(f);
         }
     }
@@ -343,6 +365,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(3, std::atoi(k)));
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_BLOCK")) { const int b = std::atoi(k); ctx->block = (b == 256 || b == 128) ? b : 64; }
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));

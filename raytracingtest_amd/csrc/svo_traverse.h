@@ -53,16 +53,19 @@ struct LaunchParams {
     int flat;             // 1: branch-flattened iteration (default), 0: branchy reference form
     int block;            // tile kernel workgroup size: 64 (one 8x8 wave) or 256 (16x16 pixels)
     int shadows;          // 1: second pass, one shadow ray per primary hit (needs hits)
-    uint32_t *wave_log;   // diagnostics (env SVO_WAVE_LOG): per wave {t0, t1, HW_ID, XCC_ID | trips << 8}
+    uint32_t *wave_log;   // diagnostics (env SVO_WAVE_LOG): per wave {t0, t1, HW_ID, XCC_ID | trips << 8,
+                          //   loop cycles, fetch-wait cycles, fetch trips, pop trips} (instrumented loop)
     // Cost-ordered dispatch (64-thread tile kernel): block b traces 8x8 tile
     // tile_order[b] (null = b) and records its wave trip count in tile_cost.
-    const uint32_t *tile_order;
+    const uint32_t *tile_order;   // n_tiles entries + 4 class boundaries
     uint16_t *tile_cost;
+    int prio;                     // s_setprio by cost class (env SVO_PRIO)
 };
 
 // Order the tiles by recorded cost, most expensive class first, into `order`
-// (one workgroup, no atomics).  Placement only: any order gives identical
-// results.  `cost` must hold order_cost_capacity(n_tiles) entries (the tail
+// (one workgroup, no atomics), followed by the 4 cumulative class sizes
+// (order must hold n_tiles + 4 entries).  Placement only: any order gives
+// identical results.  `cost` must hold order_cost_capacity(n_tiles) entries (the tail
 // beyond n_tiles is read, never used).
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream);
 size_t order_cost_capacity(int n_tiles);

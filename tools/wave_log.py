@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--camera", default="flyover")
     ap.add_argument("--max-level", type=int, default=11)
     ap.add_argument("--out", default="gpurun_out/wave_log.bin")
+    ap.add_argument("--tile-row", type=int, default=-1, help="render only this 8-row band (a near-empty GPU)")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     os.environ["SVO_WAVE_LOG"] = os.path.abspath(args.out)
@@ -37,10 +38,11 @@ def main():
     rm.UpdateShaderParameters(CAMERAS[args.camera](), W, H)
     hits = torch.empty(W * H * 24, dtype=torch.uint8, device="cuda")
     rgba = torch.empty(W * H * 4, dtype=torch.float32, device="cuda")
+    band = None if args.tile_row < 0 else (8, args.tile_row, H // 8)
     for _ in range(3):
-        rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr())
+        rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr(), band=band)
     rm.synchronize()
-    log = np.fromfile(args.out, np.uint32).reshape(-1, 4)
+    log = np.fromfile(args.out, np.uint32).reshape(-1, 8)
     log = log[(log[:, 0] != 0) | (log[:, 1] != 0)]
     t0 = log[:, 0].astype(np.int64)
     t1 = log[:, 1].astype(np.int64)
@@ -73,8 +75,20 @@ def main():
     # duration vs screen position (block order = row-major tiles)
     ntx = W // 8
     ty = np.arange(len(log)) // ntx
-    rows = [dur[ty == y].mean() for y in range(0, ty.max() + 1, 15)]
-    print("mean wave us per 15 tile-rows (top->bottom):", " ".join(f"{v:.1f}" for v in rows))
+    if ty.max() >= 15:
+        rows = [dur[ty == y].mean() for y in range(0, ty.max() + 1, 15)]
+        print("mean wave us per 15 tile-rows (top->bottom):", " ".join(f"{v:.1f}" for v in rows))
+    # instrumented loop (s_memtime shader cycles): where the heavy waves spend their trips
+    loop_c = log[:, 4].astype(np.float64)
+    fetch_c = log[:, 5].astype(np.float64)
+    ft = log[:, 6].astype(np.float64)
+    pt = log[:, 7].astype(np.float64)
+    heavy = trips >= np.percentile(trips, 99)
+    for name, m in (("all", np.ones(len(trips), bool)), ("top 1% trips", heavy)):
+        tr = trips[m].sum()
+        print(f"{name}: cycles/trip {loop_c[m].sum() / tr:.0f}, fetch-wait cycles/trip {fetch_c[m].sum() / tr:.0f}"
+              f" (per fetching trip {fetch_c[m].sum() / max(ft[m].sum(), 1):.0f}), fetching trips {ft[m].sum() / tr:.2f},"
+              f" popping trips {pt[m].sum() / tr:.2f}")
     hw = log[:, 2]
     xcc = log[:, 3] & 0xFF
     print("waves per XCC:", np.bincount(xcc, minlength=8)[:8])
