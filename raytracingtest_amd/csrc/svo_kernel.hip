@@ -499,7 +499,7 @@ __device__ __forceinline__ void from_fray(const FRay &f, Ray &r) {
 }
 
 struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
-    uint64_t fetch_cycles = 0, loop_cycles = 0;
+    uint64_t fetch_cycles = 0, loop_cycles = 0;   // fetch_cycles: unused (0)
     uint32_t fetch_trips = 0, pop_trips = 0;
 };
 
@@ -519,23 +519,16 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     int it = 0;
     uint64_t tl0 = 0;
     if (DIAG) tl0 = __builtin_amdgcn_s_memtime();
-    while (act != 0) {
+    while (act != 0 && it < MAX_ITERS) {   // one exit: the cap is part of the loop test
         // wave-uniform trip count kept in an SGPR (LLVM otherwise counts down in a VGPR)
         asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
-        if (it > MAX_ITERS) { capped = act; break; }
         const lmask need = act & ~cached;
-        uint64_t tf0 = 0;
-        if (DIAG && need) tf0 = __builtin_amdgcn_s_memtime();
         if (LM_ON(need)) {                               // N:60-62
             const uint2 nd = p.nodes[r.parent];
             r.cd16 = nd.x << 16;
             r.first = nd.y;
         }
-        if (DIAG && need) {                              // wait for the data, then stamp
-            asm volatile("v_mov_b32 %0, %0" : "+v"(r.first));
-            diag->fetch_cycles += __builtin_amdgcn_s_memtime() - tf0;
-            diag->fetch_trips += 1;
-        }
+        if (DIAG && need) diag->fetch_trips += 1;
         cached |= need;
         const float tx = r.px * r.cx - r.bx;             // N:67-70
         const float ty = r.py * r.cy - r.by;
@@ -619,6 +612,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         ovf |= of;
         act &= ~(hit | of | out);
     }
+    capped = act;                          // still tracing after MAX_ITERS trips
     if (DIAG) diag->loop_cycles = __builtin_amdgcn_s_memtime() - tl0;
     r.idx = (LM_ON(ix) ? 1 : 0) | (LM_ON(iy) ? 2 : 0) | (LM_ON(iz) ? 4 : 0);
     r.trips = it;
