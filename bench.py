@@ -37,24 +37,43 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 METRIC = "Mrays/sec + achieved HBM GB/s, 1920x1080 primary rays, depth-10 SVO"
 
 
+# BASELINE.json configs; C3 is the metric's workload.  C1-C3
+# trace in the HLSL stack mode, C4-C5 (> 2^24 nodes) in the exact one.
+CONFIGS = {
+    "C1": dict(width=256, height=256, max_level=7, sampler=4, camera="main", svo="sampler", stack_mode=0),
+    "C2": dict(width=1920, height=1080, max_level=9, sampler=-1, camera="overview", svo="menger", stack_mode=0),
+    "C3": dict(width=1920, height=1080, max_level=11, sampler=4, camera="flyover", svo="sampler", stack_mode=0),
+    "C4": dict(width=3840, height=2160, max_level=13, sampler=4, camera="overview", svo="sampler", stack_mode=1),
+    "C5": dict(width=7680, height=4320, max_level=14, sampler=4, camera="overview", svo="sampler", stack_mode=1),
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
-    p.add_argument("--max-level", type=int, default=11, help="NaiveCreator maxLevel (depth + 1)")
-    p.add_argument("--sampler", type=int, default=4, help="SampleFunctions.Type (4 = Custom1)")
-    p.add_argument("--stack-mode", type=int, default=0, help="0 = HLSL float2 stack, 1 = exact")
+    p.add_argument("--config", choices=sorted(CONFIGS), default="C3",
+                   help="BASELINE.json workload; the flags below override its fields")
+    p.add_argument("--width", type=int, default=None)
+    p.add_argument("--height", type=int, default=None)
+    p.add_argument("--max-level", type=int, default=None, help="NaiveCreator maxLevel (depth + 1)")
+    p.add_argument("--sampler", type=int, default=None, help="SampleFunctions.Type (4 = Custom1)")
+    p.add_argument("--stack-mode", type=int, default=None, help="0 = HLSL float2 stack, 1 = exact")
     p.add_argument("--split", choices=["samples", "bands"], default="samples")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--no-rgba", action="store_true")
-    p.add_argument("--camera", choices=["flyover", "overview", "main"], default="flyover")
+    p.add_argument("--camera", choices=["flyover", "overview", "main"], default=None)
     p.add_argument("--shadows", action="store_true", help="C3 '+1 shadow ray' pass after the primary rays")
     p.add_argument("--accumulate", action="store_true",
                    help="samples mode: all-reduce the RGBA samples (progressive accumulation) every step")
-    return p.parse_args()
+    a = p.parse_args()
+    cfg = CONFIGS[a.config]
+    for k in ("width", "height", "max_level", "sampler", "camera", "stack_mode"):
+        if getattr(a, k) is None:
+            setattr(a, k, cfg[k])
+    a.svo = cfg["svo"]
+    return a
 
 
 def main():
@@ -82,7 +101,11 @@ def main():
 
     W, H = args.width, args.height
     t0 = time.time()
-    svo = build_sampler_svo(args.sampler, args.max_level, device=dev.index)
+    if args.svo == "menger":   # 256^3 Menger sponge surface voxels
+        from raytracingtest_amd.builder import build_menger
+        svo = build_menger(depth=args.max_level - 1)
+    else:
+        svo = build_sampler_svo(args.sampler, args.max_level, device=dev.index)
     build_s = time.time() - t0
     n_nodes = len(svo)
 
@@ -162,7 +185,8 @@ def main():
 
     if rank == 0:
         cpu = cpu_baseline(args, svo, cam, off, host_hits) if (world == 1 and args.cpu_seconds > 0) else None
-        workload = (f"C3 depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) Custom1 SVO, "
+        kind = "Menger" if args.svo == "menger" else "Custom1"
+        workload = (f"{args.config} depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) {kind} SVO, "
                     f"{W}x{H} primary rays" + (" + 1 shadow ray per hit" if args.shadows else "") +
                     f", {args.camera} camera")
         traffic = pmc_traffic(workload)
@@ -178,7 +202,8 @@ def main():
             "scaling": "weak" if args.split == "samples" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement",
+            "data": ("synthetic: 256^3 Menger sponge surface SVO (SURVEY.md 8(d) C2)" if args.svo == "menger" else
+                     "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement"),
             "config": {"workload": workload,
                        "svo_nodes": n_nodes, "svo_format": "V%d" % svo.format, "svo_leaves": getattr(svo, "n_leaves", None),
                        "build_s": round(build_s, 2), "stack_mode": "hlsl" if args.stack_mode == 0 else "exact",

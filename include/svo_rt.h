@@ -110,6 +110,16 @@ int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode,
 enum { SVO_OPT_SHADOW_RAYS = 1 };
 int svo_set_options(svo_ctx *ctx, uint32_t options);
 
+/* ~ Graphics.Blit(Result, destination, AddMaterial) with _Sample = `sample`
+ * (RaytracingMaster.cs:70-73, AddShader.shader:10,44-47): progressive
+ * accumulation dst = src * a + dst * (1 - a), a = 1 / (sample + 1), on all four
+ * channels (source alpha = a).  d_accum and d_sample are device buffers of
+ * n_px RGBA32F pixels (16-byte aligned) on the context's device; `stream` as in
+ * svo_render_device.  The caller keeps `sample` (_currentSample): 0 after a
+ * camera change (RaytracingMaster.cs:44-47), +1 per frame. */
+int svo_accumulate(svo_ctx *ctx, void *d_accum, const void *d_sample, size_t n_px, uint32_t sample,
+                   void *stream);
+
 /* Information about the uploaded pool. */
 int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device);
 

@@ -56,6 +56,7 @@ def lib():
         L.orc_render.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp, vp]
         L.orc_render_pixels.argtypes = [vp, vp, i, i, vp, sz, i, i, vp, vp, vp]
         L.orc_v1_to_v2.argtypes = [vp, sz, vp]
+        L.orc_accumulate.argtypes = [vp, vp, sz, ctypes.c_uint32]
         _lib = L
     return _lib
 
@@ -156,3 +157,11 @@ def v1_to_v2(desc):
     out = np.zeros(len(desc), np.uint64)
     lib().orc_v1_to_v2(desc.ctypes.data, len(desc), out.ctypes.data)
     return out
+
+
+def accumulate(dst, src, sample):
+    """In-place AddShader blend of float32 RGBA frames (any shape [..., 4])."""
+    assert dst.dtype == np.float32 and src.dtype == np.float32 and dst.shape == src.shape
+    assert dst.flags.c_contiguous and src.flags.c_contiguous
+    lib().orc_accumulate(dst.ctypes.data, src.ctypes.data, dst.size // 4, int(sample))
+    return dst

@@ -405,6 +405,23 @@ void orc_render_pixels(const orc_svo *svo, const orc_camera *cam, int width, int
     run_threads(&job, nthreads, pixel_worker);
 }
 
+/* AddShader.shader:44-47 returns float4(Result.rgb, 1/(_Sample+1)); the pass
+ * blends with SrcAlpha / OneMinusSrcAlpha (:10), applied to all four channels
+ * (src alpha channel = a).  _Sample is the uint _currentSample
+ * (RaytracingMaster.cs:71-73), converted to float before the add. */
+void orc_accumulate(float *dst, const float *src, size_t n_px, uint32_t sample) {
+    const float a = 1.0f / ((float)sample + 1.0f);
+    const float b = 1.0f - a;
+    for (size_t i = 0; i < n_px; ++i) {
+        for (int c = 0; c < 4; ++c) {
+            const float s = c < 3 ? src[4 * i + c] : a;
+            float lhs = s * a;
+            float rhs = dst[4 * i + c] * b;
+            dst[4 * i + c] = lhs + rhs;
+        }
+    }
+}
+
 int orc_v1_to_v2(const int32_t *desc, size_t n, uint64_t *nodes_out) {
     for (size_t i = 0; i < n; ++i) {
         uint32_t cd = (uint32_t)desc[i];

@@ -97,6 +97,11 @@ void orc_render_pixels(const orc_svo *svo, const orc_camera *cam, int width, int
                        const uint32_t *pixels, size_t n, int stack_mode, int nthreads,
                        orc_hit *hits, float *rgba, uint32_t *fetches);
 
+/* Progressive accumulation, RaytracingMaster.cs:70-73 + AddShader.shader:44-47
+ * (Blend SrcAlpha OneMinusSrcAlpha, alpha = 1/(_Sample+1)) on n RGBA float4
+ * pixels: dst = src * a + dst * (1 - a), every channel, f32. */
+void orc_accumulate(float *dst, const float *src, size_t n_px, uint32_t sample);
+
 /* Relative (V1) -> V2 conversion used by the oracle's own V2 path. */
 int  orc_v1_to_v2(const int32_t *desc, size_t n, uint64_t *nodes_out);
 

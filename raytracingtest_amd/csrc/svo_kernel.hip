@@ -1020,6 +1020,37 @@ hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------- accumulation
+// AddShader.shader:44-47 + Blend SrcAlpha OneMinusSrcAlpha (:10), driven by
+// RaytracingMaster.cs:70-73: dst = src * a + dst * (1 - a), a = 1/(sample+1),
+// on all four channels (the source alpha is a).  Pure HBM streaming: 16 B read
+// of the sample + 16 B read and 16 B write of the accumulation per pixel,
+// float4 per lane, grid-stride.
+__global__ __launch_bounds__(256) void accumulate_kernel(float4 *__restrict__ dst, const float4 *__restrict__ src,
+                                                         size_t n, float a, float b) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float4 s = src[i];
+        float4 d = dst[i];
+        d.x = s.x * a + d.x * b;
+        d.y = s.y * a + d.y * b;
+        d.z = s.z * a + d.z * b;
+        d.w = a * a + d.w * b;
+        dst[i] = d;
+    }
+}
+
+hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32_t sample, int num_cus,
+                             hipStream_t stream) {
+    if (n_px == 0) return hipSuccess;
+    const float a = 1.0f / ((float)sample + 1.0f);
+    const float b = 1.0f - a;
+    const size_t want = (n_px + 255) / 256;
+    const unsigned blocks = (unsigned)std::min<size_t>(want, (size_t)num_cus * 16);
+    hipLaunchKernelGGL(accumulate_kernel, dim3(blocks), dim3(256), 0, stream, dst, src, n_px, a, b);
+    return hipGetLastError();
+}
+
 template <int MODE>
 static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
     const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;

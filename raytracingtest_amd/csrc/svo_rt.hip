@@ -495,6 +495,20 @@ int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device) {
     return SVO_OK;
 }
 
+int svo_accumulate(svo_ctx *ctx, void *d_accum, const void *d_sample, size_t n_px, uint32_t sample,
+                   void *stream) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (n_px == 0) return SVO_OK;
+    if (!d_accum || !d_sample) return fail(SVO_ERR_ARG, "null accumulation or sample buffer");
+    if (((uintptr_t)d_accum | (uintptr_t)d_sample) & 15u) return fail(SVO_ERR_ARG, "buffers must be 16-byte aligned");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipError_t e = svo::launch_accumulate(reinterpret_cast<float4 *>(d_accum), reinterpret_cast<const float4 *>(d_sample),
+                                          n_px, sample, ctx->num_cus, s);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("accumulate launch: ") + hipGetErrorString(e));
+    return SVO_OK;
+}
+
 int svo_synchronize(svo_ctx *ctx) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
     HIP_TRY(hipSetDevice(ctx->device));

@@ -70,6 +70,10 @@ struct LaunchParams {
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream);
 size_t order_cost_capacity(int n_tiles);
 
+// Progressive accumulation (AddShader blend) of an RGBA32F sample frame.
+hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32_t sample, int num_cus,
+                             hipStream_t stream);
+
 // kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).
 // counter: 16-byte device work counter (persistent kernel), num_cus: CU count.
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel,

@@ -7,6 +7,8 @@ Same names and argument meaning as the reference:
   SetSVOBuffer()                 RaytracingMaster.cs:90-109  (rebuild from maxLevel / sampleType)
   UpdateShaderParameters(...)    RaytracingMaster.cs:32-41
   Render(width, height)          RaytracingMaster.cs:60-74   (Dispatch + result)
+  accumulate_device(...)         RaytracingMaster.cs:70-73 + AddShader.shader (Blit with _Sample,
+                                 then _currentSample++; reset to 0 when the camera moves, :44-47)
 Errors surface as SvoError (the C-ABI status + svo_last_error text) instead of
 Unity's silent shader failures.  There is no CPU fallback.
 """
@@ -31,6 +33,8 @@ class RaytracingMaster:
         self.sampleType = sampleType    # SampleFunctions.Type.Custom1 = 4 (:18)
         self._ctx = ctypes.c_void_p()
         self._camera_set = False
+        self._c2w = None
+        self.currentSample = 0          # _currentSample (RaytracingMaster.cs:12)
         self.InitializeSVOBuffer()
 
     # ------------------------------------------------------------------ setup
@@ -69,6 +73,10 @@ class RaytracingMaster:
         else:
             c2w, inv_proj = camera.uniforms(width, height)
         light = main_light() if light is None else np.asarray(light, np.float32)
+        c2w = np.asarray(c2w, np.float32)
+        if self._c2w is None or not np.array_equal(self._c2w, c2w):   # transform.hasChanged (:44-47)
+            self.currentSample = 0
+            self._c2w = c2w.copy()
         c = column_major(c2w)
         p = column_major(inv_proj)
         lt = np.ascontiguousarray(light, np.float32)
@@ -103,6 +111,15 @@ class RaytracingMaster:
         b = None if band is None else ctypes.byref(SvoBand(*band))
         check(_lib.lib().svo_count_fetches(self._ctx, width, height, stack_mode, b, fetch_ptr, stream),
               "svo_count_fetches")
+
+    def accumulate_device(self, accum_ptr, sample_ptr, n_px, sample=None, stream=None):
+        """Blend one RGBA32F sample frame into the accumulation frame (device
+        pointers) with _Sample = `sample` (default: currentSample, which then
+        advances like _currentSample++ after the Blit)."""
+        n = self.currentSample if sample is None else int(sample)
+        check(_lib.lib().svo_accumulate(self._ctx, accum_ptr, sample_ptr, int(n_px), n, stream), "svo_accumulate")
+        if sample is None:
+            self.currentSample += 1
 
     def synchronize(self):
         check(_lib.lib().svo_synchronize(self._ctx), "svo_synchronize")

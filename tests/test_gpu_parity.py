@@ -231,3 +231,34 @@ def test_shadow_rays_parity(rm, oracle_mod, mode):
     n_sh = int(np.count_nonzero(ref_hits["flags"] & 8))
     assert 0 < n_sh < np.count_nonzero(ref_hits["flags"] & 1)
     _compare(hits, rgba, ref_hits, ref_rgba)
+
+
+def test_accumulate_matches_oracle(rm, oracle_mod):
+    """svo_accumulate (AddShader blend) == the C restatement, bit for bit, over a
+    sequence of samples; currentSample advances per blit and resets when the
+    camera transform changes (RaytracingMaster.cs:44-47,70-73)."""
+    import torch
+    rng = np.random.default_rng(11)
+    n_px = 1000 * 37 + 3                      # not a multiple of the grid stride
+    acc_h = rng.random((n_px, 4), dtype=np.float32)
+    acc_d = torch.from_numpy(acc_h.copy()).cuda()
+    rm.UpdateShaderParameters(overview_camera(), 64, 64)
+    assert rm.currentSample == 0
+    for n in range(5):
+        smp_h = rng.random((n_px, 4), dtype=np.float32)
+        smp_d = torch.from_numpy(smp_h).cuda()
+        rm.accumulate_device(acc_d.data_ptr(), smp_d.data_ptr(), n_px)
+        oracle_mod.accumulate(acc_h, smp_h, n)
+    rm.synchronize()
+    torch.cuda.synchronize()
+    assert rm.currentSample == 5
+    assert acc_d.cpu().numpy().tobytes() == acc_h.tobytes()
+    smp_d = torch.from_numpy(rng.random((n_px, 4), dtype=np.float32)).cuda()
+    rm.accumulate_device(acc_d.data_ptr(), smp_d.data_ptr(), n_px, sample=1000)
+    oracle_mod.accumulate(acc_h, smp_d.cpu().numpy(), 1000)
+    rm.synchronize()
+    assert acc_d.cpu().numpy().tobytes() == acc_h.tobytes()
+    rm.UpdateShaderParameters(main_camera(), 64, 64)   # camera moved -> restart
+    assert rm.currentSample == 0
+    with pytest.raises(SvoError):
+        rm.accumulate_device(acc_d.data_ptr() + 4, smp_d.data_ptr(), n_px)

@@ -193,3 +193,27 @@ def test_hlsl_stack_roundtrip_rarely_changes_hits(oracle_mod, text_svo):
     h1, _, _ = oracle_mod.render(osvo, cam, 128, 128, 1)
     diff = np.count_nonzero((h0["parent"] != h1["parent"]) | (h0["hit_idx"] != h1["hit_idx"]))
     assert diff <= len(h0) // 1000
+
+
+def test_accumulate_known_answers(oracle_mod):
+    """AddShader blend (AddShader.shader:10,44-47): sample 0 replaces the frame,
+    sample n weights the new frame 1/(n+1); a constant stream stays constant and
+    n frames average (f32 formula, written out here in numpy)."""
+    rng = np.random.default_rng(3)
+    dst = rng.random((7, 5, 4), dtype=np.float32)
+    src = rng.random((7, 5, 4), dtype=np.float32)
+    out = oracle_mod.accumulate(dst.copy(), src, 0)
+    assert np.array_equal(out[..., :3], src[..., :3]) and np.all(out[..., 3] == 1.0)
+    for n in (1, 2, 7, 1000):
+        a = np.float32(1.0) / (np.float32(n) + np.float32(1.0))
+        b = np.float32(1.0) - a
+        want = dst.copy()
+        want[..., :3] = src[..., :3] * a + dst[..., :3] * b
+        want[..., 3] = a * a + dst[..., 3] * b
+        got = oracle_mod.accumulate(dst.copy(), src, n)
+        assert got.tobytes() == want.tobytes(), n
+    acc = np.zeros((3, 3, 4), np.float32)
+    frames = rng.random((6, 3, 3, 4), dtype=np.float32)
+    for n, f in enumerate(frames):
+        oracle_mod.accumulate(acc, np.ascontiguousarray(f), n)
+    np.testing.assert_allclose(acc[..., :3], frames[..., :3].mean(0), rtol=1e-5)
