@@ -503,9 +503,12 @@ struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
     uint32_t fetch_trips = 0, pop_trips = 0;
 };
 
-template <int MODE, int STRIDE, bool DIAG = false>
+template <int MODE, int STRIDE, bool GUARD, bool DIAG = false>
 __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk,
                                            LeanDiag *diag = nullptr) {
+    // GUARD = false (host-proven, svo_rt.hip recompute_depth): one tree of known
+    // depth and parent indices below 2^24, so a PUSH never overflows the stack
+    // and the HLSL round trip of a parent index is the identity.
     const int slots = p.slots;
     for (int s = 0; s < slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
     const int scale_lo = S_MAX - slots;
@@ -514,8 +517,8 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     lmask ix = LM_OF(r.idx & 1), iy = LM_OF(r.idx & 2), iz = LM_OF(r.idx & 4);
     const lmask ox = LM_OF(r.octant_mask & 1), oy = LM_OF(r.octant_mask & 2), oz = LM_OF(r.octant_mask & 4);
     lmask cached = 0, capped = 0, ovf = 0;
-    const uint32_t push_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk -
-                               (uint32_t)(104 + scale_lo) * (uint32_t)(STRIDE * sizeof(uint2));
+    const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
+    const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * (uint32_t)(STRIDE * sizeof(uint2));
     int it = 0;
     uint64_t tl0 = 0;
     if (DIAG) tl0 = __builtin_amdgcn_s_memtime();
@@ -541,7 +544,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
         const lmask hit = descend & leaf;                // N:93-94
         const lmask store = descend & ~leaf & LM_OF(tc_max < r.h);
-        const lmask of = store & LM_OF(r.sexp < sexp_lo);
+        const lmask of = GUARD ? (store & LM_OF(r.sexp < sexp_lo)) : (lmask)0;
         const lmask push = descend & ~leaf & ~of;
         const lmask adv = act & ~descend;
         if (LM_ON(store & ~of)) {                        // N:97-98 (raw; round trip on POP)
@@ -574,40 +577,39 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         ix = (push & cx) | (~push & (ix ^ sx));
         iy = (push & cy) | (~push & (iy ^ sy));
         iz = (push & cz) | (~push & (iz ^ sz));
-        cached &= ~push;
+        cached &= ~(push | pop);
         r.px = qx; r.py = qy; r.pz = qz;
         lmask out = 0;
-        if (pop != 0) {
+        if (pop != 0) {                                  // N:134-154
+            // Evaluated by the whole wave (a divergent region costs exec
+            // bookkeeping and copies of values live on both sides); the popping
+            // lanes take the results.  Other lanes read an in-range slot.
             if (DIAG) diag->pop_trips += 1;
-            uint32_t bit = 0;
-            if (LM_ON(pop)) {                            // N:134-154
-                uint32_t differing = 0;
-                if (LM_ON(sx)) differing |= __float_as_uint(qx) ^ __float_as_uint(qx + se);
-                if (LM_ON(sy)) differing |= __float_as_uint(qy) ^ __float_as_uint(qy + se);
-                if (LM_ON(sz)) differing |= __float_as_uint(qz) ^ __float_as_uint(qz + se);
-                const uint32_t fd = __float_as_uint((float)differing);
-                const int scale = (int)(fd >> 23) - 127;
-                r.sexp = __uint_as_float((fd & 0x7F800000u) - (23u << 23));
-                const uint2 e = stk[(scale - scale_lo) * STRIDE];   // slot == slots only when leaving the root
-                uint32_t pa = e.x, tm = e.y;
-                if (MODE == 0) {                         // int2 <- float2((int)parent, asint(t_max))
-                    pa = (uint32_t)cvt_i32((float)(int32_t)pa);
-                    tm = (uint32_t)cvt_i32((float)(int32_t)tm);
-                }
-                r.parent = pa;
-                r.t_max = __uint_as_float(tm);
-                const uint32_t keep = 0xFFFFFFFFu << scale;
-                bit = 1u << scale;
-                r.px = __uint_as_float(__float_as_uint(qx) & keep);
-                r.py = __uint_as_float(__float_as_uint(qy) & keep);
-                r.pz = __uint_as_float(__float_as_uint(qz) & keep);
-                r.h = 0.0f;
+            const uint32_t dx = LM_ON(sx) ? (__float_as_uint(qx) ^ __float_as_uint(qx + se)) : 0u;
+            const uint32_t dy = LM_ON(sy) ? (__float_as_uint(qy) ^ __float_as_uint(qy + se)) : 0u;
+            const uint32_t dz = LM_ON(sz) ? (__float_as_uint(qz) ^ __float_as_uint(qz + se)) : 0u;
+            const uint32_t fd = __float_as_uint((float)(dx | dy | dz));
+            const int scale = (int)(fd >> 23) - 127;
+            const int slot = min(max(scale - scale_lo, 0), slots);
+            const uint2 e = stk[slot * STRIDE];          // slot == slots only when leaving the root
+            uint32_t pa = e.x, tm = e.y;
+            if (MODE == 0) {                             // int2 <- float2((int)parent, asint(t_max))
+                if (GUARD) pa = (uint32_t)cvt_i32((float)(int32_t)pa);
+                tm = (uint32_t)cvt_i32((float)(int32_t)tm);
             }
+            const uint32_t keep = 0xFFFFFFFFu << scale, bit = 1u << scale;
+            const bool pl = LM_ON(pop);
+            r.sexp = pl ? __uint_as_float((fd & 0x7F800000u) - (23u << 23)) : r.sexp;
+            r.parent = pl ? pa : r.parent;
+            r.t_max = pl ? __uint_as_float(tm) : r.t_max;
+            r.px = pl ? __uint_as_float(__float_as_uint(qx) & keep) : r.px;
+            r.py = pl ? __uint_as_float(__float_as_uint(qy) & keep) : r.py;
+            r.pz = pl ? __uint_as_float(__float_as_uint(qz) & keep) : r.pz;
+            r.h = pl ? 0.0f : r.h;
             ix = (ix & ~pop) | (pop & LM_OF((__float_as_uint(qx) & bit) != 0u));
             iy = (iy & ~pop) | (pop & LM_OF((__float_as_uint(qy) & bit) != 0u));
             iz = (iz & ~pop) | (pop & LM_OF((__float_as_uint(qz) & bit) != 0u));
-            cached &= ~pop;
-            out = pop & LM_OF(r.sexp >= 1.0f);
+            out = pop & LM_OF(scale >= S_MAX);
         }
         ovf |= of;
         act &= ~(hit | of | out);
@@ -719,8 +721,12 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
         FRay f;
         to_fray(r, f);
         LeanDiag dg;
-        if (p.wave_log) trace_lean<MODE, BS, true>(p, f, stk, &dg);
-        else trace_lean<MODE, BS>(p, f, stk);
+        if (p.wave_log) {
+            if (p.guard) trace_lean<MODE, BS, true, true>(p, f, stk, &dg);
+            else trace_lean<MODE, BS, false, true>(p, f, stk, &dg);
+        }
+        else if (p.guard) trace_lean<MODE, BS, true>(p, f, stk);
+        else trace_lean<MODE, BS, false>(p, f, stk);
         from_fray(f, r);
         if (BS == 64 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every lane
         if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID

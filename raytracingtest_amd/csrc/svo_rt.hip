@@ -48,6 +48,7 @@ struct Upload {
     size_t offset, count;
     int depth;
     bool external;   // has child links outside its own range (sub-SVO linking)
+    bool tree;       // every node reached once from the upload's first node (no sharing, no cycles)
 };
 
 }  // namespace
@@ -65,6 +66,7 @@ struct svo_ctx {
     bool cam_set = false;
     std::vector<Upload> uploads;
     int depth = 0;
+    bool depth_exact = false;        // see recompute_depth
     // host-path output scratch
     void *d_out_hits = nullptr;
     void *d_out_rgba = nullptr;
@@ -113,7 +115,8 @@ __global__ void convert_v1_kernel(const int32_t *__restrict__ desc, uint2 *__res
 // Host-side level walk: validates every non-leaf child index and returns the
 // number of descriptor levels reachable from the upload's first node.
 int walk_depth(const uint32_t *lo, const uint32_t *first, size_t n, size_t base, size_t pool_n,
-               int *depth_out, bool *external_out, std::string *err) {
+               int *depth_out, bool *external_out, bool *tree_out, std::string *err) {
+    *tree_out = true;
     std::vector<uint8_t> seen(n, 0);
     std::vector<uint32_t> cur{0}, nxt;
     int depth = 0;
@@ -138,7 +141,7 @@ int walk_depth(const uint32_t *lo, const uint32_t *first, size_t n, size_t base,
                 }
                 if (child < base || child >= base + n) { external = true; continue; }
                 uint32_t cl = (uint32_t)(child - base);
-                if (seen[cl]) continue;   // shared subtrees are legal; cycles are bounded by depth
+                if (seen[cl]) { *tree_out = false; continue; }   // shared subtrees are legal (DAG)
                 seen[cl] = 1;
                 nxt.push_back(cl);
             }
@@ -160,18 +163,23 @@ void recompute_depth(svo_ctx *ctx) {
     }
     ctx->depth = root_depth + (ext ? other : 0);
     if (ctx->depth > 22) ctx->depth = 22;
+    // A single self-contained tree at offset 0: every descent path has at most
+    // `depth` levels, so the traversal stack cannot overflow while parents are
+    // exact (the kernel may then drop its overflow guard).
+    ctx->depth_exact = ctx->uploads.size() == 1 && ctx->uploads[0].offset == 0 && !ctx->uploads[0].external &&
+                       ctx->uploads[0].tree && ctx->depth <= 22 && root_depth == ctx->depth;
 }
 
 int record_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, size_t n, size_t base) {
     std::string err;
     int depth = 0;
-    bool ext = false;
+    bool ext = false, tree = true;
     size_t pool_n = std::max(ctx->n_nodes, base + n);
-    if (walk_depth(lo, first, n, base, pool_n, &depth, &ext, &err) != 0) return fail(SVO_ERR_FORMAT, err);
+    if (walk_depth(lo, first, n, base, pool_n, &depth, &ext, &tree, &err) != 0) return fail(SVO_ERR_FORMAT, err);
     ctx->uploads.erase(std::remove_if(ctx->uploads.begin(), ctx->uploads.end(),
                                       [&](const Upload &u) { return u.offset == base; }),
                        ctx->uploads.end());
-    ctx->uploads.push_back({base, n, depth, ext});
+    ctx->uploads.push_back({base, n, depth, ext, tree});
     ctx->n_nodes = pool_n;
     recompute_depth(ctx);
     return SVO_OK;
@@ -229,6 +237,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.band_count = b.band_count;
     p.local_rows = band_rows_local(height, b);
     p.slots = std::max(ctx->depth - 1, 1);
+    // guard: stack-overflow test + HLSL parent round trip, needed unless the
+    // pool is one tree of known depth whose parent indices are exact in f32
+    p.guard = !ctx->depth_exact || (stack_mode == 0 && ctx->n_nodes > ((size_t)1 << 24));
     p.hits = reinterpret_cast<svo::Hit *>(d_hits);
     p.rgba = reinterpret_cast<float4 *>(d_rgba);
     p.fetches = d_fetch;

@@ -60,6 +60,7 @@ struct LaunchParams {
     const uint32_t *tile_order;   // n_tiles entries + 4 class boundaries
     uint16_t *tile_cost;
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
+    int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
 };
 
 // Order the tiles by recorded cost, most expensive class first, into `order`

@@ -42,6 +42,16 @@ def main():
     for _ in range(3):
         rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr(), band=band)
     rm.synchronize()
+    # uninstrumented timing of the same launch (the log is only taken while SVO_WAVE_LOG is set)
+    del os.environ["SVO_WAVE_LOG"]
+    s = torch.cuda.Stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+    for a, b in evs:
+        a.record(s)
+        rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr(), band=band, stream=s.cuda_stream)
+        b.record(s)
+    torch.cuda.synchronize()
+    print(f"uninstrumented launch: {np.median([a.elapsed_time(b) for a, b in evs]) * 1e3:.1f} us (median of 10)")
     log = np.fromfile(args.out, np.uint32).reshape(-1, 8)
     log = log[(log[:, 0] != 0) | (log[:, 1] != 0)]
     t0 = log[:, 0].astype(np.int64)
