@@ -514,8 +514,8 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     const int scale_lo = S_MAX - slots;
     const float sexp_lo = __int_as_float((scale_lo - S_MAX + 127) << 23);   // push below scale_lo overflows
     lmask act = LM_OF(true);
-    lmask ix = LM_OF(r.idx & 1), iy = LM_OF(r.idx & 2), iz = LM_OF(r.idx & 4);
-    const lmask ox = LM_OF(r.octant_mask & 1), oy = LM_OF(r.octant_mask & 2), oz = LM_OF(r.octant_mask & 4);
+    int idx = r.idx;                       // child index bits (per lane, VGPR)
+    const int oct = r.octant_mask;
     lmask cached = 0, capped = 0, ovf = 0;
     const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
     const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * (uint32_t)(STRIDE * sizeof(uint2));
@@ -537,8 +537,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const float ty = r.py * r.cy - r.by;
         const float tz = r.pz * r.cz - r.bz;
         const float tc_max = fminf(fminf(tx, ty), tz);
-        const int k = lanes_to_idx(ix ^ ox, iy ^ oy, iz ^ oz);
-        const uint32_t cm = r.cd16 << k;                 // valid bit -> bit 31, leaf bit -> bit 23
+        const uint32_t cm = r.cd16 << (idx ^ oct);       // valid bit -> bit 31, leaf bit -> bit 23
         const float tv_max = vmin(r.t_max, tc_max);
         const lmask descend = act & LM_OF((int32_t)cm < 0) & LM_OF(r.t_min <= tv_max);
         const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
@@ -565,8 +564,11 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const float qx = r.px + (LM_ON((push & cx) | sx) ? delta : 0.0f);
         const float qy = r.py + (LM_ON((push & cy) | sy) ? delta : 0.0f);
         const float qz = r.pz + (LM_ON((push & cz) | sz) ? delta : 0.0f);
-        const lmask pop = (sx & ~ix) | (sy & ~iy) | (sz & ~iz);   // N:130-131
+        const int step = lanes_to_idx(sx, sy, sz);       // 0 outside ADVANCE lanes
+        const lmask pop = LM_OF((step & ~idx) != 0);     // N:130-131: (idx ^ step) & step
         const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
+        const int cidx = lanes_to_idx(cx, cy, cz);
+        idx = LM_ON(push) ? cidx : (idx ^ step);
         if (LM_ON(push)) {
             r.parent = child;
             r.h = tc_max;
@@ -574,9 +576,6 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             r.sexp = half;
         }
         r.t_min = LM_ON(adv) ? tc_max : r.t_min;
-        ix = (push & cx) | (~push & (ix ^ sx));
-        iy = (push & cy) | (~push & (iy ^ sy));
-        iz = (push & cz) | (~push & (iz ^ sz));
         cached &= ~(push | pop);
         r.px = qx; r.py = qy; r.pz = qz;
         lmask out = 0;
@@ -597,7 +596,10 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
                 if (GUARD) pa = (uint32_t)cvt_i32((float)(int32_t)pa);
                 tm = (uint32_t)cvt_i32((float)(int32_t)tm);
             }
-            const uint32_t keep = 0xFFFFFFFFu << scale, bit = 1u << scale;
+            const uint32_t keep = 0xFFFFFFFFu << scale;
+            const uint32_t bx_ = __builtin_amdgcn_ubfe(__float_as_uint(qx), scale, 1);
+            const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
+            const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
             const bool pl = LM_ON(pop);
             r.sexp = pl ? __uint_as_float((fd & 0x7F800000u) - (23u << 23)) : r.sexp;
             r.parent = pl ? pa : r.parent;
@@ -606,9 +608,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             r.py = pl ? __uint_as_float(__float_as_uint(qy) & keep) : r.py;
             r.pz = pl ? __uint_as_float(__float_as_uint(qz) & keep) : r.pz;
             r.h = pl ? 0.0f : r.h;
-            ix = (ix & ~pop) | (pop & LM_OF((__float_as_uint(qx) & bit) != 0u));
-            iy = (iy & ~pop) | (pop & LM_OF((__float_as_uint(qy) & bit) != 0u));
-            iz = (iz & ~pop) | (pop & LM_OF((__float_as_uint(qz) & bit) != 0u));
+            idx = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) : idx;
             out = pop & LM_OF(scale >= S_MAX);
         }
         ovf |= of;
@@ -616,7 +616,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     }
     capped = act;                          // still tracing after MAX_ITERS trips
     if (DIAG) diag->loop_cycles = __builtin_amdgcn_s_memtime() - tl0;
-    r.idx = (LM_ON(ix) ? 1 : 0) | (LM_ON(iy) ? 2 : 0) | (LM_ON(iz) ? 4 : 0);
+    r.idx = idx;
     r.trips = it;
     if (LM_ON(capped)) r.flags |= 2u;
     if (LM_ON(ovf)) r.flags |= 4u;
