@@ -314,9 +314,10 @@ static void trace_pixel(const orc_svo *svo, const orc_camera *cam, int width, in
                         uint32_t *fetch_out) {
     float o[3], d[3], alb[3];
     orc_hit h;
-    uint32_t f = 0;
+    uint32_t f = 0, it = 0;
     orc_camera_ray(cam, x, y, width, height, o, d);
-    orc_intersect(svo, o, d, mode & 0xFF, &h, alb, &f, NULL);
+    orc_intersect(svo, o, d, mode & 0xFF, &h, alb, &f, &it);
+    if (mode & ORC_COUNT_ITERS) f = it;   /* diagnostics: loop iterations instead of fetches */
     int shadowed = 0;
     if ((mode & ORC_SHADOW_RAYS) && (h.flags & 1)) {
         shadowed = orc_shadow_ray(svo, cam, o, d, &h, mode);

@@ -42,6 +42,8 @@ enum { ORC_FMT_V1 = 1, ORC_FMT_V2 = 2 };
 enum { ORC_STACK_HLSL = 0, ORC_STACK_EXACT = 1 };
 /* OR-ed into the render mode: trace one shadow ray per primary hit. */
 #define ORC_SHADOW_RAYS 0x100
+/* OR into mode: the fetches output receives loop iterations (NVIDIASVO.compute:57) instead */
+#define ORC_COUNT_ITERS 0x200
 
 /* Per-pixel hit record: identical layout to svo_hit in include/svo_rt.h. */
 typedef struct orc_hit {

@@ -499,11 +499,11 @@ __device__ __forceinline__ void from_fray(const FRay &f, Ray &r) {
 }
 
 struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
-    uint64_t fetch_cycles = 0, loop_cycles = 0;   // fetch_cycles: unused (0)
+    uint64_t fetch_cycles = 0, loop_cycles = 0;   // fetch_cycles: push-only trips | adv-only trips << 16
     uint32_t fetch_trips = 0, pop_trips = 0;
 };
 
-template <int MODE, int STRIDE, bool GUARD, bool DIAG = false>
+template <int MODE, int STRIDE, bool GUARD, bool DIAG = false, bool V2 = false, bool PF = false, int PAD = 0>
 __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk,
                                            LeanDiag *diag = nullptr) {
     // GUARD = false (host-proven, svo_rt.hip recompute_depth): one tree of known
@@ -515,10 +515,19 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     const float sexp_lo = __int_as_float((scale_lo - S_MAX + 127) << 23);   // push below scale_lo overflows
     lmask act = LM_OF(true);
     int idx = r.idx;                       // child index bits (per lane, VGPR)
-    const int oct = r.octant_mask;
+    const int oct = V2 ? (r.octant_mask | 16) : r.octant_mask;   // V2: c ^ (oct | 16) == (c ^ oct) + 16
     lmask cached = 0, capped = 0, ovf = 0;
+    lmask pf = 0;          // PF: lanes whose next node is already in `spec`
+    uint2 spec = make_uint2(0u, 0u);
+    if (PF) asm volatile("" : "+v"(spec.x), "+v"(spec.y), "+v"(r.parent));   // per-lane values (LLVM uniformity)
     const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
-    const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * (uint32_t)(STRIDE * sizeof(uint2));
+    constexpr uint32_t SLOT = (uint32_t)(STRIDE * sizeof(uint2));
+    constexpr int SLOT_SH = 23 - (STRIDE == 64 ? 9 : STRIDE == 128 ? 10 : 11);   // (bits >> 23) * SLOT
+    static_assert(SLOT == (1u << (23 - SLOT_SH)), "stride must be 64, 128 or 256 lanes");
+    const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
+    // V2 POP: slot address from the exponent field e of float(differing), e = scale + 127
+    const uint2 *stk_pop = stk - (127 + scale_lo) * STRIDE;   // indexed by e (never below slot 1)
+    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots);   // leaving the root: the spare slot
     int it = 0;
     uint64_t tl0 = 0;
     if (DIAG) tl0 = __builtin_amdgcn_s_memtime();
@@ -526,19 +535,48 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         // wave-uniform trip count kept in an SGPR (LLVM otherwise counts down in a VGPR)
         asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
         const lmask need = act & ~cached;
-        if (LM_ON(need)) {                               // N:60-62
+        if (PF) {
+            // lanes that pushed last trip find their node in `spec` (loaded one trip early);
+            // the others (after a POP, or the root) fetch on demand
+            if (LM_ON(need & ~pf)) spec = p.nodes[r.parent];
+            if (LM_ON(need)) {
+                uint32_t x = spec.x;
+                asm volatile("" : "+v"(x));
+                r.cd16 = x;
+                r.first = spec.y;
+            }
+        } else if (LM_ON(need)) {                        // N:60-62
             const uint2 nd = p.nodes[r.parent];
-            r.cd16 = nd.x << 16;
+            uint32_t x = nd.x;
+            if (V2) asm volatile("" : "+v"(x));   // opaque VGPR value (works round an LLVM uniformity bug)
+            r.cd16 = V2 ? x : x << 16;
             r.first = nd.y;
         }
         if (DIAG && need) diag->fetch_trips += 1;
         cached |= need;
+        if (PAD == 1) {   // experiment: 8 extra independent VALU per trip
+            uint32_t j0 = 0, j1 = 0;
+            asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\t"
+                         "v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1" : "+v"(j0), "+v"(j1));
+        }
+        if (PAD == 2) {   // experiment: 8 extra independent SALU per trip
+            uint32_t j0 = 0, j1 = 0;
+            asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\t"
+                         "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1" : "+s"(j0), "+s"(j1) : : "scc");
+        }
         const float tx = r.px * r.cx - r.bx;             // N:67-70
         const float ty = r.py * r.cy - r.by;
         const float tz = r.pz * r.cz - r.bz;
         const float tc_max = fminf(fminf(tx, ty), tz);
         const uint32_t cm = r.cd16 << (idx ^ oct);       // valid bit -> bit 31, leaf bit -> bit 23
         const float tv_max = vmin(r.t_max, tc_max);
+        const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
+        if (PF) {
+            // speculative fetch of the child a PUSH would enter (valid, non-leaf): a PUSH
+            // implies it, so next trip's descriptor is in flight during this trip's math
+            const lmask cand = act & LM_OF((int32_t)(cm & 0x80800000u) == (int32_t)0x80800000u);
+            if (LM_ON(cand)) spec = p.nodes[child];
+        }
         const lmask descend = act & LM_OF((int32_t)cm < 0) & LM_OF(r.t_min <= tv_max);
         const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
         const lmask hit = descend & leaf;                // N:93-94
@@ -546,10 +584,16 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const lmask of = GUARD ? (store & LM_OF(r.sexp < sexp_lo)) : (lmask)0;
         const lmask push = descend & ~leaf & ~of;
         const lmask adv = act & ~descend;
+        if (DIAG) {   // wave-uniform trip kinds: PUSH lanes only / ADVANCE lanes only
+            if (adv == 0 && push != 0) diag->fetch_cycles += 1;
+            if (push == 0 && adv != 0) diag->fetch_cycles += 1u << 16;
+        }
         if (LM_ON(store & ~of)) {                        // N:97-98 (raw; round trip on POP)
             // slot = scale - scale_lo = (bits(scale_exp2) >> 23) - 104 - scale_lo; two dwords by
             // ds_write2_b32: no copy into an aligned register pair
-            const uint32_t a = push_base + (__float_as_uint(r.sexp) >> 23) * (uint32_t)(STRIDE * sizeof(uint2));
+            // V2: scale_exp2 is an exact power of two (zero mantissa), so the shift needs no mask
+            const uint32_t a = V2 ? push_base + (__float_as_uint(r.sexp) >> SLOT_SH)
+                                  : push_base + (__float_as_uint(r.sexp) >> 23) * SLOT;
             asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(r.t_max) : "memory");
         }
         const float half = r.sexp * 0.5f;                // N:111-116
@@ -561,12 +605,12 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const lmask sz = adv & LM_OF(tz <= tc_max);
         const float se = r.sexp;
         const float delta = LM_ON(push) ? half : -se;
+        const float ox = r.px, oy = r.py, oz = r.pz;
         const float qx = r.px + (LM_ON((push & cx) | sx) ? delta : 0.0f);
         const float qy = r.py + (LM_ON((push & cy) | sy) ? delta : 0.0f);
         const float qz = r.pz + (LM_ON((push & cz) | sz) ? delta : 0.0f);
         const int step = lanes_to_idx(sx, sy, sz);       // 0 outside ADVANCE lanes
         const lmask pop = LM_OF((step & ~idx) != 0);     // N:130-131: (idx ^ step) & step
-        const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
         const int cidx = lanes_to_idx(cx, cy, cz);
         idx = LM_ON(push) ? cidx : (idx ^ step);
         if (LM_ON(push)) {
@@ -577,6 +621,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         }
         r.t_min = LM_ON(adv) ? tc_max : r.t_min;
         cached &= ~(push | pop);
+        if (PF) pf = push;
         r.px = qx; r.py = qy; r.pz = qz;
         lmask out = 0;
         if (pop != 0) {                                  // N:134-154
@@ -584,13 +629,28 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             // bookkeeping and copies of values live on both sides); the popping
             // lanes take the results.  Other lanes read an in-range slot.
             if (DIAG) diag->pop_trips += 1;
-            const uint32_t dx = LM_ON(sx) ? (__float_as_uint(qx) ^ __float_as_uint(qx + se)) : 0u;
-            const uint32_t dy = LM_ON(sy) ? (__float_as_uint(qy) ^ __float_as_uint(qy + se)) : 0u;
-            const uint32_t dz = LM_ON(sz) ? (__float_as_uint(qz) ^ __float_as_uint(qz + se)) : 0u;
-            const uint32_t fd = __float_as_uint((float)(dx | dy | dz));
-            const int scale = (int)(fd >> 23) - 127;
-            const int slot = min(max(scale - scale_lo, 0), slots);
-            const uint2 e = stk[slot * STRIDE];          // slot == slots only when leaving the root
+            uint32_t diff;
+            if (V2) {
+                // stepped axis: q + scale_exp2 == o exactly (multiples of scale_exp2 in [0.5, 2));
+                // unstepped axis: q == o, xor 0 -- N:135-137 without masks or re-adds
+                diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) | (__float_as_uint(oy) ^ __float_as_uint(qy)) |
+                       (__float_as_uint(oz) ^ __float_as_uint(qz));
+            } else {
+                const uint32_t dx = LM_ON(sx) ? (__float_as_uint(qx) ^ __float_as_uint(qx + se)) : 0u;
+                const uint32_t dy = LM_ON(sy) ? (__float_as_uint(qy) ^ __float_as_uint(qy + se)) : 0u;
+                const uint32_t dz = LM_ON(sz) ? (__float_as_uint(qz) ^ __float_as_uint(qz + se)) : 0u;
+                diff = dx | dy | dz;
+            }
+            const uint32_t fd = __float_as_uint((float)diff);
+            const uint32_t ef = V2 ? __builtin_amdgcn_ubfe(fd, 23, 8) : fd >> 23;   // scale + 127
+            const int scale = (int)ef - 127;
+            uint2 e;
+            if (V2) {
+                e = stk_pop[min(ef, e_max) * STRIDE];   // e_max: leaving the root
+            } else {
+                const int slot = min(max(scale - scale_lo, 0), slots);
+                e = stk[slot * STRIDE];                  // slot == slots only when leaving the root
+            }
             uint32_t pa = e.x, tm = e.y;
             if (MODE == 0) {                             // int2 <- float2((int)parent, asint(t_max))
                 if (GUARD) pa = (uint32_t)cvt_i32((float)(int32_t)pa);
@@ -601,7 +661,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
             const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
             const bool pl = LM_ON(pop);
-            r.sexp = pl ? __uint_as_float((fd & 0x7F800000u) - (23u << 23)) : r.sexp;
+            r.sexp = pl ? __uint_as_float(V2 ? (ef << 23) - (23u << 23) : (fd & 0x7F800000u) - (23u << 23)) : r.sexp;
             r.parent = pl ? pa : r.parent;
             r.t_max = pl ? __uint_as_float(tm) : r.t_max;
             r.px = pl ? __uint_as_float(__float_as_uint(qx) & keep) : r.px;
@@ -620,6 +680,126 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     r.trips = it;
     if (LM_ON(capped)) r.flags |= 2u;
     if (LM_ON(ovf)) r.flags |= 4u;
+}
+
+// Latency-hiding lean loop (SVO_FLAT=8; one wave64 per workgroup, unguarded
+// pools only).  The heaviest 8x8 tiles bound the launch (a lone wave of the
+// heaviest tile row takes ~70 % of the full frame's time), and a lone wave
+// spends most of a trip waiting for its node fetch.  So no trip waits for a
+// demand fetch:
+//   * each stack entry also holds the descriptor of its node (16 bytes:
+//     parent, t_max, node word, first child), so a POP restores the node
+//     without touching HBM (N:60-62 would re-fetch it: same value);
+//   * the child a PUSH would enter (valid, non-leaf) is fetched speculatively
+//     as soon as its index is known, early in the trip, and consumed at the
+//     top of the next trip by the lanes that pushed;
+//   * never-written entries read as {root, 0, root descriptor} instead of
+//     zero (the HLSL reads parent 0 / t_max 0 and then fetches the root).
+// Other lanes/trips behave exactly as trace_lean<..., V2>.
+__device__ __forceinline__ void lds_write_b128(uint32_t addr, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = { a, b, c, d };
+    asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(v) : "memory");
+}
+
+template <int MODE>
+__device__ __forceinline__ void trace_pf2(const LaunchParams &p, FRay &r, uint4 *__restrict__ stk) {
+    constexpr int STRIDE = 64;
+    constexpr uint32_t SLOT = STRIDE * sizeof(uint4);   // 1024 B per slot: (bits(sexp) >> 13) addresses it
+    const int slots = p.slots;
+    const int scale_lo = S_MAX - slots;
+    const uint2 root = p.nodes[0];
+    for (int s = 0; s <= slots; ++s) stk[s * STRIDE] = make_uint4(0u, 0u, root.x, root.y);
+    lmask act = LM_OF(true);
+    int idx = r.idx;
+    const int oct = r.octant_mask | 16;    // c ^ (oct | 16) == (c ^ oct) + 16
+    const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4 *)stk;
+    const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
+    const uint4 *stk_pop = stk - (127 + scale_lo) * STRIDE;    // indexed by e = scale + 127
+    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots);
+    uint32_t cd = root.x, first = root.y;
+    uint2 spec = make_uint2(0u, 0u);
+    asm volatile("" : "+v"(spec.x), "+v"(spec.y), "+v"(r.parent), "+v"(cd), "+v"(first));
+    lmask took = 0;        // lanes that pushed last trip: their node is in `spec`
+    int it = 0;
+    while (act != 0 && it < MAX_ITERS) {
+        asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
+        if (LM_ON(took)) { cd = spec.x; first = spec.y; }
+        const float tx = r.px * r.cx - r.bx;             // N:67-70
+        const float ty = r.py * r.cy - r.by;
+        const float tz = r.pz * r.cz - r.bz;
+        const uint32_t cm = cd << (idx ^ oct);           // valid bit -> bit 31, non-leaf bit -> bit 23
+        const uint32_t child = first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
+        const lmask cand = act & LM_OF((cm & 0x80800000u) == 0x80800000u);
+        if (LM_ON(cand)) spec = p.nodes[child];          // speculative: consumed next trip if pushed
+        const float tc_max = fminf(fminf(tx, ty), tz);
+        const float tv_max = vmin(r.t_max, tc_max);
+        const lmask descend = act & LM_OF((int32_t)cm < 0) & LM_OF(r.t_min <= tv_max);
+        const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
+        const lmask hit = descend & leaf;                // N:93-94
+        const lmask push = descend & ~leaf;
+        const lmask store = push & LM_OF(tc_max < r.h);
+        const lmask adv = act & ~descend;
+        if (LM_ON(store))                                // N:97-98 (raw; round trip on POP)
+            lds_write_b128(push_base + (__float_as_uint(r.sexp) >> 13), r.parent, __float_as_uint(r.t_max), cd, first);
+        const float half = r.sexp * 0.5f;                // N:111-116
+        const lmask cx = LM_OF(half * r.cx + tx > r.t_min);
+        const lmask cy = LM_OF(half * r.cy + ty > r.t_min);
+        const lmask cz = LM_OF(half * r.cz + tz > r.t_min);
+        const lmask sx = adv & LM_OF(tx <= tc_max);      // N:122-125
+        const lmask sy = adv & LM_OF(ty <= tc_max);
+        const lmask sz = adv & LM_OF(tz <= tc_max);
+        const float se = r.sexp;
+        const float delta = LM_ON(push) ? half : -se;
+        const float ox = r.px, oy = r.py, oz = r.pz;
+        const float qx = ox + (LM_ON((push & cx) | sx) ? delta : 0.0f);
+        const float qy = oy + (LM_ON((push & cy) | sy) ? delta : 0.0f);
+        const float qz = oz + (LM_ON((push & cz) | sz) ? delta : 0.0f);
+        const int step = lanes_to_idx(sx, sy, sz);
+        const lmask pop = LM_OF((step & ~idx) != 0);     // N:130-131
+        const int cidx = lanes_to_idx(cx, cy, cz);
+        idx = LM_ON(push) ? cidx : (idx ^ step);
+        if (LM_ON(push)) {
+            r.parent = child;
+            r.h = tc_max;
+            r.t_max = tv_max;
+            r.sexp = half;
+        }
+        r.t_min = LM_ON(adv) ? tc_max : r.t_min;
+        took = push;
+        r.px = qx; r.py = qy; r.pz = qz;
+        lmask out = 0;
+        if (pop != 0) {                                  // N:134-154
+            const uint32_t diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) |
+                                  (__float_as_uint(oy) ^ __float_as_uint(qy)) |
+                                  (__float_as_uint(oz) ^ __float_as_uint(qz));
+            const uint32_t ef = __float_as_uint((float)diff) >> 23;   // scale + 127
+            const int scale = (int)ef - 127;
+            const uint4 e = stk_pop[min(ef, e_max) * STRIDE];         // e_max: leaving the root
+            uint32_t tm = e.y;
+            if (MODE == 0) tm = (uint32_t)cvt_i32((float)(int32_t)tm);   // asint(t_max) through float (N:98)
+            const uint32_t keep = 0xFFFFFFFFu << scale;
+            const uint32_t bx_ = __builtin_amdgcn_ubfe(__float_as_uint(qx), scale, 1);
+            const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
+            const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
+            const bool pl = LM_ON(pop);
+            r.sexp = pl ? __uint_as_float((ef << 23) - (23u << 23)) : r.sexp;
+            r.parent = pl ? e.x : r.parent;
+            r.t_max = pl ? __uint_as_float(tm) : r.t_max;
+            cd = pl ? e.z : cd;
+            first = pl ? e.w : first;
+            r.px = pl ? __uint_as_float(__float_as_uint(qx) & keep) : r.px;
+            r.py = pl ? __uint_as_float(__float_as_uint(qy) & keep) : r.py;
+            r.pz = pl ? __uint_as_float(__float_as_uint(qz) & keep) : r.pz;
+            r.h = pl ? 0.0f : r.h;
+            idx = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) : idx;
+            out = pop & LM_OF(ef >= (uint32_t)(127 + S_MAX));
+        }
+        act &= ~(hit | out);
+    }
+    r.idx = idx;
+    r.trips = it;
+    if (LM_ON(act)) r.flags |= 2u;
 }
 
 // N:158-186 hit decode; R:93-127 Shade; R:167 store
@@ -697,13 +877,13 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int t = (STEP == 3 && BS == 64 && p.tile_order) ? (int)p.tile_order[blockIdx.x]
+    const int t = (STEP >= 3 && BS == 64 && p.tile_order) ? (int)p.tile_order[blockIdx.x]
                                                          : tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
     const int bx = t % blocks_x, by = t / blocks_x;
     const int x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
     const int lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
     if (x >= p.width || lr >= p.local_rows) return;
-    if (STEP == 3 && BS == 64 && p.tile_order && p.prio) {
+    if (STEP >= 3 && BS == 64 && p.tile_order && p.prio) {
         // issue priority by the previous launch's cost class: the heaviest tiles
         // bound the launch, so their waves win issue arbitration on a busy SIMD
         const uint32_t b = blockIdx.x, n = gridDim.x;
@@ -715,7 +895,7 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     init_ray(p, x, global_row(p, lr), r);
     const int scale_lo = S_MAX - p.slots;
     uint2 *stk = stk_base + tid;
-    if (STEP == 3 && !COUNT) {
+    if (STEP >= 3 && !COUNT) {
         uint32_t t0 = 0;
         if (p.wave_log) t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
         FRay f;
@@ -725,8 +905,9 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
             if (p.guard) trace_lean<MODE, BS, true, true>(p, f, stk, &dg);
             else trace_lean<MODE, BS, false, true>(p, f, stk, &dg);
         }
-        else if (p.guard) trace_lean<MODE, BS, true>(p, f, stk);
-        else trace_lean<MODE, BS, false>(p, f, stk);
+        else if (p.guard) trace_lean<MODE, BS, true, false, STEP >= 4, STEP == 5, STEP == 6 || STEP == 7 ? STEP - 5 : 0>(p, f, stk);
+        else if (STEP == 8 && BS == 64) trace_pf2<MODE>(p, f, reinterpret_cast<uint4 *>(stk_base) + tid);
+        else trace_lean<MODE, BS, false, false, STEP >= 4, STEP == 5, STEP == 6 || STEP == 7 ? STEP - 5 : 0>(p, f, stk);
         from_fray(f, r);
         if (BS == 64 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every lane
         if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
@@ -744,7 +925,7 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
         r.nd = p.nodes[0];
         while (!step_pf<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
         }
-    } else if (STEP == 1 || STEP == 3) {
+    } else if (STEP == 1 || STEP >= 3) {
         while (!step_flat<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
         }
     } else {
@@ -880,7 +1061,22 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
         if (p.block == 64) {
             const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
             const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
-            if (p.flat == 3)
+            if (p.flat == 5)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 5, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                                   lds64, stream, p, bx, p.xcd_remap);
+            else if (p.flat == 8)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 8, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                                   2 * lds64, stream, p, bx, p.xcd_remap);
+            else if (p.flat == 6)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 6, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                                   lds64, stream, p, bx, p.xcd_remap);
+            else if (p.flat == 7)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 7, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                                   lds64, stream, p, bx, p.xcd_remap);
+            else if (p.flat == 4)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                                   lds64, stream, p, bx, p.xcd_remap);
+            else if (p.flat == 3)
                 hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 64>), dim3((unsigned)(bx * by)), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat == 2)

@@ -259,7 +259,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.tile_order = nullptr;
     p.tile_cost = nullptr;
     p.prio = ctx->prio;
-    const bool ordered = ctx->tile_order && ctx->kernel == 0 && ctx->flat == 3 && ctx->block == 64 && !p.fetches;
+    const bool ordered = ctx->tile_order && ctx->kernel == 0 && ctx->flat >= 3 && ctx->block == 64 && !p.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
     long long key = -1;
     if (ordered) {
@@ -374,7 +374,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "persistent") == 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
     if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(3, std::atoi(k)));
+    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(8, std::atoi(k)));
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));

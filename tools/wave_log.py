@@ -94,11 +94,13 @@ def main():
     ft = log[:, 6].astype(np.float64)
     pt = log[:, 7].astype(np.float64)
     heavy = trips >= np.percentile(trips, 99)
+    push_only = log[:, 5].astype(np.int64) & 0xFFFF
+    adv_only = log[:, 5].astype(np.int64) >> 16
     for name, m in (("all", np.ones(len(trips), bool)), ("top 1% trips", heavy)):
         tr = trips[m].sum()
-        print(f"{name}: cycles/trip {loop_c[m].sum() / tr:.0f}, fetch-wait cycles/trip {fetch_c[m].sum() / tr:.0f}"
-              f" (per fetching trip {fetch_c[m].sum() / max(ft[m].sum(), 1):.0f}), fetching trips {ft[m].sum() / tr:.2f},"
-              f" popping trips {pt[m].sum() / tr:.2f}")
+        print(f"{name}: cycles/trip {loop_c[m].sum() / tr:.0f}, fetching trips {ft[m].sum() / tr:.2f},"
+              f" popping trips {pt[m].sum() / tr:.2f}, push-only trips {push_only[m].sum() / tr:.2f},"
+              f" advance-only trips {adv_only[m].sum() / tr:.2f}")
     hw = log[:, 2]
     xcc = log[:, 3] & 0xFF
     print("waves per XCC:", np.bincount(xcc, minlength=8)[:8])
