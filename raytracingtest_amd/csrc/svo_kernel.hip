@@ -478,6 +478,7 @@ struct FRay {
     uint32_t parent, cd16, first, flags;
     int idx, octant_mask;   // only at entry / exit
     int trips;              // wave-uniform loop trip count (diagnostics)
+    int lane_trips;         // this ray's iteration count (COSTREC launches)
 };
 
 __device__ __forceinline__ void to_fray(const Ray &r, FRay &f) {
@@ -503,7 +504,8 @@ struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
     uint32_t fetch_trips = 0, pop_trips = 0;
 };
 
-template <int MODE, int STRIDE, bool GUARD, bool DIAG = false, bool V2 = false, bool PF = false, int PAD = 0>
+template <int MODE, int STRIDE, bool GUARD, bool DIAG = false, bool V2 = false, bool PF = false, int PAD = 0,
+          bool COSTREC = false>
 __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk,
                                            LeanDiag *diag = nullptr) {
     // GUARD = false (host-proven, svo_rt.hip recompute_depth): one tree of known
@@ -517,6 +519,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     int idx = r.idx;                       // child index bits (per lane, VGPR)
     const int oct = V2 ? (r.octant_mask | 16) : r.octant_mask;   // V2: c ^ (oct | 16) == (c ^ oct) + 16
     lmask cached = 0, capped = 0, ovf = 0;
+    int lane_it = 0;       // COSTREC: trips until this lane's ray finished
     lmask pf = 0;          // PF: lanes whose next node is already in `spec`
     uint2 spec = make_uint2(0u, 0u);
     if (PF) asm volatile("" : "+v"(spec.x), "+v"(spec.y), "+v"(r.parent));   // per-lane values (LLVM uniformity)
@@ -536,8 +539,8 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
         const lmask need = act & ~cached;
         if (PF) {
-            // lanes that pushed last trip find their node in `spec` (loaded one trip early);
-            // the others (after a POP, or the root) fetch on demand
+            // lanes that pushed or popped last trip find their node in `spec` (loaded
+            // during that trip); only the root's first fetch is on demand
             if (LM_ON(need & ~pf)) spec = p.nodes[r.parent];
             if (LM_ON(need)) {
                 uint32_t x = spec.x;
@@ -670,10 +673,19 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             r.h = pl ? 0.0f : r.h;
             idx = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) : idx;
             out = pop & LM_OF(scale >= S_MAX);
+            if (PF) {
+                // the popped parent's descriptor (N:60-62 re-fetches it next trip): issued now,
+                // so its latency overlaps the rest of this trip
+                const lmask pnext = pop & ~out;
+                if (LM_ON(pnext)) spec = p.nodes[pa];
+                pf |= pnext;
+            }
         }
         ovf |= of;
+        if (COSTREC) lane_it = LM_ON(act & (hit | of | out)) ? it : lane_it;   // this ray's iteration count
         act &= ~(hit | of | out);
     }
+    if (COSTREC) r.lane_trips = LM_ON(act) ? it : lane_it;
     capped = act;                          // still tracing after MAX_ITERS trips
     if (DIAG) diag->loop_cycles = __builtin_amdgcn_s_memtime() - tl0;
     r.idx = idx;
@@ -877,16 +889,37 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int t = (STEP >= 3 && BS == 64 && p.tile_order) ? (int)p.tile_order[blockIdx.x]
-                                                         : tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
-    const int bx = t % blocks_x, by = t / blocks_x;
-    const int x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
-    const int lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
+    int t;
+    if (STEP >= 3 && BS == 64 && p.tile_order) {
+        // split launch: the heavy kernel takes order positions [0, n_heavy), the light one the rest
+        if (p.part != 0) {
+            const uint32_t n_heavy = min(p.tile_order[p.n_tiles + p.heavy_classes - 1], (uint32_t)p.heavy_cap);
+            if (p.part == 1 ? blockIdx.x >= n_heavy : blockIdx.x < n_heavy) return;
+        }
+        t = (int)p.tile_order[blockIdx.x];
+    } else {
+        t = tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
+    }
+    int x, lr;
+    if (STEP >= 3 && BS == 64 && p.sorted) {
+        // cost-sorted lanes: t is a group = 64 rays of one 16x16 block, 4 groups per block;
+        // lane_perm lists the block's pixels by the previous cost map, heaviest first
+        // (null: group k = the block's k-th 8x8 quadrant)
+        const int blk = t >> 2, k = t & 3;
+        const int off = p.lane_perm ? (int)p.lane_perm[(size_t)blk * 256 + k * 64 + lane]
+                                    : ((k >> 1) * 8 + (lane >> 3)) * 16 + (k & 1) * 8 + (lane & 7);
+        x = (blk % p.nbx16) * 16 + (off & 15);
+        lr = (blk / p.nbx16) * 16 + (off >> 4);
+    } else {
+        const int bx = t % blocks_x, by = t / blocks_x;
+        x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
+        lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
+    }
     if (x >= p.width || lr >= p.local_rows) return;
     if (STEP >= 3 && BS == 64 && p.tile_order && p.prio) {
         // issue priority by the previous launch's cost class: the heaviest tiles
         // bound the launch, so their waves win issue arbitration on a busy SIMD
-        const uint32_t b = blockIdx.x, n = gridDim.x;
+        const uint32_t b = blockIdx.x, n = (uint32_t)p.n_tiles;
         if (b < p.tile_order[n]) __builtin_amdgcn_s_setprio(3);
         else if (b < p.tile_order[n + 1]) __builtin_amdgcn_s_setprio(2);
         else if (b < p.tile_order[n + 2]) __builtin_amdgcn_s_setprio(1);
@@ -905,11 +938,17 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
             if (p.guard) trace_lean<MODE, BS, true, true>(p, f, stk, &dg);
             else trace_lean<MODE, BS, false, true>(p, f, stk, &dg);
         }
+        else if (STEP == 4 && BS == 64 && p.ray_cost) {   // cost-map launch (sorted lanes)
+            if (p.guard) trace_lean<MODE, BS, true, false, true, false, 0, true>(p, f, stk);
+            else trace_lean<MODE, BS, false, false, true, false, 0, true>(p, f, stk);
+        }
         else if (p.guard) trace_lean<MODE, BS, true, false, STEP >= 4, STEP == 5, STEP == 6 || STEP == 7 ? STEP - 5 : 0>(p, f, stk);
         else if (STEP == 8 && BS == 64) trace_pf2<MODE>(p, f, reinterpret_cast<uint4 *>(stk_base) + tid);
         else trace_lean<MODE, BS, false, false, STEP >= 4, STEP == 5, STEP == 6 || STEP == 7 ? STEP - 5 : 0>(p, f, stk);
         from_fray(f, r);
         if (BS == 64 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every lane
+        if (STEP == 4 && BS == 64 && p.ray_cost && !p.wave_log)
+            p.ray_cost[(size_t)lr * (size_t)p.width + (size_t)x] = (uint8_t)min(f.lane_trips, 255);
         if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
             uint32_t *w = p.wave_log + 8 * ((size_t)blockIdx.x * (BS / 64) + wave);
             w[0] = t0;
@@ -1059,34 +1098,36 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
             return hipGetLastError();
         }
         if (p.block == 64) {
-            const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
+            const int bx = (p.width + 7) / 8;
+            const int by = (p.local_rows + 7) / 8;
+            const unsigned grid64 = p.sorted ? (unsigned)p.n_tiles : (unsigned)(bx * by);   // sorted: one block per group
             const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
             if (p.flat == 5)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 5, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 5, 64>), dim3(grid64), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat == 8)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 8, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 8, 64>), dim3(grid64), dim3(64),
                                    2 * lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat == 6)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 6, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 6, 64>), dim3(grid64), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat == 7)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 7, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 7, 64>), dim3(grid64), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat == 4)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64>), dim3(grid64), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat == 3)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 64>), dim3(grid64), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat == 2)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 2, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 2, 64>), dim3(grid64), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 64>), dim3(grid64), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             else
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 64>), dim3((unsigned)(bx * by)), dim3(64),
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 64>), dim3(grid64), dim3(64),
                                    lds64, stream, p, bx, p.xcd_remap);
             return hipGetLastError();
         }
@@ -1222,6 +1263,63 @@ hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------- lane sort
+// Cost-sorted lanes (SVO_SORT): per 16x16 block, the pixels by descending
+// recorded ray cost (iterations, u8) -- a counting sort in LDS, one wave per
+// block -- so each group of 64 consecutive pixels (one wave) holds rays of
+// similar cost, and each group's cost = its first (largest) entry for the
+// heaviest-first group order.  Pixels outside the frame sort last (cost 0);
+// the render kernel drops them.  Placement only: results never depend on it.
+__global__ __launch_bounds__(64) void sort_lanes_kernel(const uint8_t *__restrict__ ray_cost, int width, int rows,
+                                                        int nbx16, uint8_t *__restrict__ perm,
+                                                        uint16_t *__restrict__ group_cost) {
+    __shared__ uint32_t hist[256];
+    const int lane = threadIdx.x;
+    const int blk = blockIdx.x;
+    const int x0 = (blk % nbx16) * 16, y0 = (blk / nbx16) * 16;
+    for (int i = lane; i < 256; i += 64) hist[i] = 0;
+    __syncthreads();
+    uint32_t c[4], rank[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int off = j * 64 + lane;
+        const int x = x0 + (off & 15), y = y0 + (off >> 4);
+        c[j] = (x < width && y < rows) ? ray_cost[(size_t)y * width + x] : 0u;
+        rank[j] = atomicAdd(&hist[255 - c[j]], 1u);   // bucket 0 = most expensive
+    }
+    __syncthreads();
+    // exclusive scan of hist (4 buckets per lane)
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = hist[lane * 4 + j]; sum += v[j]; }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= d) incl += o;
+    }
+    uint32_t run = incl - sum;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { hist[lane * 4 + j] = run; run += v[j]; }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t pos = hist[255 - c[j]] + rank[j];
+        perm[(size_t)blk * 256 + pos] = (uint8_t)(j * 64 + lane);
+        if ((pos & 63) == 0) group_cost[blk * 4 + (pos >> 6)] = (uint16_t)c[j];
+    }
+}
+
+hipError_t launch_sort_lanes(const uint8_t *ray_cost, int width, int rows, uint8_t *perm, uint16_t *group_cost,
+                             hipStream_t stream) {
+    const int nbx16 = (width + 15) / 16, nby16 = (rows + 15) / 16;
+    if (nbx16 * nby16 == 0) return hipSuccess;
+    hipLaunchKernelGGL(sort_lanes_kernel, dim3((unsigned)(nbx16 * nby16)), dim3(64), 0, stream, ray_cost, width, rows,
+                       nbx16, perm, group_cost);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------- accumulation
 // AddShader.shader:44-47 + Blend SrcAlpha OneMinusSrcAlpha (:10), driven by
 // RaytracingMaster.cs:70-73: dst = src * a + dst * (1 - a), a = 1/(sample+1),
@@ -1259,6 +1357,37 @@ static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
     const size_t lds = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
     hipLaunchKernelGGL((shadow_tile_kernel<MODE, 64>), dim3((unsigned)(bx * by)), dim3(64), lds, stream, p, bx);
     return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_split_primary(const LaunchParams &p, hipStream_t stream, hipStream_t side, hipEvent_t fork,
+                                       hipEvent_t join) {
+    const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
+    LaunchParams ph = p, pl = p;
+    ph.part = 1;
+    pl.part = 2;
+    hipError_t e = hipEventRecord(fork, stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
+    if (e != hipSuccess) return e;
+    // heavy tiles first, on the side stream, so their waves are placed before the light launch fills the chip
+    hipLaunchKernelGGL((render_tile_kernel<MODE, false, 8, 64>), dim3((unsigned)p.heavy_cap), dim3(64), 2 * lds64, side,
+                       ph, (p.width + 7) / 8, 0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((render_tile_kernel<MODE, false, 4, 64>), dim3((unsigned)p.n_tiles), dim3(64), lds64, stream,
+                       pl, (p.width + 7) / 8, 0);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventRecord(join, side);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
+    return e;
+}
+
+hipError_t launch_render_split(const LaunchParams &p, int stack_mode, hipStream_t stream, hipStream_t side,
+                               hipEvent_t fork, hipEvent_t join) {
+    hipError_t e = stack_mode == 0 ? launch_split_primary<0>(p, stream, side, fork, join)
+                                   : launch_split_primary<1>(p, stream, side, fork, join);
+    if (e != hipSuccess || !(p.shadows && p.hits)) return e;
+    return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
 }
 
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel, uint32_t *counter,
