@@ -90,7 +90,6 @@ struct Ray {
     int idx, octant_mask, scale, iters;
     uint32_t flags;
     bool cached;
-    uint2 nd;                  // prefetched node (step_pf): issued when the parent changes
 };
 
 // R:151 uv, R:129-141 CreateCameraRay
@@ -334,97 +333,6 @@ __device__ __forceinline__ bool step_flat(const LaunchParams &p, Ray &r, uint2 *
     return false;
 }
 
-template <int MODE, bool COUNT, int STRIDE = BLOCK>
-__device__ __forceinline__ bool step_pf(const LaunchParams &p, Ray &r, uint2 *__restrict__ stk, int scale_lo,
-                                          int dummy) {
-    if (++r.iters > MAX_ITERS) { r.flags |= 2u; r.scale = S_MAX; return true; }
-    if (!r.cached) {                                       // N:60-62 (load issued one step early)
-        r.cd = r.nd.x;
-        r.first = r.nd.y;
-        r.cached = (r.nd.x | r.nd.y) != 0u;
-        if (COUNT) ++r.fetches;
-    }
-    const float tx_corner = r.px * r.tx_coef - r.tx_bias;
-    const float ty_corner = r.py * r.ty_coef - r.ty_bias;
-    const float tz_corner = r.pz * r.tz_coef - r.tz_bias;
-    const float tc_max = fminf(fminf(tx_corner, ty_corner), tz_corner);
-    const uint32_t child_masks = r.cd << (r.idx ^ r.octant_mask);
-    const float tv_max = fminf(r.t_max, tc_max);
-    const bool descend = (child_masks & 0x8000u) != 0u && r.t_min <= r.t_max && r.t_min <= tv_max;
-    const bool do_store = descend && tc_max < r.h;
-    const int s_push = r.scale - scale_lo;
-    if ((descend && (child_masks & 0x0080u) == 0u) || (do_store && s_push < 0)) {
-        if (!(descend && (child_masks & 0x0080u) == 0u)) { r.flags |= 4u; r.scale = S_MAX; }
-        return true;                                       // leaf hit (N:93-94) or stack overflow
-    }
-    const float half = r.scale_exp2 * 0.5f;
-    // PUSH candidate (N:83-117)
-    const float tx_center = half * r.tx_coef + tx_corner;
-    const float ty_center = half * r.ty_coef + ty_corner;
-    const float tz_center = half * r.tz_coef + tz_corner;
-    const int cidx = (tx_center > r.t_min ? 1 : 0) | (ty_center > r.t_min ? 2 : 0) | (tz_center > r.t_min ? 4 : 0);
-    // ADVANCE candidate (N:122-128)
-    const int step_mask = (tx_corner <= tc_max ? 1 : 0) | (ty_corner <= tc_max ? 2 : 0) | (tz_corner <= tc_max ? 4 : 0);
-    // stack store (N:97-98); lanes that do not push write their dummy slot
-    uint2 e;
-    if (MODE == 0) {   // int2 <- float2((int)parent, asint(t_max))
-        e.x = (uint32_t)cvt_i32((float)(int32_t)r.parent);
-        e.y = (uint32_t)cvt_i32((float)__float_as_int(r.t_max));
-    } else {
-        e.x = r.parent;
-        e.y = (uint32_t)__float_as_int(r.t_max);
-    }
-    stk[(do_store ? s_push : dummy) * STRIDE] = e;
-    r.written |= do_store ? (1u << s_push) : 0u;
-
-    const int mx = descend ? (cidx & 1) : (step_mask & 1);
-    const int my = descend ? (cidx & 2) : (step_mask & 2);
-    const int mz = descend ? (cidx & 4) : (step_mask & 4);
-    const float delta = descend ? half : -r.scale_exp2;
-    const float qx = r.px + (mx ? delta : 0.0f);
-    const float qy = r.py + (my ? delta : 0.0f);
-    const float qz = r.pz + (mz ? delta : 0.0f);
-    const int new_idx = descend ? cidx : (r.idx ^ step_mask);
-    const uint32_t child = r.first + (uint32_t)__builtin_popcount(child_masks & 0x7Fu);
-    r.h = descend ? tc_max : r.h;
-    r.parent = descend ? child : r.parent;
-    r.t_max = descend ? tv_max : r.t_max;
-    r.t_min = descend ? r.t_min : tc_max;
-    r.cached = descend ? false : r.cached;
-    if (!descend && (new_idx & step_mask) != 0) {
-        // POP (N:134-154)
-        uint32_t differing = 0;
-        if (step_mask & 1) differing |= (uint32_t)(__float_as_int(qx) ^ __float_as_int(qx + r.scale_exp2));
-        if (step_mask & 2) differing |= (uint32_t)(__float_as_int(qy) ^ __float_as_int(qy + r.scale_exp2));
-        if (step_mask & 4) differing |= (uint32_t)(__float_as_int(qz) ^ __float_as_int(qz + r.scale_exp2));
-        const int scale = (__float_as_int((float)differing) >> 23) - 127;
-        r.scale = scale;
-        r.scale_exp2 = __int_as_float((scale - S_MAX + 127) << 23);
-        const int s = scale - scale_lo;   // in [0, slots]; slots == dummy only when leaving the root
-        const uint2 se = stk[s * STRIDE];
-        const bool ok = (r.written >> s) & 1u;
-        r.parent = ok ? se.x : 0u;
-        r.t_max = __int_as_float(ok ? (int32_t)se.y : 0);
-        const int32_t shx = __float_as_int(qx) >> scale;
-        const int32_t shy = __float_as_int(qy) >> scale;
-        const int32_t shz = __float_as_int(qz) >> scale;
-        r.px = __int_as_float((int32_t)((uint32_t)shx << scale));
-        r.py = __int_as_float((int32_t)((uint32_t)shy << scale));
-        r.pz = __int_as_float((int32_t)((uint32_t)shz << scale));
-        r.idx = (shx & 1) | ((shy & 1) << 1) | ((shz & 1) << 2);
-        r.h = 0.0f;
-        r.cached = false;
-        if (r.scale < S_MAX) r.nd = p.nodes[r.parent];   // prefetch the popped parent
-        return r.scale >= S_MAX;
-    }
-    r.scale = descend ? r.scale - 1 : r.scale;
-    r.scale_exp2 = descend ? half : r.scale_exp2;
-    r.px = qx; r.py = qy; r.pz = qz;
-    r.idx = new_idx;
-    if (!r.cached) r.nd = p.nodes[r.parent];             // prefetch the child (or re-fetch an empty root)
-    return false;
-}
-
 // ------------------------------------------------------- lean traversal
 // The default tile-kernel loop.  Same results as step()/step_flat() (the GPU
 // parity tests compare them all against the oracle), restructured for VALU
@@ -478,7 +386,6 @@ struct FRay {
     uint32_t parent, cd16, first, flags;
     int idx, octant_mask;   // only at entry / exit
     int trips;              // wave-uniform loop trip count (diagnostics)
-    int lane_trips;         // this ray's iteration count (COSTREC launches)
 };
 
 __device__ __forceinline__ void to_fray(const Ray &r, FRay &f) {
@@ -504,8 +411,7 @@ struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
     uint32_t fetch_trips = 0, pop_trips = 0;
 };
 
-template <int MODE, int STRIDE, bool GUARD, bool DIAG = false, bool V2 = false, bool PF = false, int PAD = 0,
-          bool COSTREC = false>
+template <int MODE, int STRIDE, bool GUARD, bool DIAG = false, bool V2 = false>
 __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk,
                                            LeanDiag *diag = nullptr) {
     // GUARD = false (host-proven, svo_rt.hip recompute_depth): one tree of known
@@ -519,10 +425,6 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     int idx = r.idx;                       // child index bits (per lane, VGPR)
     const int oct = V2 ? (r.octant_mask | 16) : r.octant_mask;   // V2: c ^ (oct | 16) == (c ^ oct) + 16
     lmask cached = 0, capped = 0, ovf = 0;
-    int lane_it = 0;       // COSTREC: trips until this lane's ray finished
-    lmask pf = 0;          // PF: lanes whose next node is already in `spec`
-    uint2 spec = make_uint2(0u, 0u);
-    if (PF) asm volatile("" : "+v"(spec.x), "+v"(spec.y), "+v"(r.parent));   // per-lane values (LLVM uniformity)
     const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
     constexpr uint32_t SLOT = (uint32_t)(STRIDE * sizeof(uint2));
     constexpr int SLOT_SH = 23 - (STRIDE == 64 ? 9 : STRIDE == 128 ? 10 : 11);   // (bits >> 23) * SLOT
@@ -538,17 +440,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         // wave-uniform trip count kept in an SGPR (LLVM otherwise counts down in a VGPR)
         asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
         const lmask need = act & ~cached;
-        if (PF) {
-            // lanes that pushed or popped last trip find their node in `spec` (loaded
-            // during that trip); only the root's first fetch is on demand
-            if (LM_ON(need & ~pf)) spec = p.nodes[r.parent];
-            if (LM_ON(need)) {
-                uint32_t x = spec.x;
-                asm volatile("" : "+v"(x));
-                r.cd16 = x;
-                r.first = spec.y;
-            }
-        } else if (LM_ON(need)) {                        // N:60-62
+        if (LM_ON(need)) {                               // N:60-62
             const uint2 nd = p.nodes[r.parent];
             uint32_t x = nd.x;
             if (V2) asm volatile("" : "+v"(x));   // opaque VGPR value (works round an LLVM uniformity bug)
@@ -557,29 +449,12 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         }
         if (DIAG && need) diag->fetch_trips += 1;
         cached |= need;
-        if (PAD == 1) {   // experiment: 8 extra independent VALU per trip
-            uint32_t j0 = 0, j1 = 0;
-            asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\t"
-                         "v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1" : "+v"(j0), "+v"(j1));
-        }
-        if (PAD == 2) {   // experiment: 8 extra independent SALU per trip
-            uint32_t j0 = 0, j1 = 0;
-            asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\t"
-                         "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1" : "+s"(j0), "+s"(j1) : : "scc");
-        }
         const float tx = r.px * r.cx - r.bx;             // N:67-70
         const float ty = r.py * r.cy - r.by;
         const float tz = r.pz * r.cz - r.bz;
         const float tc_max = fminf(fminf(tx, ty), tz);
         const uint32_t cm = r.cd16 << (idx ^ oct);       // valid bit -> bit 31, leaf bit -> bit 23
         const float tv_max = vmin(r.t_max, tc_max);
-        const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
-        if (PF) {
-            // speculative fetch of the child a PUSH would enter (valid, non-leaf): a PUSH
-            // implies it, so next trip's descriptor is in flight during this trip's math
-            const lmask cand = act & LM_OF((int32_t)(cm & 0x80800000u) == (int32_t)0x80800000u);
-            if (LM_ON(cand)) spec = p.nodes[child];
-        }
         const lmask descend = act & LM_OF((int32_t)cm < 0) & LM_OF(r.t_min <= tv_max);
         const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
         const lmask hit = descend & leaf;                // N:93-94
@@ -614,6 +489,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const float qz = r.pz + (LM_ON((push & cz) | sz) ? delta : 0.0f);
         const int step = lanes_to_idx(sx, sy, sz);       // 0 outside ADVANCE lanes
         const lmask pop = LM_OF((step & ~idx) != 0);     // N:130-131: (idx ^ step) & step
+        const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
         const int cidx = lanes_to_idx(cx, cy, cz);
         idx = LM_ON(push) ? cidx : (idx ^ step);
         if (LM_ON(push)) {
@@ -624,7 +500,6 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         }
         r.t_min = LM_ON(adv) ? tc_max : r.t_min;
         cached &= ~(push | pop);
-        if (PF) pf = push;
         r.px = qx; r.py = qy; r.pz = qz;
         lmask out = 0;
         if (pop != 0) {                                  // N:134-154
@@ -673,145 +548,16 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             r.h = pl ? 0.0f : r.h;
             idx = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) : idx;
             out = pop & LM_OF(scale >= S_MAX);
-            if (PF) {
-                // the popped parent's descriptor (N:60-62 re-fetches it next trip): issued now,
-                // so its latency overlaps the rest of this trip
-                const lmask pnext = pop & ~out;
-                if (LM_ON(pnext)) spec = p.nodes[pa];
-                pf |= pnext;
-            }
         }
         ovf |= of;
-        if (COSTREC) lane_it = LM_ON(act & (hit | of | out)) ? it : lane_it;   // this ray's iteration count
         act &= ~(hit | of | out);
     }
-    if (COSTREC) r.lane_trips = LM_ON(act) ? it : lane_it;
     capped = act;                          // still tracing after MAX_ITERS trips
     if (DIAG) diag->loop_cycles = __builtin_amdgcn_s_memtime() - tl0;
     r.idx = idx;
     r.trips = it;
     if (LM_ON(capped)) r.flags |= 2u;
     if (LM_ON(ovf)) r.flags |= 4u;
-}
-
-// Latency-hiding lean loop (SVO_FLAT=8; one wave64 per workgroup, unguarded
-// pools only).  The heaviest 8x8 tiles bound the launch (a lone wave of the
-// heaviest tile row takes ~70 % of the full frame's time), and a lone wave
-// spends most of a trip waiting for its node fetch.  So no trip waits for a
-// demand fetch:
-//   * each stack entry also holds the descriptor of its node (16 bytes:
-//     parent, t_max, node word, first child), so a POP restores the node
-//     without touching HBM (N:60-62 would re-fetch it: same value);
-//   * the child a PUSH would enter (valid, non-leaf) is fetched speculatively
-//     as soon as its index is known, early in the trip, and consumed at the
-//     top of the next trip by the lanes that pushed;
-//   * never-written entries read as {root, 0, root descriptor} instead of
-//     zero (the HLSL reads parent 0 / t_max 0 and then fetches the root).
-// Other lanes/trips behave exactly as trace_lean<..., V2>.
-__device__ __forceinline__ void lds_write_b128(uint32_t addr, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = { a, b, c, d };
-    asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(v) : "memory");
-}
-
-template <int MODE>
-__device__ __forceinline__ void trace_pf2(const LaunchParams &p, FRay &r, uint4 *__restrict__ stk) {
-    constexpr int STRIDE = 64;
-    constexpr uint32_t SLOT = STRIDE * sizeof(uint4);   // 1024 B per slot: (bits(sexp) >> 13) addresses it
-    const int slots = p.slots;
-    const int scale_lo = S_MAX - slots;
-    const uint2 root = p.nodes[0];
-    for (int s = 0; s <= slots; ++s) stk[s * STRIDE] = make_uint4(0u, 0u, root.x, root.y);
-    lmask act = LM_OF(true);
-    int idx = r.idx;
-    const int oct = r.octant_mask | 16;    // c ^ (oct | 16) == (c ^ oct) + 16
-    const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4 *)stk;
-    const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
-    const uint4 *stk_pop = stk - (127 + scale_lo) * STRIDE;    // indexed by e = scale + 127
-    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots);
-    uint32_t cd = root.x, first = root.y;
-    uint2 spec = make_uint2(0u, 0u);
-    asm volatile("" : "+v"(spec.x), "+v"(spec.y), "+v"(r.parent), "+v"(cd), "+v"(first));
-    lmask took = 0;        // lanes that pushed last trip: their node is in `spec`
-    int it = 0;
-    while (act != 0 && it < MAX_ITERS) {
-        asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
-        if (LM_ON(took)) { cd = spec.x; first = spec.y; }
-        const float tx = r.px * r.cx - r.bx;             // N:67-70
-        const float ty = r.py * r.cy - r.by;
-        const float tz = r.pz * r.cz - r.bz;
-        const uint32_t cm = cd << (idx ^ oct);           // valid bit -> bit 31, non-leaf bit -> bit 23
-        const uint32_t child = first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
-        const lmask cand = act & LM_OF((cm & 0x80800000u) == 0x80800000u);
-        if (LM_ON(cand)) spec = p.nodes[child];          // speculative: consumed next trip if pushed
-        const float tc_max = fminf(fminf(tx, ty), tz);
-        const float tv_max = vmin(r.t_max, tc_max);
-        const lmask descend = act & LM_OF((int32_t)cm < 0) & LM_OF(r.t_min <= tv_max);
-        const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
-        const lmask hit = descend & leaf;                // N:93-94
-        const lmask push = descend & ~leaf;
-        const lmask store = push & LM_OF(tc_max < r.h);
-        const lmask adv = act & ~descend;
-        if (LM_ON(store))                                // N:97-98 (raw; round trip on POP)
-            lds_write_b128(push_base + (__float_as_uint(r.sexp) >> 13), r.parent, __float_as_uint(r.t_max), cd, first);
-        const float half = r.sexp * 0.5f;                // N:111-116
-        const lmask cx = LM_OF(half * r.cx + tx > r.t_min);
-        const lmask cy = LM_OF(half * r.cy + ty > r.t_min);
-        const lmask cz = LM_OF(half * r.cz + tz > r.t_min);
-        const lmask sx = adv & LM_OF(tx <= tc_max);      // N:122-125
-        const lmask sy = adv & LM_OF(ty <= tc_max);
-        const lmask sz = adv & LM_OF(tz <= tc_max);
-        const float se = r.sexp;
-        const float delta = LM_ON(push) ? half : -se;
-        const float ox = r.px, oy = r.py, oz = r.pz;
-        const float qx = ox + (LM_ON((push & cx) | sx) ? delta : 0.0f);
-        const float qy = oy + (LM_ON((push & cy) | sy) ? delta : 0.0f);
-        const float qz = oz + (LM_ON((push & cz) | sz) ? delta : 0.0f);
-        const int step = lanes_to_idx(sx, sy, sz);
-        const lmask pop = LM_OF((step & ~idx) != 0);     // N:130-131
-        const int cidx = lanes_to_idx(cx, cy, cz);
-        idx = LM_ON(push) ? cidx : (idx ^ step);
-        if (LM_ON(push)) {
-            r.parent = child;
-            r.h = tc_max;
-            r.t_max = tv_max;
-            r.sexp = half;
-        }
-        r.t_min = LM_ON(adv) ? tc_max : r.t_min;
-        took = push;
-        r.px = qx; r.py = qy; r.pz = qz;
-        lmask out = 0;
-        if (pop != 0) {                                  // N:134-154
-            const uint32_t diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) |
-                                  (__float_as_uint(oy) ^ __float_as_uint(qy)) |
-                                  (__float_as_uint(oz) ^ __float_as_uint(qz));
-            const uint32_t ef = __float_as_uint((float)diff) >> 23;   // scale + 127
-            const int scale = (int)ef - 127;
-            const uint4 e = stk_pop[min(ef, e_max) * STRIDE];         // e_max: leaving the root
-            uint32_t tm = e.y;
-            if (MODE == 0) tm = (uint32_t)cvt_i32((float)(int32_t)tm);   // asint(t_max) through float (N:98)
-            const uint32_t keep = 0xFFFFFFFFu << scale;
-            const uint32_t bx_ = __builtin_amdgcn_ubfe(__float_as_uint(qx), scale, 1);
-            const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
-            const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
-            const bool pl = LM_ON(pop);
-            r.sexp = pl ? __uint_as_float((ef << 23) - (23u << 23)) : r.sexp;
-            r.parent = pl ? e.x : r.parent;
-            r.t_max = pl ? __uint_as_float(tm) : r.t_max;
-            cd = pl ? e.z : cd;
-            first = pl ? e.w : first;
-            r.px = pl ? __uint_as_float(__float_as_uint(qx) & keep) : r.px;
-            r.py = pl ? __uint_as_float(__float_as_uint(qy) & keep) : r.py;
-            r.pz = pl ? __uint_as_float(__float_as_uint(qz) & keep) : r.pz;
-            r.h = pl ? 0.0f : r.h;
-            idx = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) : idx;
-            out = pop & LM_OF(ef >= (uint32_t)(127 + S_MAX));
-        }
-        act &= ~(hit | out);
-    }
-    r.idx = idx;
-    r.trips = it;
-    if (LM_ON(act)) r.flags |= 2u;
 }
 
 // N:158-186 hit decode; R:93-127 Shade; R:167 store
@@ -889,37 +635,16 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    int t;
-    if (STEP >= 3 && BS == 64 && p.tile_order) {
-        // split launch: the heavy kernel takes order positions [0, n_heavy), the light one the rest
-        if (p.part != 0) {
-            const uint32_t n_heavy = min(p.tile_order[p.n_tiles + p.heavy_classes - 1], (uint32_t)p.heavy_cap);
-            if (p.part == 1 ? blockIdx.x >= n_heavy : blockIdx.x < n_heavy) return;
-        }
-        t = (int)p.tile_order[blockIdx.x];
-    } else {
-        t = tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
-    }
-    int x, lr;
-    if (STEP >= 3 && BS == 64 && p.sorted) {
-        // cost-sorted lanes: t is a group = 64 rays of one 16x16 block, 4 groups per block;
-        // lane_perm lists the block's pixels by the previous cost map, heaviest first
-        // (null: group k = the block's k-th 8x8 quadrant)
-        const int blk = t >> 2, k = t & 3;
-        const int off = p.lane_perm ? (int)p.lane_perm[(size_t)blk * 256 + k * 64 + lane]
-                                    : ((k >> 1) * 8 + (lane >> 3)) * 16 + (k & 1) * 8 + (lane & 7);
-        x = (blk % p.nbx16) * 16 + (off & 15);
-        lr = (blk / p.nbx16) * 16 + (off >> 4);
-    } else {
-        const int bx = t % blocks_x, by = t / blocks_x;
-        x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
-        lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
-    }
+    const int t = (STEP >= 3 && BS == 64 && p.tile_order) ? (int)p.tile_order[blockIdx.x]
+                                                         : tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
+    const int bx = t % blocks_x, by = t / blocks_x;
+    const int x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
+    const int lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
     if (x >= p.width || lr >= p.local_rows) return;
     if (STEP >= 3 && BS == 64 && p.tile_order && p.prio) {
         // issue priority by the previous launch's cost class: the heaviest tiles
         // bound the launch, so their waves win issue arbitration on a busy SIMD
-        const uint32_t b = blockIdx.x, n = (uint32_t)p.n_tiles;
+        const uint32_t b = blockIdx.x, n = gridDim.x;
         if (b < p.tile_order[n]) __builtin_amdgcn_s_setprio(3);
         else if (b < p.tile_order[n + 1]) __builtin_amdgcn_s_setprio(2);
         else if (b < p.tile_order[n + 2]) __builtin_amdgcn_s_setprio(1);
@@ -938,17 +663,10 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
             if (p.guard) trace_lean<MODE, BS, true, true>(p, f, stk, &dg);
             else trace_lean<MODE, BS, false, true>(p, f, stk, &dg);
         }
-        else if (STEP == 4 && BS == 64 && p.ray_cost) {   // cost-map launch (sorted lanes)
-            if (p.guard) trace_lean<MODE, BS, true, false, true, false, 0, true>(p, f, stk);
-            else trace_lean<MODE, BS, false, false, true, false, 0, true>(p, f, stk);
-        }
-        else if (p.guard) trace_lean<MODE, BS, true, false, STEP >= 4, STEP == 5, STEP == 6 || STEP == 7 ? STEP - 5 : 0>(p, f, stk);
-        else if (STEP == 8 && BS == 64) trace_pf2<MODE>(p, f, reinterpret_cast<uint4 *>(stk_base) + tid);
-        else trace_lean<MODE, BS, false, false, STEP >= 4, STEP == 5, STEP == 6 || STEP == 7 ? STEP - 5 : 0>(p, f, stk);
+        else if (p.guard) trace_lean<MODE, BS, true, false, STEP == 4>(p, f, stk);
+        else trace_lean<MODE, BS, false, false, STEP == 4>(p, f, stk);
         from_fray(f, r);
         if (BS == 64 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every lane
-        if (STEP == 4 && BS == 64 && p.ray_cost && !p.wave_log)
-            p.ray_cost[(size_t)lr * (size_t)p.width + (size_t)x] = (uint8_t)min(f.lane_trips, 255);
         if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
             uint32_t *w = p.wave_log + 8 * ((size_t)blockIdx.x * (BS / 64) + wave);
             w[0] = t0;
@@ -959,10 +677,6 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
             w[5] = (uint32_t)dg.fetch_cycles;
             w[6] = dg.fetch_trips;
             w[7] = dg.pop_trips;
-        }
-    } else if (STEP == 2) {
-        r.nd = p.nodes[0];
-        while (!step_pf<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
         }
     } else if (STEP == 1 || STEP >= 3) {
         while (!step_flat<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
@@ -1098,37 +812,17 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
             return hipGetLastError();
         }
         if (p.block == 64) {
-            const int bx = (p.width + 7) / 8;
-            const int by = (p.local_rows + 7) / 8;
-            const unsigned grid64 = p.sorted ? (unsigned)p.n_tiles : (unsigned)(bx * by);   // sorted: one block per group
+            const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
             const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
-            if (p.flat == 5)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 5, 64>), dim3(grid64), dim3(64),
-                                   lds64, stream, p, bx, p.xcd_remap);
-            else if (p.flat == 8)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 8, 64>), dim3(grid64), dim3(64),
-                                   2 * lds64, stream, p, bx, p.xcd_remap);
-            else if (p.flat == 6)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 6, 64>), dim3(grid64), dim3(64),
-                                   lds64, stream, p, bx, p.xcd_remap);
-            else if (p.flat == 7)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 7, 64>), dim3(grid64), dim3(64),
-                                   lds64, stream, p, bx, p.xcd_remap);
-            else if (p.flat == 4)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64>), dim3(grid64), dim3(64),
-                                   lds64, stream, p, bx, p.xcd_remap);
+            const dim3 grid((unsigned)(bx * by)), block(64);
+            if (p.flat == 4)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat == 3)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 64>), dim3(grid64), dim3(64),
-                                   lds64, stream, p, bx, p.xcd_remap);
-            else if (p.flat == 2)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 2, 64>), dim3(grid64), dim3(64),
-                                   lds64, stream, p, bx, p.xcd_remap);
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 64>), dim3(grid64), dim3(64),
-                                   lds64, stream, p, bx, p.xcd_remap);
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
             else
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 64>), dim3(grid64), dim3(64),
-                                   lds64, stream, p, bx, p.xcd_remap);
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
             return hipGetLastError();
         }
         const int bx = (p.width + 15) / 16, by = (p.local_rows + 15) / 16;
@@ -1263,63 +957,6 @@ hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles
     return hipGetLastError();
 }
 
-// ---------------------------------------------------------- lane sort
-// Cost-sorted lanes (SVO_SORT): per 16x16 block, the pixels by descending
-// recorded ray cost (iterations, u8) -- a counting sort in LDS, one wave per
-// block -- so each group of 64 consecutive pixels (one wave) holds rays of
-// similar cost, and each group's cost = its first (largest) entry for the
-// heaviest-first group order.  Pixels outside the frame sort last (cost 0);
-// the render kernel drops them.  Placement only: results never depend on it.
-__global__ __launch_bounds__(64) void sort_lanes_kernel(const uint8_t *__restrict__ ray_cost, int width, int rows,
-                                                        int nbx16, uint8_t *__restrict__ perm,
-                                                        uint16_t *__restrict__ group_cost) {
-    __shared__ uint32_t hist[256];
-    const int lane = threadIdx.x;
-    const int blk = blockIdx.x;
-    const int x0 = (blk % nbx16) * 16, y0 = (blk / nbx16) * 16;
-    for (int i = lane; i < 256; i += 64) hist[i] = 0;
-    __syncthreads();
-    uint32_t c[4], rank[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int off = j * 64 + lane;
-        const int x = x0 + (off & 15), y = y0 + (off >> 4);
-        c[j] = (x < width && y < rows) ? ray_cost[(size_t)y * width + x] : 0u;
-        rank[j] = atomicAdd(&hist[255 - c[j]], 1u);   // bucket 0 = most expensive
-    }
-    __syncthreads();
-    // exclusive scan of hist (4 buckets per lane)
-    uint32_t v[4], sum = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { v[j] = hist[lane * 4 + j]; sum += v[j]; }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-        if (lane >= d) incl += o;
-    }
-    uint32_t run = incl - sum;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { hist[lane * 4 + j] = run; run += v[j]; }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t pos = hist[255 - c[j]] + rank[j];
-        perm[(size_t)blk * 256 + pos] = (uint8_t)(j * 64 + lane);
-        if ((pos & 63) == 0) group_cost[blk * 4 + (pos >> 6)] = (uint16_t)c[j];
-    }
-}
-
-hipError_t launch_sort_lanes(const uint8_t *ray_cost, int width, int rows, uint8_t *perm, uint16_t *group_cost,
-                             hipStream_t stream) {
-    const int nbx16 = (width + 15) / 16, nby16 = (rows + 15) / 16;
-    if (nbx16 * nby16 == 0) return hipSuccess;
-    hipLaunchKernelGGL(sort_lanes_kernel, dim3((unsigned)(nbx16 * nby16)), dim3(64), 0, stream, ray_cost, width, rows,
-                       nbx16, perm, group_cost);
-    return hipGetLastError();
-}
-
 // ---------------------------------------------------------- accumulation
 // AddShader.shader:44-47 + Blend SrcAlpha OneMinusSrcAlpha (:10), driven by
 // RaytracingMaster.cs:70-73: dst = src * a + dst * (1 - a), a = 1/(sample+1),
@@ -1357,37 +994,6 @@ static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
     const size_t lds = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
     hipLaunchKernelGGL((shadow_tile_kernel<MODE, 64>), dim3((unsigned)(bx * by)), dim3(64), lds, stream, p, bx);
     return hipGetLastError();
-}
-
-template <int MODE>
-static hipError_t launch_split_primary(const LaunchParams &p, hipStream_t stream, hipStream_t side, hipEvent_t fork,
-                                       hipEvent_t join) {
-    const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
-    LaunchParams ph = p, pl = p;
-    ph.part = 1;
-    pl.part = 2;
-    hipError_t e = hipEventRecord(fork, stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
-    if (e != hipSuccess) return e;
-    // heavy tiles first, on the side stream, so their waves are placed before the light launch fills the chip
-    hipLaunchKernelGGL((render_tile_kernel<MODE, false, 8, 64>), dim3((unsigned)p.heavy_cap), dim3(64), 2 * lds64, side,
-                       ph, (p.width + 7) / 8, 0);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((render_tile_kernel<MODE, false, 4, 64>), dim3((unsigned)p.n_tiles), dim3(64), lds64, stream,
-                       pl, (p.width + 7) / 8, 0);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipEventRecord(join, side);
-    if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
-    return e;
-}
-
-hipError_t launch_render_split(const LaunchParams &p, int stack_mode, hipStream_t stream, hipStream_t side,
-                               hipEvent_t fork, hipEvent_t join) {
-    hipError_t e = stack_mode == 0 ? launch_split_primary<0>(p, stream, side, fork, join)
-                                   : launch_split_primary<1>(p, stream, side, fork, join);
-    if (e != hipSuccess || !(p.shadows && p.hits)) return e;
-    return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
 }
 
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel, uint32_t *counter,

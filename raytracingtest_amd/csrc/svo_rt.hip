@@ -77,7 +77,7 @@ struct svo_ctx {
     int refill_at = 40;              // env SVO_REFILL
     int blocks_per_cu = 8;           // env SVO_BLOCKS_PER_CU
     int xcd_remap = 0;               // env SVO_XCD_REMAP (measured slower: XCD load imbalance)
-    int flat = 4;                    // env SVO_FLAT: 4 lean V2 (default), 3 lean, 1 flat, 0 branchy, 2/5/8 prefetch variants
+    int flat = 4;                    // env SVO_FLAT: 4 lean V2 (default), 3 lean, 1 flat, 0 branchy
     int block = 64;                  // env SVO_BLOCK (64 | 256)
     uint32_t options = 0;            // svo_set_options
     uint32_t *d_wave_log = nullptr;  // diagnostics: env SVO_WAVE_LOG=<file> (tile kernel, SVO_FLAT=3)
@@ -94,17 +94,6 @@ struct svo_ctx {
     size_t tile_cap = 0;
     long long order_key = -1;        // geometry d_tile_order was built for (-1: none)
     hipStream_t order_stream = nullptr;   // stream of the last order kernel (a launch elsewhere syncs it first)
-    // Split launch (env SVO_SPLIT=k, 0 = off): tiles of the k heaviest cost classes
-    // run the latency-hiding loop on a side stream beside the lean launch.
-    int split = 0;
-    int heavy_cap = 2048;            // env SVO_HEAVY_CAP
-    // Cost-sorted lanes (env SVO_SORT=1): rays regrouped per 16x16 block by the
-    // recorded per-ray cost map (refreshed with the tile order)
-    int sort = 0;
-    uint8_t *d_ray_cost = nullptr, *d_perm = nullptr;
-    size_t ray_cost_cap = 0, perm_cap = 0;
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool order_pending = false;
 };
 
@@ -271,18 +260,11 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.tile_cost = nullptr;
     p.prio = ctx->prio;
     const bool ordered = ctx->tile_order && ctx->kernel == 0 && ctx->flat >= 3 && ctx->block == 64 && !p.fetches;
-    // cost-sorted lanes: groups of 64 rays per 16x16 block instead of 8x8 tiles
-    const bool sorted = ordered && ctx->sort && ctx->flat == 4 && ctx->split == 0;
-    const int nbx16 = (width + 15) / 16, nby16 = (p.local_rows + 15) / 16;
-    const int n_tiles = sorted ? nbx16 * nby16 * 4 : ((width + 7) / 8) * ((p.local_rows + 7) / 8);
-    p.sorted = sorted ? 1 : 0;
-    p.nbx16 = nbx16;
-    p.lane_perm = nullptr;
-    p.ray_cost = nullptr;
+    const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
     long long key = -1;
     if (ordered) {
         key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^ ((long long)b.band_rows << 8) ^
-              (long long)b.band_rank ^ ((long long)b.band_count << 4) ^ ((long long)sorted << 62);
+              (long long)b.band_rank ^ ((long long)b.band_count << 4);
         if (ctx->tile_cap < (size_t)n_tiles) {
             HIP_TRY(hipDeviceSynchronize());   // a pending launch may still use the old buffers
             if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
@@ -340,49 +322,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         HIP_TRY(hipStreamSynchronize(ctx->order_stream));
         ctx->order_pending = false;
     }
-    // refresh: this launch's costs become the next launches' order (and lane sort)
-    const bool refresh = p.tile_cost && (ctx->order_key != key || ctx->order_launches++ % ctx->order_every == 0);
-    if (sorted) {
-        const size_t n_px = (size_t)width * (size_t)p.local_rows, n_perm = (size_t)nbx16 * nby16 * 256;
-        if (ctx->ray_cost_cap < n_px || ctx->perm_cap < n_perm) {
-            HIP_TRY(hipDeviceSynchronize());
-            if (ctx->d_ray_cost) hipFree(ctx->d_ray_cost);
-            if (ctx->d_perm) hipFree(ctx->d_perm);
-            ctx->d_ray_cost = ctx->d_perm = nullptr;
-            ctx->ray_cost_cap = ctx->perm_cap = 0;
-            ctx->order_key = -1;
-            HIP_TRY(hipMalloc(&ctx->d_ray_cost, n_px));
-            HIP_TRY(hipMalloc(&ctx->d_perm, n_perm));
-            ctx->ray_cost_cap = n_px;
-            ctx->perm_cap = n_perm;
-            p.tile_order = nullptr;   // the order (if any) predates these buffers
-        }
-        if (p.tile_order) p.lane_perm = ctx->d_perm;   // order and lane sort are refreshed together
-        if (refresh) p.ray_cost = ctx->d_ray_cost;
-    }
-    p.part = 0;
-    p.heavy_classes = std::max(1, ctx->split);
-    p.n_tiles = n_tiles;
-    p.heavy_cap = std::min(n_tiles, ctx->heavy_cap);
-    hipError_t e;
-    if (ctx->split > 0 && p.tile_order && !p.guard && !p.fetches && !p.wave_log && ctx->kernel == 0 &&
-        ctx->block == 64 && ctx->flat >= 3) {
-        if (!ctx->side) {
-            e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
-            if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("side stream: ") + hipGetErrorString(e));
-        }
-        e = svo::launch_render_split(p, stack_mode, s, ctx->side, ctx->ev_fork, ctx->ev_join);
-    } else {
-        e = svo::launch_render(p, stack_mode, s, ctx->kernel, ctx->d_counter, ctx->num_cus);
-    }
+    hipError_t e = svo::launch_render(p, stack_mode, s, ctx->kernel, ctx->d_counter, ctx->num_cus);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
+    const bool refresh = p.tile_cost && (ctx->order_key != key || ctx->order_launches++ % ctx->order_every == 0);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
-        if (sorted) {   // regroup each block's rays by cost; group costs replace the recorded ones
-            e = svo::launch_sort_lanes(ctx->d_ray_cost, width, p.local_rows, ctx->d_perm, ctx->d_tile_cost, s);
-            if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("lane sort launch: ") + hipGetErrorString(e));
-        }
         e = svo::launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, s);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         ctx->order_stream = s;
@@ -431,10 +374,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "persistent") == 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
     if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(8, std::atoi(k)));
-    if (const char *k = std::getenv("SVO_SPLIT")) ctx->split = std::max(0, std::min(4, std::atoi(k)));
-    if (const char *k = std::getenv("SVO_SORT")) ctx->sort = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_HEAVY_CAP")) ctx->heavy_cap = std::max(64, std::atoi(k));
+    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(4, std::atoi(k)));
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
@@ -601,11 +541,6 @@ int svo_destroy(svo_ctx *ctx) {
     if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
     if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
-    if (ctx->side) hipStreamDestroy(ctx->side);
-    if (ctx->d_ray_cost) hipFree(ctx->d_ray_cost);
-    if (ctx->d_perm) hipFree(ctx->d_perm);
-    if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
-    if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
     delete ctx;
     return SVO_OK;
 }

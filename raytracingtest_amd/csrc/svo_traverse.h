@@ -61,21 +61,6 @@ struct LaunchParams {
     uint16_t *tile_cost;
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
-    // Split launch (tile order present, unguarded pool): part 1 = the heaviest
-    // cost classes (< heavy_classes) through the latency-hiding loop on a side
-    // stream, part 2 = the other tiles through the lean loop, concurrently.
-    int part;                     // 0 = all tiles
-    int heavy_classes;            // 1..4
-    int n_tiles;                  // tiles of the frame (tile_order holds n_tiles + 4 entries)
-    int heavy_cap;                // grid of the heavy launch (at most this many heavy tiles)
-    // Cost-sorted lanes (64-thread lean kernel): a "tile" is a group of 64 rays of
-    // one 16x16 block (4 groups per block, nbx16 blocks per row); lane_perm
-    // (nullable) maps group lanes to block pixels; ray_cost (nullable) receives
-    // every ray's iteration count (u8) on cost-map launches.
-    int sorted;
-    int nbx16;
-    const uint8_t *lane_perm;
-    uint8_t *ray_cost;
 };
 
 // Order the tiles by recorded cost, most expensive class first, into `order`
@@ -84,9 +69,6 @@ struct LaunchParams {
 // identical results.  `cost` must hold order_cost_capacity(n_tiles) entries (the tail
 // beyond n_tiles is read, never used).
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream);
-// Per 16x16 block: pixels by descending ray cost -> perm (256 B per block), group costs (4 per block).
-hipError_t launch_sort_lanes(const uint8_t *ray_cost, int width, int rows, uint8_t *perm, uint16_t *group_cost,
-                             hipStream_t stream);
 size_t order_cost_capacity(int n_tiles);
 
 // Progressive accumulation (AddShader blend) of an RGBA32F sample frame.
@@ -95,11 +77,6 @@ hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32
 
 // kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).
 // counter: 16-byte device work counter (persistent kernel), num_cus: CU count.
-// Split primary pass (p.tile_order set, p.guard == 0, 64-thread tiles): heavy
-// classes on `side` (latency-hiding loop), the rest on `stream`; `stream`
-// waits for both.  Shadow rays, if enabled, follow on `stream`.
-hipError_t launch_render_split(const LaunchParams &p, int stack_mode, hipStream_t stream, hipStream_t side,
-                               hipEvent_t fork, hipEvent_t join);
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel,
                          uint32_t *counter, int num_cus);
 
