@@ -4,7 +4,7 @@
 Workload (config C3 of BASELINE.json): a depth-10 (1024^3)
 SVO built from the reference's Custom1 OpenSimplex terrain sampler
 (SampleFunctions.cs:40-47, seed 7) by the native NaiveCreator restatement,
-1920x1080 primary rays from the 'overview' camera, Main.unity intrinsics and
+1920x1080 primary rays from the 'flyover' camera, Main.unity intrinsics and
 light.  A step = one CSMain-equivalent pass: every pixel's camera ray,
 IntersectSVO, hit decode, Shade, RGBA + 24-byte hit record written to HBM.
 Inputs (node pool, camera) are resident before the timed region.
@@ -178,6 +178,28 @@ def main():
     else:
         kern_ms_max = kern_ms
 
+    # C3's '+1 shadow ray' (BASELINE.json configs[2]): the same frame with the
+    # shadow pass, timed separately on one GPU (reported beside, not as `value`)
+    shadow = None
+    if world == 1 and not args.shadows and args.svo != "menger" and args.steps > 0:
+        rm.SetShadowRays(True)
+        for _ in range(2):
+            step()
+        k = max(1, args.steps // 2)
+        se = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k)]
+        torch.cuda.synchronize(dev)
+        for a, b in se:
+            a.record(stream)
+            step()
+            b.record(stream)
+        torch.cuda.synchronize(dev)
+        rm.SetShadowRays(False)
+        sh_ms = float(np.mean([a.elapsed_time(b) for a, b in se]))
+        shadow = {"ms_per_frame": round(sh_ms, 4), "primary_rays": n_px, "shadow_rays": n_hit,
+                  "Mrays_per_s": round((n_px + n_hit) / (sh_ms * 1e-3) / 1e6, 2),
+                  "note": "primary pass + one shadow ray per primary hit (RaytraceCompute.compute:105-112), "
+                          "HIP events on the launch stream"}
+
     rays_per_step = n_px * world
     ms_per_step = elapsed / args.steps * 1e3
     mrays = rays_per_step / (ms_per_step * 1e-3) / 1e6
@@ -217,6 +239,7 @@ def main():
                          "bytes_formula": "8*F + 8*hits + 24*rays + 16*rays(rgba)" +
                                           (" (primary pass only; kernel_ms covers both passes)" if args.shadows else "")},
             "cpu_baseline": cpu,
+            "c3_plus_shadow_ray": shadow,
         }
         print(json.dumps(out), flush=True)
     rm.close()

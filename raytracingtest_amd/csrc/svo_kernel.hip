@@ -722,10 +722,12 @@ __global__ __launch_bounds__(BS) void shadow_tile_kernel(LaunchParams p, int blo
     }
     Ray r;
     setup_ray(so, sd, r);
-    const int scale_lo = S_MAX - p.slots;
     uint2 *stk = stk_base + tid;
-    while (!step_flat<MODE, false, BS>(p, r, stk, scale_lo, p.slots)) {
-    }
+    FRay f;   // the primary rays' lean loop (one wave of shadow rays per tile, parallel directions)
+    to_fray(r, f);
+    if (p.guard) trace_lean<MODE, BS, true, false, true>(p, f, stk);
+    else trace_lean<MODE, BS, false, false, true>(p, f, stk);
+    from_fray(f, r);
     if (r.scale < S_MAX) {   // occluded
         rec[0] = make_uint2(w01.x, w01.y | (8u << 16));
         if (p.rgba) p.rgba[out] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
