@@ -436,29 +436,37 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     int it = 0;
     uint64_t tl0 = 0;
     if (DIAG) tl0 = __builtin_amdgcn_s_memtime();
+    // per-lane values from here on (works round an LLVM uniformity-analysis bug that
+    // otherwise rejects the SGPR trip counter below: "illegal VGPR to SGPR copy")
+    if (V2) asm volatile("" : "+v"(r.parent), "+v"(r.cd16), "+v"(r.first));
     while (act != 0 && it < MAX_ITERS) {   // one exit: the cap is part of the loop test
         // wave-uniform trip count kept in an SGPR (LLVM otherwise counts down in a VGPR)
         asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
         const lmask need = act & ~cached;
         if (LM_ON(need)) {                               // N:60-62
             const uint2 nd = p.nodes[r.parent];
-            uint32_t x = nd.x;
-            if (V2) asm volatile("" : "+v"(x));   // opaque VGPR value (works round an LLVM uniformity bug)
-            r.cd16 = V2 ? x : x << 16;
+            r.cd16 = V2 ? nd.x : nd.x << 16;
             r.first = nd.y;
         }
         if (DIAG && need) diag->fetch_trips += 1;
         cached |= need;
+        // node-independent work first: it overlaps the fetch (waited for at the first use of cd16)
         const float tx = r.px * r.cx - r.bx;             // N:67-70
         const float ty = r.py * r.cy - r.by;
         const float tz = r.pz * r.cz - r.bz;
         const float tc_max = fminf(fminf(tx, ty), tz);
-        const uint32_t cm = r.cd16 << (idx ^ oct);       // valid bit -> bit 31, leaf bit -> bit 23
         const float tv_max = vmin(r.t_max, tc_max);
-        const lmask descend = act & LM_OF((int32_t)cm < 0) & LM_OF(r.t_min <= tv_max);
+        const float half = r.sexp * 0.5f;                // N:111-116
+        const lmask cx = LM_OF(half * r.cx + tx > r.t_min);
+        const lmask cy = LM_OF(half * r.cy + ty > r.t_min);
+        const lmask cz = LM_OF(half * r.cz + tz > r.t_min);
+        const lmask lx = LM_OF(tx <= tc_max), ly = LM_OF(ty <= tc_max), lz = LM_OF(tz <= tc_max);
+        const lmask in_span = LM_OF(r.t_min <= tv_max), below_h = LM_OF(tc_max < r.h);
+        const uint32_t cm = r.cd16 << (idx ^ oct);       // valid bit -> bit 31, leaf bit -> bit 23
+        const lmask descend = act & LM_OF((int32_t)cm < 0) & in_span;
         const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
         const lmask hit = descend & leaf;                // N:93-94
-        const lmask store = descend & ~leaf & LM_OF(tc_max < r.h);
+        const lmask store = descend & ~leaf & below_h;
         const lmask of = GUARD ? (store & LM_OF(r.sexp < sexp_lo)) : (lmask)0;
         const lmask push = descend & ~leaf & ~of;
         const lmask adv = act & ~descend;
@@ -474,13 +482,9 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
                                   : push_base + (__float_as_uint(r.sexp) >> 23) * SLOT;
             asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(r.t_max) : "memory");
         }
-        const float half = r.sexp * 0.5f;                // N:111-116
-        const lmask cx = LM_OF(half * r.cx + tx > r.t_min);
-        const lmask cy = LM_OF(half * r.cy + ty > r.t_min);
-        const lmask cz = LM_OF(half * r.cz + tz > r.t_min);
-        const lmask sx = adv & LM_OF(tx <= tc_max);      // N:122-125
-        const lmask sy = adv & LM_OF(ty <= tc_max);
-        const lmask sz = adv & LM_OF(tz <= tc_max);
+        const lmask sx = adv & lx;                       // N:122-125
+        const lmask sy = adv & ly;
+        const lmask sz = adv & lz;
         const float se = r.sexp;
         const float delta = LM_ON(push) ? half : -se;
         const float ox = r.px, oy = r.py, oz = r.pz;
