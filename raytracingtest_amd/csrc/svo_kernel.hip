@@ -546,9 +546,16 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             r.sexp = pl ? __uint_as_float(V2 ? (ef << 23) - (23u << 23) : (fd & 0x7F800000u) - (23u << 23)) : r.sexp;
             r.parent = pl ? pa : r.parent;
             r.t_max = pl ? __uint_as_float(tm) : r.t_max;
-            r.px = pl ? __uint_as_float(__float_as_uint(qx) & keep) : r.px;
-            r.py = pl ? __uint_as_float(__float_as_uint(qy) & keep) : r.py;
-            r.pz = pl ? __uint_as_float(__float_as_uint(qz) & keep) : r.pz;
+            if (V2) {   // one select of the mask, then in-place ands (r.p == q here)
+                const uint32_t k = pl ? keep : 0xFFFFFFFFu;
+                r.px = __uint_as_float(__float_as_uint(r.px) & k);
+                r.py = __uint_as_float(__float_as_uint(r.py) & k);
+                r.pz = __uint_as_float(__float_as_uint(r.pz) & k);
+            } else {
+                r.px = pl ? __uint_as_float(__float_as_uint(qx) & keep) : r.px;
+                r.py = pl ? __uint_as_float(__float_as_uint(qy) & keep) : r.py;
+                r.pz = pl ? __uint_as_float(__float_as_uint(qz) & keep) : r.pz;
+            }
             r.h = pl ? 0.0f : r.h;
             idx = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) : idx;
             out = pop & LM_OF(scale >= S_MAX);
