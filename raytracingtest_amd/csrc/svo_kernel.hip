@@ -633,6 +633,26 @@ __device__ __forceinline__ int global_row(const LaunchParams &p, int lr) {
 // band of screen tiles, so each XCD's private 4 MB L2 holds the SVO nodes of
 // its own screen band instead of every XCD caching the whole visible tree.
 // Placement only changes speed, never results.
+// remap 2: interleaved column strips.  Screen tile columns are grouped into
+// super-columns of G columns; super-column sc belongs to XCD sc % 8.  Blocks
+// b with b % 8 == x land on XCD x (MI355X_MICROARCH.md "Workgroup dispatch"),
+// so XCD x's L2 only caches the nodes seen through its own super-columns, and
+// every XCD samples the whole screen (sky and terrain alike).  Needs the tile
+// columns to be a multiple of 8 G (the host checks).  e = position within the
+// XCD's share, in super-column-major, then column-major order.
+__device__ __forceinline__ int strip_tile(int x, int e, int tiles_x, int tiles_y, int g) {
+    const int per_sc = g * tiles_y, nsc8 = tiles_x / (8 * g);
+    const int m = e / per_sc, within = e - m * per_sc;
+    const int sc = m * 8 + x;
+    const int cix = within / tiles_y;
+    return (within - cix * tiles_y) * tiles_x + sc * g + cix;
+    (void)nsc8;
+}
+
+__device__ __forceinline__ int tile_of_block_strips(int b, int nb, int tiles_x, int g) {
+    return strip_tile(b % 8, b / 8, tiles_x, nb / tiles_x, g);
+}
+
 __device__ __forceinline__ int tile_of_block(int b, int nb, bool remap) {
     if (!remap) return b;
     const int q = nb / 8, rem = nb % 8, xcd = b % 8;   // bijective for any nb
@@ -647,7 +667,8 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int t = (STEP >= 3 && BS == 64 && p.tile_order) ? (int)p.tile_order[blockIdx.x]
-                                                         : tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
+                        : remap == 2 && BS == 64 ? tile_of_block_strips((int)blockIdx.x, (int)gridDim.x, blocks_x, p.strip_w)
+                                                 : tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
     const int bx = t % blocks_x, by = t / blocks_x;
     const int x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
     const int lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
@@ -655,10 +676,12 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
     if (STEP >= 3 && BS == 64 && p.tile_order && p.prio) {
         // issue priority by the previous launch's cost class: the heaviest tiles
         // bound the launch, so their waves win issue arbitration on a busy SIMD
-        const uint32_t b = blockIdx.x, n = gridDim.x;
-        if (b < p.tile_order[n]) __builtin_amdgcn_s_setprio(3);
-        else if (b < p.tile_order[n + 1]) __builtin_amdgcn_s_setprio(2);
-        else if (b < p.tile_order[n + 2]) __builtin_amdgcn_s_setprio(1);
+        const uint32_t n = gridDim.x;
+        const uint32_t b = remap == 2 ? blockIdx.x / 8 : blockIdx.x;
+        const uint32_t *bound = remap == 2 ? p.tile_order + n + 4 + 4 * (blockIdx.x % 8) : p.tile_order + n;
+        if (b < bound[0]) __builtin_amdgcn_s_setprio(3);
+        else if (b < bound[1]) __builtin_amdgcn_s_setprio(2);
+        else if (b < bound[2]) __builtin_amdgcn_s_setprio(1);
     }
     Ray r;
     init_ray(p, x, global_row(p, lr), r);
@@ -962,6 +985,56 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_tiles_kernel(const uint16
 
 size_t order_cost_capacity(int n_tiles) {
     return ((size_t)n_tiles + ORDER_CHUNK - 1) / ORDER_CHUNK * ORDER_CHUNK;
+}
+
+// XCD strips (remap 2): workgroup x orders the tiles of chunk x (the strip
+// that lands on XCD x, see tile_of_block_strips) heaviest class first and
+// writes them to the block positions b = 8 j + x; the per-XCD class ends (in
+// units of j) go to order[n + 4 + 4 x + c].
+__global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint16_t *__restrict__ cost,
+                                                                     uint32_t *__restrict__ order, int n, int tiles_x,
+                                                                     int g) {
+    __shared__ uint32_t red[ORDER_THREADS / 64];
+    __shared__ uint32_t cnt[4], base[4];
+    const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int len = n / 8, tiles_y = n / tiles_x;
+    auto tile_at = [&](int e) { return strip_tile(x, e, tiles_x, tiles_y, g); };
+    uint32_t mx = 0;
+    for (int e = tid; e < len; e += ORDER_THREADS) mx = max(mx, (uint32_t)cost[tile_at(e)]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+    if (lane == 0) red[wave] = mx;
+    if (tid < 4) cnt[tid] = 0;
+    __syncthreads();
+    mx = 0;
+#pragma unroll
+    for (int w = 0; w < ORDER_THREADS / 64; ++w) mx = max(mx, red[w]);
+    auto cls = [mx](uint32_t k) { return 2 * k >= mx ? 0 : 4 * k >= mx ? 1 : 8 * k >= mx ? 2 : 3; };
+    for (int e = tid; e < len; e += ORDER_THREADS) atomicAdd(&cnt[cls(cost[tile_at(e)])], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int c = 0; c < 4; ++c) {
+            base[c] = run;
+            run += cnt[c];
+            order[n + 4 + 4 * x + c] = run;
+        }
+        if (x == 0) for (int c = 0; c < 4; ++c) order[n + c] = 0;   // global bounds unused in this mode
+    }
+    __syncthreads();
+    for (int e = tid; e < len; e += ORDER_THREADS) {
+        const int t = tile_at(e);
+        const uint32_t j = atomicAdd(&base[cls(cost[t])], 1u);
+        order[(size_t)j * 8 + x] = (uint32_t)t;
+    }
+}
+
+hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, int strip_w,
+                               hipStream_t stream) {
+    if (n_tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
+                       strip_w);
+    return hipGetLastError();
 }
 
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream) {

@@ -76,7 +76,8 @@ struct svo_ctx {
     int kernel = 0;                  // 0 = tile (default), 1 = persistent; env SVO_KERNEL=tile|persistent
     int refill_at = 40;              // env SVO_REFILL
     int blocks_per_cu = 8;           // env SVO_BLOCKS_PER_CU
-    int xcd_remap = 0;               // env SVO_XCD_REMAP (measured slower: XCD load imbalance)
+    int xcd_remap = 2;               // env SVO_XCD_REMAP: 2 interleaved column strips (default), 1 row bands, 0 off
+    int strip_w = 1;                 // env SVO_STRIP_W: tile columns per strip (xcd_remap 2)
     int flat = 4;                    // env SVO_FLAT: 4 lean V2 (default), 3 lean, 1 flat, 0 branchy
     int block = 64;                  // env SVO_BLOCK (64 | 256)
     uint32_t options = 0;            // svo_set_options
@@ -246,6 +247,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.refill_at = ctx->refill_at;
     p.blocks_per_cu = ctx->blocks_per_cu;
     p.xcd_remap = ctx->xcd_remap;
+    p.strip_w = ctx->strip_w;
+    if (p.xcd_remap == 2 && (ctx->block != 64 || ((width + 7) / 8) % (8 * p.strip_w) != 0)) p.xcd_remap = 0;
     p.flat = ctx->flat;
     p.block = ctx->block;
     p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? 1 : 0;
@@ -264,7 +267,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     long long key = -1;
     if (ordered) {
         key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^ ((long long)b.band_rows << 8) ^
-              (long long)b.band_rank ^ ((long long)b.band_count << 4);
+              (long long)b.band_rank ^ ((long long)b.band_count << 4) ^ ((long long)ctx->xcd_remap << 60) ^ ((long long)ctx->strip_w << 52);
         if (ctx->tile_cap < (size_t)n_tiles) {
             HIP_TRY(hipDeviceSynchronize());   // a pending launch may still use the old buffers
             if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
@@ -276,7 +279,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             const size_t cap = svo::order_cost_capacity(n_tiles);
             HIP_TRY(hipMalloc(&ctx->d_tile_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(ctx->d_tile_cost, 0, cap * sizeof(uint16_t)));
-            HIP_TRY(hipMalloc(&ctx->d_tile_order, ((size_t)n_tiles + 4) * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&ctx->d_tile_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
             ctx->tile_cap = (size_t)n_tiles;
         }
         if (const char *f = std::getenv("SVO_ORDER_FILE")) {   // experiments: a fixed host-made order
@@ -326,7 +329,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
     const bool refresh = p.tile_cost && (ctx->order_key != key || ctx->order_launches++ % ctx->order_every == 0);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
-        e = svo::launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, s);
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, (width + 7) / 8,
+                                                        p.strip_w, s)
+                                : svo::launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, s);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         ctx->order_stream = s;
         ctx->order_pending = true;
@@ -373,7 +378,8 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "persistent") == 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
-    if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::max(0, std::min(2, std::atoi(k)));
+    if (const char *k = std::getenv("SVO_STRIP_W")) ctx->strip_w = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(4, std::atoi(k)));
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;

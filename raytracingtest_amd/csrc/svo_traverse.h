@@ -61,6 +61,7 @@ struct LaunchParams {
     uint16_t *tile_cost;
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
+    int strip_w;                  // xcd_remap 2: tile columns per super-column
 };
 
 // Order the tiles by recorded cost, most expensive class first, into `order`
@@ -70,6 +71,9 @@ struct LaunchParams {
 // beyond n_tiles is read, never used).
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream);
 size_t order_cost_capacity(int n_tiles);
+// The same per XCD strip (xcd_remap 2): order must hold n_tiles + 36 entries.
+hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, int strip_w,
+                               hipStream_t stream);
 
 // Progressive accumulation (AddShader blend) of an RGBA32F sample frame.
 hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32_t sample, int num_cus,

@@ -262,3 +262,18 @@ def test_accumulate_matches_oracle(rm, oracle_mod):
     assert rm.currentSample == 0
     with pytest.raises(SvoError):
         rm.accumulate_device(acc_d.data_ptr() + 4, smp_d.data_ptr(), n_px)
+
+
+def test_ordered_dispatch_repeat_renders_identical(rm, oracle_mod):
+    """Launches after the first dispatch tiles by recorded cost (heaviest class
+    first, interleaved XCD column strips, refreshed every 8th launch): placement
+    only, so every frame stays bit-identical to the oracle."""
+    svo = build_menger(8)
+    cam = overview_camera()
+    w, h = 960, 544
+    rm.SetSVOBuffer(svo)
+    rm.UpdateShaderParameters(cam, w, h)
+    ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, svo, cam, w, h)
+    for _ in range(10):
+        rgba, hits = rm.Render(w, h)
+        _compare(hits, rgba, ref_hits, ref_rgba)
