@@ -11,7 +11,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libsvo_rt.so")
+# SVO_RT_LIB: diagnostics only -- another build of this same library (tools/ab_lib.sh
+# compiles variants under build/ab/ and A/B-tests them in one GPU session)
+LIB_PATH = os.environ.get("SVO_RT_LIB") or os.path.join(PKG_DIR, "libsvo_rt.so")
 BUILDER_PATH = os.path.join(PKG_DIR, "libsvo_build.so")
 
 SVO_OK = 0

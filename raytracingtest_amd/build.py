@@ -18,7 +18,10 @@ INCLUDE = os.path.join(ROOT, "include")
 ARCH = os.environ.get("SVO_OFFLOAD_ARCH", "gfx950")
 
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+# -fno-slp-vectorize (device): packed f32 ops (v_pk_mul/add_f32) and the register
+# pair copies they need made the traversal loop ~3 % slower (tools/ab_lib.sh).
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+          "-Xarch_device", "-fno-slp-vectorize",
           "-Wno-unused-value", "-Wno-unused-result", "-I" + INCLUDE, "-I" + CSRC]
 
 TARGETS = {
