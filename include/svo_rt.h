@@ -107,8 +107,16 @@ int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode,
  * the reference's shadow test is commented out at RaytraceCompute.compute:105-112):
  * origin = world hit point + 0.001 * normal; an occluded pixel gets hit flag
  * bit 3 and a black Result. */
-enum { SVO_OPT_SHADOW_RAYS = 1 };
+enum { SVO_OPT_SHADOW_RAYS = 1, SVO_OPT_KERNEL_TIMING = 2 };
 int svo_set_options(svo_ctx *ctx, uint32_t options);
+
+/* SVO_OPT_KERNEL_TIMING: every render launch brackets its primary-ray kernel
+ * (only that kernel: not the shadow pass, not the dispatch-order kernel) with
+ * HIP events on the launch stream.  svo_kernel_time waits for the recorded
+ * launches and returns their mean kernel duration in ms and their number, then
+ * forgets them.  Measurement only (bench.py's roofline); no reference
+ * counterpart. */
+int svo_kernel_time(svo_ctx *ctx, double *mean_ms, uint64_t *launches);
 
 /* ~ Graphics.Blit(Result, destination, AddMaterial) with _Sample = `sample`
  * (RaytracingMaster.cs:70-73, AddShader.shader:10,44-47): progressive

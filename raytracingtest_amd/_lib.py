@@ -27,8 +27,10 @@ assert HIT_DTYPE.itemsize == 24
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
-           "svo_destroy", "svo_last_error", "svo_abi_version", "svo_set_options", "svo_accumulate")
+           "svo_destroy", "svo_last_error", "svo_abi_version", "svo_set_options", "svo_accumulate",
+           "svo_kernel_time")
 SVO_OPT_SHADOW_RAYS = 1
+SVO_OPT_KERNEL_TIMING = 2
 
 
 class SvoBand(ctypes.Structure):
@@ -67,6 +69,7 @@ def lib():
     L.svo_render_device.argtypes = [vp, i, i, i, vp, vp, vp, vp]
     L.svo_count_fetches.argtypes = [vp, i, i, i, vp, vp, vp]
     L.svo_set_options.argtypes = [vp, ctypes.c_uint32]
+    L.svo_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
     L.svo_accumulate.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, vp]
     L.svo_get_info.argtypes = [vp, ctypes.POINTER(sz), ctypes.POINTER(i), ctypes.POINTER(i)]
     L.svo_synchronize.argtypes = [vp]

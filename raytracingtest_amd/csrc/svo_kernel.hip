@@ -422,8 +422,8 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     const int scale_lo = S_MAX - slots;
     const float sexp_lo = __int_as_float((scale_lo - S_MAX + 127) << 23);   // push below scale_lo overflows
     lmask act = LM_OF(true);
-    int idx = r.idx;                       // child index bits (per lane, VGPR)
     const int oct = V2 ? (r.octant_mask | 16) : r.octant_mask;   // V2: c ^ (oct | 16) == (c ^ oct) + 16
+    int sh = r.idx ^ oct;                  // child index bits ^ oct: the descriptor shift (per lane, VGPR)
     lmask cached = 0, capped = 0, ovf = 0;
     const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
     constexpr uint32_t SLOT = (uint32_t)(STRIDE * sizeof(uint2));
@@ -465,7 +465,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const lmask cz = LM_OF(half * r.cz + tz > r.t_min);
         const lmask lx = LM_OF(tx <= tc_max), ly = LM_OF(ty <= tc_max), lz = LM_OF(tz <= tc_max);
         const lmask in_span = LM_OF(r.t_min <= tv_max), below_h = LM_OF(tc_max < r.h);
-        const uint32_t cm = r.cd16 << (idx ^ oct);       // valid bit -> bit 31, leaf bit -> bit 23
+        const uint32_t cm = r.cd16 << sh;                // valid bit -> bit 31, leaf bit -> bit 23
         const lmask descend = act & LM_OF((int32_t)cm < 0) & in_span;
         const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
         const lmask hit = descend & leaf;                // N:93-94
@@ -491,14 +491,18 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const float se = r.sexp;
         const float delta = LM_ON(push) ? half : -se;
         const float ox = r.px, oy = r.py, oz = r.pz;
-        const float qx = r.px + (LM_ON((push & cx) | sx) ? delta : 0.0f);
-        const float qy = r.py + (LM_ON((push & cy) | sy) ? delta : 0.0f);
-        const float qz = r.pz + (LM_ON((push & cz) | sz) ? delta : 0.0f);
-        const int step = lanes_to_idx(sx, sy, sz);       // 0 outside ADVANCE lanes
-        const lmask pop = LM_OF((step & ~idx) != 0);     // N:130-131: (idx ^ step) & step
+        // per axis: PUSH lanes move into the child half, ADVANCE lanes step (PUSH and
+        // ADVANCE lanes are disjoint, so one mask per axis serves both)
+        const lmask mvx = (push & cx) | sx, mvy = (push & cy) | sy, mvz = (push & cz) | sz;
+        const float qx = r.px + (LM_ON(mvx) ? delta : 0.0f);
+        const float qy = r.py + (LM_ON(mvy) ? delta : 0.0f);
+        const float qz = r.pz + (LM_ON(mvz) ? delta : 0.0f);
+        // the same three masks as an integer: the child index on PUSH lanes (N:111-116),
+        // the step mask on ADVANCE lanes (N:122-128), 0 elsewhere
+        const int mv = lanes_to_idx(mvx, mvy, mvz);
+        const lmask pop = adv & LM_OF((mv & ~(sh ^ oct)) != 0);   // N:130-131: (idx ^ step) & step
         const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
-        const int cidx = lanes_to_idx(cx, cy, cz);
-        idx = LM_ON(push) ? cidx : (idx ^ step);
+        sh = (LM_ON(push) ? oct : sh) ^ mv;             // PUSH: idx = mv, else idx ^= mv
         if (LM_ON(push)) {
             r.parent = child;
             r.h = tc_max;
@@ -560,7 +564,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
                 r.pz = pl ? __uint_as_float(__float_as_uint(qz) & keep) : r.pz;
             }
             r.h = pl ? 0.0f : r.h;
-            idx = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) : idx;
+            sh = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) ^ oct : sh;
             out = pop & LM_OF(scale >= S_MAX);
         }
         ovf |= of;
@@ -568,7 +572,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     }
     capped = act;                          // still tracing after MAX_ITERS trips
     if (DIAG) diag->loop_cycles = __builtin_amdgcn_s_memtime() - tl0;
-    r.idx = idx;
+    r.idx = sh ^ oct;
     r.trips = it;
     if (LM_ON(capped)) r.flags |= 2u;
     if (LM_ON(ovf)) r.flags |= 4u;
@@ -1086,19 +1090,21 @@ static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
 }
 
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel, uint32_t *counter,
-                         int num_cus) {
+                         int num_cus, hipEvent_t primary_start, hipEvent_t primary_end) {
+    // primary_start / primary_end (nullable): events around the primary-ray kernel only
     const bool count = p.fetches != nullptr;
-    if (!count && p.shadows && p.hits) {
-        hipError_t e = stack_mode == 0 ? launch_variant<0, false>(p, stream, kernel, counter, num_cus)
-                                       : launch_variant<1, false>(p, stream, kernel, counter, num_cus);
-        if (e != hipSuccess) return e;
-        return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
-    }
+    hipError_t e = hipSuccess;
+    if (primary_start && (e = hipEventRecord(primary_start, stream)) != hipSuccess) return e;
     if (stack_mode == 0)
-        return count ? launch_variant<0, true>(p, stream, kernel, counter, num_cus)
-                     : launch_variant<0, false>(p, stream, kernel, counter, num_cus);
-    return count ? launch_variant<1, true>(p, stream, kernel, counter, num_cus)
-                 : launch_variant<1, false>(p, stream, kernel, counter, num_cus);
+        e = count ? launch_variant<0, true>(p, stream, kernel, counter, num_cus)
+                  : launch_variant<0, false>(p, stream, kernel, counter, num_cus);
+    else
+        e = count ? launch_variant<1, true>(p, stream, kernel, counter, num_cus)
+                  : launch_variant<1, false>(p, stream, kernel, counter, num_cus);
+    if (e != hipSuccess) return e;
+    if (primary_end && (e = hipEventRecord(primary_end, stream)) != hipSuccess) return e;
+    if (!count && p.shadows && p.hits) return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
+    return hipSuccess;
 }
 
 }  // namespace svo

@@ -81,6 +81,9 @@ struct svo_ctx {
     int flat = 4;                    // env SVO_FLAT: 4 lean V2 (default), 3 lean, 1 flat, 0 branchy
     int block = 64;                  // env SVO_BLOCK (64 | 256)
     uint32_t options = 0;            // svo_set_options
+    // SVO_OPT_KERNEL_TIMING: event pairs around the primary kernel of each launch
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timing_events;   // recorded, not yet read
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timing_free;     // reusable
     uint32_t *d_wave_log = nullptr;  // diagnostics: env SVO_WAVE_LOG=<file> (tile kernel, SVO_FLAT=3)
     size_t wave_log_cap = 0;
     // Cost-ordered tile dispatch: every launch records each 8x8 tile's trip
@@ -325,7 +328,22 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         HIP_TRY(hipStreamSynchronize(ctx->order_stream));
         ctx->order_pending = false;
     }
-    hipError_t e = svo::launch_render(p, stack_mode, s, ctx->kernel, ctx->d_counter, ctx->num_cus);
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if ((ctx->options & SVO_OPT_KERNEL_TIMING) && !p.fetches) {
+        if (ctx->timing_free.empty()) {
+            HIP_TRY(hipEventCreate(&ev0));
+            if (hipEventCreate(&ev1) != hipSuccess) {
+                hipEventDestroy(ev0);
+                return fail(SVO_ERR_HIP, "hipEventCreate");
+            }
+        } else {
+            ev0 = ctx->timing_free.back().first;
+            ev1 = ctx->timing_free.back().second;
+            ctx->timing_free.pop_back();
+        }
+        ctx->timing_events.emplace_back(ev0, ev1);
+    }
+    hipError_t e = svo::launch_render(p, stack_mode, s, ctx->kernel, ctx->d_counter, ctx->num_cus, ev0, ev1);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
     const bool refresh = p.tile_cost && (ctx->order_key != key || ctx->order_launches++ % ctx->order_every == 0);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
@@ -499,8 +517,28 @@ int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode, const
 
 int svo_set_options(svo_ctx *ctx, uint32_t options) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
-    if (options & ~(uint32_t)SVO_OPT_SHADOW_RAYS) return fail(SVO_ERR_ARG, "unknown option bits");
+    if (options & ~(uint32_t)(SVO_OPT_SHADOW_RAYS | SVO_OPT_KERNEL_TIMING)) return fail(SVO_ERR_ARG, "unknown option bits");
     ctx->options = options;
+    return SVO_OK;
+}
+
+int svo_kernel_time(svo_ctx *ctx, double *mean_ms, uint64_t *launches) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    HIP_TRY(hipSetDevice(ctx->device));
+    double sum = 0.0;
+    uint64_t n = 0;
+    hipError_t err = hipSuccess;
+    for (auto &ev : ctx->timing_events) {
+        float ms = 0.0f;
+        if (err == hipSuccess) err = hipEventSynchronize(ev.second);
+        if (err == hipSuccess) err = hipEventElapsedTime(&ms, ev.first, ev.second);
+        if (err == hipSuccess) { sum += ms; ++n; }
+        ctx->timing_free.push_back(ev);
+    }
+    ctx->timing_events.clear();
+    if (err != hipSuccess) return fail(SVO_ERR_HIP, std::string("svo_kernel_time: ") + hipGetErrorString(err));
+    if (mean_ms) *mean_ms = n ? sum / (double)n : 0.0;
+    if (launches) *launches = n;
     return SVO_OK;
 }
 
@@ -543,6 +581,8 @@ int svo_destroy(svo_ctx *ctx) {
     if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
     if (ctx->d_counter) hipFree(ctx->d_counter);
+    for (auto &ev : ctx->timing_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+    for (auto &ev : ctx->timing_free) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
     if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
     if (ctx->d_tile_order) hipFree(ctx->d_tile_order);

@@ -82,6 +82,7 @@ hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32
 // kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).
 // counter: 16-byte device work counter (persistent kernel), num_cus: CU count.
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel,
-                         uint32_t *counter, int num_cus);
+                         uint32_t *counter, int num_cus, hipEvent_t primary_start = nullptr,
+                         hipEvent_t primary_end = nullptr);
 
 }  // namespace svo

@@ -34,6 +34,7 @@ class RaytracingMaster:
         self._ctx = ctypes.c_void_p()
         self._camera_set = False
         self._c2w = None
+        self._options = 0               # svo_set_options bits
         self.currentSample = 0          # _currentSample (RaytracingMaster.cs:12)
         self.InitializeSVOBuffer()
 
@@ -44,6 +45,7 @@ class RaytracingMaster:
             L.svo_destroy(self._ctx)
             self._ctx = ctypes.c_void_p()
         check(L.svo_create(self.device, self.capacity_nodes, ctypes.byref(self._ctx)), "svo_create")
+        self._options = 0
 
     def SetSVOBuffer(self, data=None, offset=0):
         """Upload an SVOData at descriptor `offset`; with no data, build one from
@@ -84,10 +86,26 @@ class RaytracingMaster:
                                         float(pixel_offset[1]), lt.ctypes.data), "svo_set_camera")
         self._camera_set = True
 
+    def _set_option(self, bit, enable):
+        self._options = (self._options | bit) if enable else (self._options & ~bit)
+        check(_lib.lib().svo_set_options(self._ctx, self._options), "svo_set_options")
+
     def SetShadowRays(self, enable=True):
         """Trace one shadow ray per primary hit toward -_DirectionalLight (the
         reference's commented-out test, RaytraceCompute.compute:105-112)."""
-        check(_lib.lib().svo_set_options(self._ctx, _lib.SVO_OPT_SHADOW_RAYS if enable else 0), "svo_set_options")
+        self._set_option(_lib.SVO_OPT_SHADOW_RAYS, enable)
+
+    def set_kernel_timing(self, enable=True):
+        """Bracket the primary-ray kernel of every launch with HIP events
+        (measurement only; read with kernel_time())."""
+        self._set_option(_lib.SVO_OPT_KERNEL_TIMING, enable)
+
+    def kernel_time(self):
+        """(mean primary-kernel ms, launches) over the launches timed since the last call."""
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        check(_lib.lib().svo_kernel_time(self._ctx, ctypes.byref(ms), ctypes.byref(n)), "svo_kernel_time")
+        return ms.value, n.value
 
     # ----------------------------------------------------------------- render
     def Render(self, width, height, stack_mode=STACK_HLSL, want_rgba=True, want_hits=True):
