@@ -112,6 +112,12 @@ void orc_sky(const float dir[3], float out[3]) {
  * V1 keeps its whole word so the HLSL `child_descriptor == 0` test holds) and
  * the absolute first-child index in *first. */
 static inline int fetch_node(const orc_svo *svo, uint32_t parent, uint32_t *lo, uint32_t *first) {
+    if ((size_t)parent >= svo->n_nodes) {
+        /* only an HLSL-rounded stack parent of a pool above 2^24 nodes gets here:
+         * an out-of-range StructuredBuffer element reads as 0 */
+        *lo = 0; *first = 0;
+        return 0;
+    }
     if (svo->format == ORC_FMT_V1) {
         uint32_t cd = (uint32_t)svo->desc[parent];
         *lo = cd;

@@ -233,6 +233,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     svo::LaunchParams p;
     p.nodes = ctx->d_nodes;
     p.att = ctx->d_att;
+    p.n_nodes = (uint32_t)std::min<size_t>(ctx->n_nodes, 0xFFFFFFFFu);
     p.cam = ctx->cam;
     p.width = width;
     p.height = height;

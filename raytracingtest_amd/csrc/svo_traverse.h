@@ -40,6 +40,7 @@ static_assert(sizeof(Hit) == 24, "hit record layout");
 struct LaunchParams {
     const uint2 *nodes;
     const uint2 *att;
+    uint32_t n_nodes;     // pool size (index bound for fetches of HLSL-rounded parents)
     Camera cam;
     int width, height;
     int band_rows, band_rank, band_count, local_rows;
