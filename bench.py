@@ -224,7 +224,8 @@ def main():
         workload = (f"{args.config} depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) {kind} SVO, "
                     f"{W}x{H} primary rays" + (" + 1 shadow ray per hit" if args.shadows else "") +
                     f", {args.camera} camera")
-        traffic = pmc_traffic(workload)
+        # the committed PMC figure is per launch of the full-frame workload (not a band of it)
+        traffic = pmc_traffic(workload) if band is None else None
         out = {
             "metric": METRIC,
             "value": round(mrays, 2),
