@@ -1015,9 +1015,23 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     __shared__ uint32_t cnt[4], base[4];
     const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int len = n / 8, tiles_y = n / tiles_x;
-    auto tile_at = [&](int e) { return strip_tile(x, e, tiles_x, tiles_y, g); };
+    // position e of this XCD's list is (column c = e / tiles_y, row e % tiles_y) of its
+    // strips (strip_tile); the threads walk it in steps of ORDER_THREADS with one
+    // division at the start instead of integer divisions per element (11.6 -> 9.7 us
+    // per launch at 1080p)
+    const int dc = ORDER_THREADS / tiles_y, dr = ORDER_THREADS % tiles_y;
+    struct Walk { int e, c, r; };
+    auto start = [&]() { return Walk{tid, tid / tiles_y, tid % tiles_y}; };
+    auto next = [&](Walk &w) {
+        w.e += ORDER_THREADS; w.c += dc; w.r += dr;
+        if (w.r >= tiles_y) { w.r -= tiles_y; w.c += 1; }
+    };
+    auto tile_of = [&](const Walk &w) {
+        const int m = g == 1 ? w.c : w.c / g, cix = g == 1 ? 0 : w.c - m * g;
+        return w.r * tiles_x + (m * 8 + x) * g + cix;
+    };
     uint32_t mx = 0;
-    for (int e = tid; e < len; e += ORDER_THREADS) mx = max(mx, (uint32_t)cost[tile_at(e)]);
+    for (Walk w = start(); w.e < len; next(w)) mx = max(mx, (uint32_t)cost[tile_of(w)]);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
     if (lane == 0) red[wave] = mx;
@@ -1027,7 +1041,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
 #pragma unroll
     for (int w = 0; w < ORDER_THREADS / 64; ++w) mx = max(mx, red[w]);
     auto cls = [mx](uint32_t k) { return 2 * k >= mx ? 0 : 4 * k >= mx ? 1 : 8 * k >= mx ? 2 : 3; };
-    for (int e = tid; e < len; e += ORDER_THREADS) atomicAdd(&cnt[cls(cost[tile_at(e)])], 1u);
+    for (Walk w = start(); w.e < len; next(w)) atomicAdd(&cnt[cls(cost[tile_of(w)])], 1u);
     __syncthreads();
     if (tid == 0) {
         uint32_t run = 0;
@@ -1039,8 +1053,8 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         if (x == 0) for (int c = 0; c < 4; ++c) order[n + c] = 0;   // global bounds unused in this mode
     }
     __syncthreads();
-    for (int e = tid; e < len; e += ORDER_THREADS) {
-        const int t = tile_at(e);
+    for (Walk w = start(); w.e < len; next(w)) {
+        const int t = tile_of(w);
         const uint32_t j = atomicAdd(&base[cls(cost[t])], 1u);
         order[(size_t)j * 8 + x] = (uint32_t)t;
     }
