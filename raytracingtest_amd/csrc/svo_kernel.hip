@@ -711,8 +711,8 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
         to_fray(r, f);
         LeanDiag dg;
         if (p.wave_log) {
-            if (p.guard) trace_lean<MODE, BS, true, true>(p, f, stk, &dg);
-            else trace_lean<MODE, BS, false, true>(p, f, stk, &dg);
+            if (p.guard) trace_lean<MODE, BS, true, true, STEP == 4>(p, f, stk, &dg);
+            else trace_lean<MODE, BS, false, true, STEP == 4>(p, f, stk, &dg);
         }
         else if (p.guard) trace_lean<MODE, BS, true, false, STEP == 4>(p, f, stk);
         else trace_lean<MODE, BS, false, false, STEP == 4>(p, f, stk);
