@@ -277,3 +277,75 @@ def test_ordered_dispatch_repeat_renders_identical(rm, oracle_mod):
     for _ in range(10):
         rgba, hits = rm.Render(w, h)
         _compare(hits, rgba, ref_hits, ref_rgba)
+
+
+def _rounded_parent_pool(base):
+    """Depth-3 V2 pool: root -> 8 interior children at base..base+7 -> 64 leaf
+    parents (indices 1..64) with one leaf each.  With base = 2^24 - 4 the
+    children sit at 2^24 - 4 .. 2^24 + 3, so the HLSL stack round trip
+    (int2 <- float2((int)parent, ...), NVIDIASVO.compute:98) turns 2^24 + 1 into
+    2^24 (another node) and 2^24 + 3 into 2^24 + 4 == the pool size."""
+    n = base + 8
+    nodes = np.zeros(n, np.uint64)
+    nodes[0] = (np.uint64(base) << np.uint64(32)) | np.uint64(0xFFFF)
+    for k in range(8):
+        nodes[base + k] = (np.uint64(1 + 8 * k) << np.uint64(32)) | np.uint64(0xFFFF)
+    for g in range(1, 65):
+        nodes[g] = np.uint64((1 << ((g * 5) % 8)) << 8)      # one leaf child, no non-leaf ones
+    return SVOData(nodes=nodes)
+
+
+def test_out_of_range_rounded_parent_reads_zero(oracle_mod):
+    """A pool above 2^24 nodes traced with the HLSL stack: a POP may restore a
+    rounded parent index beyond the pool; kernel and oracle both read it as 0
+    (an out-of-range StructuredBuffer element) -- bit-identical frames, and
+    different from the same tree laid out below 2^24 (so the path is exercised)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    big = _rounded_parent_pool((1 << 24) - 4)
+    small = _rounded_parent_pool(65)
+    cam = overview_camera()
+    w, h = 192, 128
+    frames = {}
+    for name, svo in (("big", big), ("small", small)):
+        m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+        try:
+            m.SetSVOBuffer(svo)
+            m.UpdateShaderParameters(cam, w, h)
+            rgba, hits = m.Render(w, h, stack_mode=0)
+        finally:
+            m.close()
+        ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, svo, cam, w, h, mode=0)
+        _compare(hits, rgba, ref_hits, ref_rgba)
+        frames[name] = hits.reshape(-1)
+    hit_big = (frames["big"]["flags"] & 1) != 0
+    hit_small = (frames["small"]["flags"] & 1) != 0
+    assert hit_small.sum() > 0
+    assert np.count_nonzero(hit_big != hit_small) > 0, "no ray went through a rounded parent"
+
+
+def test_kernel_timing_counts_primary_launches(rm, text_svo):
+    """SVO_OPT_KERNEL_TIMING brackets the primary-ray kernel of every launch
+    (not the shadow pass); svo_kernel_time returns the mean and forgets them."""
+    import torch
+    w, h = 256, 128
+    rm.SetSVOBuffer(text_svo)
+    rm.UpdateShaderParameters(overview_camera(), w, h)
+    hits = torch.empty(w * h * 24, dtype=torch.uint8, device="cuda")
+    rm.set_kernel_timing(True)
+    try:
+        rm.kernel_time()
+        for _ in range(3):
+            rm.render_device(w, h, hits_ptr=hits.data_ptr())
+        rm.SetShadowRays(True)
+        rm.render_device(w, h, hits_ptr=hits.data_ptr())
+        rm.SetShadowRays(False)
+        ms, n = rm.kernel_time()
+        assert n == 4 and ms > 0.0
+        assert rm.kernel_time() == (0.0, 0)
+    finally:
+        rm.set_kernel_timing(False)
+    rm.render_device(w, h, hits_ptr=hits.data_ptr())
+    rm.synchronize()
+    assert rm.kernel_time() == (0.0, 0)
