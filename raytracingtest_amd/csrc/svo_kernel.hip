@@ -752,14 +752,30 @@ __global__ __launch_bounds__(BS) void shadow_tile_kernel(LaunchParams p, int blo
     extern __shared__ uint2 stk_base[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int t = (int)blockIdx.x;
+    // cost-ordered like the primary pass (the shadow pass's own recorded trip
+    // counts): heaviest class first, interleaved XCD column strips, s_setprio by class
+    const int t = p.shadow_order ? (int)p.shadow_order[blockIdx.x]
+                : p.xcd_remap == 2 ? tile_of_block_strips((int)blockIdx.x, (int)gridDim.x, blocks_x, p.strip_w)
+                                   : (int)blockIdx.x;
+    if (p.shadow_order && p.prio) {
+        const bool strips = p.xcd_remap == 2;
+        const uint32_t *bound = strips ? p.shadow_order + gridDim.x + 4 + 4 * (blockIdx.x % 8) : p.shadow_order + gridDim.x;
+        const uint32_t b = strips ? blockIdx.x / 8 : blockIdx.x;
+        if (b < bound[0]) __builtin_amdgcn_s_setprio(3);
+        else if (b < bound[1]) __builtin_amdgcn_s_setprio(2);
+        else if (b < bound[2]) __builtin_amdgcn_s_setprio(1);
+    }
     const int x = (t % blocks_x) * 8 + (lane & 7);
     const int lr = (t / blocks_x) * 8 + (lane >> 3);
-    if (x >= p.width || lr >= p.local_rows) return;
+    const bool inside = x < p.width && lr < p.local_rows;
     const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
     uint2 *rec = reinterpret_cast<uint2 *>(p.hits + out);
-    const uint2 w01 = rec[0], w23 = rec[1], w45 = rec[2];
-    if (!((w01.y >> 16) & 1u)) return;
+    const uint2 w01 = inside ? rec[0] : make_uint2(0u, 0u);
+    const bool hit = (w01.y >> 16) & 1u;
+    const bool any_hit = __ballot(hit) != 0;   // whole wave, before any lane leaves
+    if (p.shadow_cost && lane == 0 && !any_hit) p.shadow_cost[t] = 0;
+    if (!hit) return;
+    const uint2 w23 = rec[1], w45 = rec[2];
     float org[3], dir[3];
     camera_ray(p, x, global_row(p, lr), org, dir);
     const float tw = __int_as_float((int32_t)w23.x) * (1.0f / 64.0f);
@@ -779,6 +795,7 @@ __global__ __launch_bounds__(BS) void shadow_tile_kernel(LaunchParams p, int blo
     if (p.guard) trace_lean<MODE, BS, true, false, true>(p, f, stk);
     else trace_lean<MODE, BS, false, false, true>(p, f, stk);
     from_fray(f, r);
+    if (p.shadow_cost) p.shadow_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every tracing lane
     if (r.scale < S_MAX) {   // occluded
         rec[0] = make_uint2(w01.x, w01.y | (8u << 16));
         if (p.rgba) p.rgba[out] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);

@@ -91,10 +91,15 @@ struct svo_ctx {
     // heaviest-first dispatch order of the next launch at the same geometry.
     int tile_order = 1;              // env SVO_TILE_ORDER=0 disables
     int prio = 1;                    // env SVO_PRIO=0: no issue priority by cost class
+    int shadow_order_enabled = 1;    // env SVO_SHADOW_ORDER=0: shadow tiles in plain strip order
     int order_every = 8;             // env SVO_ORDER_EVERY: rebuild the order every k-th launch (~20 us one-CU kernel)
     unsigned long long order_launches = 0;
     uint16_t *d_tile_cost = nullptr;
     uint32_t *d_tile_order = nullptr;
+    uint16_t *d_shadow_cost = nullptr;   // the shadow pass's own costs and order
+    uint32_t *d_shadow_order = nullptr;
+    long long shadow_order_key = -1;
+    unsigned long long shadow_launches = 0;
     size_t tile_cap = 0;
     long long order_key = -1;        // geometry d_tile_order was built for (-1: none)
     hipStream_t order_stream = nullptr;   // stream of the last order kernel (a launch elsewhere syncs it first)
@@ -265,6 +270,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.wave_log = nullptr;
     p.tile_order = nullptr;
     p.tile_cost = nullptr;
+    p.shadow_order = nullptr;
+    p.shadow_cost = nullptr;
     p.prio = ctx->prio;
     const bool ordered = ctx->tile_order && ctx->kernel == 0 && ctx->flat >= 3 && ctx->block == 64 && !p.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
@@ -276,14 +283,22 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             HIP_TRY(hipDeviceSynchronize());   // a pending launch may still use the old buffers
             if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
             if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
+            if (ctx->d_shadow_cost) hipFree(ctx->d_shadow_cost);
+            if (ctx->d_shadow_order) hipFree(ctx->d_shadow_order);
             ctx->d_tile_cost = nullptr;
             ctx->d_tile_order = nullptr;
+            ctx->d_shadow_cost = nullptr;
+            ctx->d_shadow_order = nullptr;
             ctx->tile_cap = 0;
             ctx->order_key = -1;
+            ctx->shadow_order_key = -1;
             const size_t cap = svo::order_cost_capacity(n_tiles);
             HIP_TRY(hipMalloc(&ctx->d_tile_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(ctx->d_tile_cost, 0, cap * sizeof(uint16_t)));
             HIP_TRY(hipMalloc(&ctx->d_tile_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&ctx->d_shadow_cost, cap * sizeof(uint16_t)));
+            HIP_TRY(hipMemset(ctx->d_shadow_cost, 0, cap * sizeof(uint16_t)));
+            HIP_TRY(hipMalloc(&ctx->d_shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
             ctx->tile_cap = (size_t)n_tiles;
         }
         if (const char *f = std::getenv("SVO_ORDER_FILE")) {   // experiments: a fixed host-made order
@@ -308,6 +323,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             p.tile_order = ctx->order_key == key ? ctx->d_tile_order : nullptr;
         }
         if (!std::getenv("SVO_ORDER_FILE")) p.tile_cost = ctx->d_tile_cost;
+        if (p.shadows && ctx->shadow_order_enabled) {
+            p.shadow_cost = ctx->d_shadow_cost;
+            p.shadow_order = ctx->shadow_order_key == key ? ctx->d_shadow_order : nullptr;
+        }
     }
     const char *log_path = std::getenv("SVO_WAVE_LOG");
     const size_t n_wave = (size_t)((width + 15) / 16) * (size_t)((p.local_rows + 15) / 16) * 4;   // >= any tiling
@@ -356,6 +375,15 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         ctx->order_pending = true;
         ctx->order_key = key;
     }
+    if (p.shadow_cost && (ctx->shadow_order_key != key || ctx->shadow_launches++ % ctx->order_every == 0)) {
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(ctx->d_shadow_cost, ctx->d_shadow_order, n_tiles, (width + 7) / 8,
+                                                        p.strip_w, s)
+                             : svo::launch_order_tiles(ctx->d_shadow_cost, ctx->d_shadow_order, n_tiles, s);
+        if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("shadow order launch: ") + hipGetErrorString(e));
+        ctx->order_stream = s;
+        ctx->order_pending = true;
+        ctx->shadow_order_key = key;
+    }
     if (p.wave_log) {   // blocking dump of the last launch's per-wave record
         HIP_TRY(hipStreamSynchronize(s));
         std::vector<uint32_t> h(n_wave * 8);
@@ -402,6 +430,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(4, std::atoi(k)));
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_SHADOW_ORDER")) ctx->shadow_order_enabled = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_BLOCK")) { const int b = std::atoi(k); ctx->block = (b == 256 || b == 128) ? b : 64; }
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));
@@ -582,6 +611,8 @@ int svo_destroy(svo_ctx *ctx) {
     if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
     if (ctx->d_counter) hipFree(ctx->d_counter);
+    if (ctx->d_shadow_cost) hipFree(ctx->d_shadow_cost);
+    if (ctx->d_shadow_order) hipFree(ctx->d_shadow_order);
     for (auto &ev : ctx->timing_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     for (auto &ev : ctx->timing_free) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     if (ctx->d_wave_log) hipFree(ctx->d_wave_log);

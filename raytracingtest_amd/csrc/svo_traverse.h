@@ -63,6 +63,9 @@ struct LaunchParams {
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
     int strip_w;                  // xcd_remap 2: tile columns per super-column
+    // The same cost-ordered dispatch for the shadow pass (its own costs and order).
+    const uint32_t *shadow_order;
+    uint16_t *shadow_cost;
 };
 
 // Order the tiles by recorded cost, most expensive class first, into `order`
