@@ -414,9 +414,10 @@ struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
 template <int MODE, int STRIDE, bool GUARD, bool DIAG = false, bool V2 = false>
 __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk,
                                            LeanDiag *diag = nullptr) {
-    // GUARD = false (host-proven, svo_rt.hip recompute_depth): one tree of known
-    // depth and parent indices below 2^24, so a PUSH never overflows the stack
-    // and the HLSL round trip of a parent index is the identity.
+    // GUARD = false (host-proven, svo_rt.hip launch / recompute_depth): one tree of
+    // known depth, fewer than 2^29 nodes, and (HLSL stack) parent indices below
+    // 2^24, so a PUSH never overflows the stack, the HLSL round trip of a parent
+    // index is the identity and node byte offsets fit 32 bits.
     const int slots = p.slots;
     // + the spare slot: a ray that leaves the root takes its parent from there, and
     // (V2, !GUARD) every lane, finished ones too, fetches nodes[parent] on every trip
@@ -452,8 +453,8 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         // ray that left the root holds the cleared spare slot's 0.
         const lmask need = (V2 && !GUARD) ? ~(lmask)0 : act & ~cached;
         if ((V2 && !GUARD) || LM_ON(need)) {
-            // GUARD == false: pool below 2^24 nodes, so the byte offset fits 32 bits
-            // (global_load saddr + 32-bit voffset, no 64-bit address add).  GUARD: an
+            // GUARD == false: pool below 2^29 nodes (svo_rt.hip), so the byte offset fits
+            // 32 bits (global_load saddr + 32-bit voffset, no 64-bit address add).  GUARD: an
             // HLSL-rounded parent index (> 2^24 nodes) may lie outside the pool; it
             // reads as 0 like an out-of-range StructuredBuffer element.
             const uint2 nd = GUARD ? (r.parent < p.n_nodes ? p.nodes[r.parent] : make_uint2(0u, 0u))

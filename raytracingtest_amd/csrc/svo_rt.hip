@@ -249,7 +249,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.slots = std::max(ctx->depth - 1, 1);
     // guard: stack-overflow test + HLSL parent round trip, needed unless the
     // pool is one tree of known depth whose parent indices are exact in f32
-    p.guard = !ctx->depth_exact || (stack_mode == 0 && ctx->n_nodes > ((size_t)1 << 24));
+    // (and the lean loop's 32-bit node byte offsets need fewer than 2^29 nodes)
+    p.guard = !ctx->depth_exact || (stack_mode == 0 && ctx->n_nodes > ((size_t)1 << 24)) ||
+              ctx->n_nodes >= ((size_t)1 << 29);
     p.hits = reinterpret_cast<svo::Hit *>(d_hits);
     p.rgba = reinterpret_cast<float4 *>(d_rgba);
     p.fetches = d_fetch;
