@@ -411,7 +411,7 @@ struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
     uint32_t fetch_trips = 0, pop_trips = 0;
 };
 
-template <int MODE, int STRIDE, bool GUARD, bool DIAG = false, bool V2 = false>
+template <int MODE, int STRIDE, bool GUARD, bool DIAG = false, bool V2 = false, bool FETCH_ALL = false>
 __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk,
                                            LeanDiag *diag = nullptr) {
     // GUARD = false (host-proven, svo_rt.hip launch / recompute_depth): one tree of
@@ -445,14 +445,17 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     while (act != 0 && it < MAX_ITERS) {   // one exit: the cap is part of the loop test
         // wave-uniform trip count kept in an SGPR (LLVM otherwise counts down in a VGPR)
         asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
-        // N:60-62.  V2 && !GUARD: every lane fetches on every trip, unpredicated --
-        // re-fetching a cached node reads the same word, and a load outside a
-        // divergent branch issues at the top of the trip with nothing to wait for
-        // (measured 5 % faster than fetching only the lanes that need it).  Every
-        // lane's parent is a valid index: a pool proven to be one tree, and a
-        // ray that left the root holds the cleared spare slot's 0.
-        const lmask need = (V2 && !GUARD) ? ~(lmask)0 : act & ~cached;
-        if ((V2 && !GUARD) || LM_ON(need)) {
+        // N:60-62.  FETCH_ALL (V2, !GUARD, pools below 2^24 nodes -- svo_rt.hip):
+        // every lane fetches on every trip, unpredicated; re-fetching a cached node
+        // reads the same word, and a load outside a divergent branch issues at the
+        // top of the trip with nothing to wait for (C3: 5 % faster, 9 % on the
+        // sky-heavy overview pose).  On the 25 M / 100 M-node pools of C4 / C5 the
+        // extra loads cost 6-12 %, so those fetch only the lanes that need a node.
+        // Every lane's parent is a valid index: a pool proven to be one tree, and
+        // a ray that left the root holds the cleared spare slot's 0.
+        constexpr bool ALWAYS = V2 && !GUARD && FETCH_ALL;
+        const lmask need = ALWAYS ? ~(lmask)0 : act & ~cached;
+        if (ALWAYS || LM_ON(need)) {
             // GUARD == false: pool below 2^29 nodes (svo_rt.hip), so the byte offset fits
             // 32 bits (global_load saddr + 32-bit voffset, no 64-bit address add).  GUARD: an
             // HLSL-rounded parent index (> 2^24 nodes) may lie outside the pool; it
@@ -677,7 +680,10 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, bool remap) {
     return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / 8;
 }
 
-template <int MODE, bool COUNT, int STEP, int BS>
+// FA: the lean V2 loop's unpredicated node loads (p.fetch_all) -- a separate
+// instantiation, so each form keeps its own register allocation (both loops in
+// one kernel took 82 SGPRs: 7 waves/SIMD, MI355X_MICROARCH.md occupancy table)
+template <int MODE, bool COUNT, int STEP, int BS, bool FA = false>
 __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blocks_x, int remap) {
     // BS = 256: a block is 16x16 pixels (4 waves of 8x8); 128: 16x8 (2 waves); 64: one 8x8 wave.
     extern __shared__ uint2 stk_base[];   // [p.slots + 1][BS]
@@ -716,7 +722,7 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
             else trace_lean<MODE, BS, false, true, STEP == 4>(p, f, stk, &dg);
         }
         else if (p.guard) trace_lean<MODE, BS, true, false, STEP == 4>(p, f, stk);
-        else trace_lean<MODE, BS, false, false, STEP == 4>(p, f, stk);
+        else trace_lean<MODE, BS, false, false, STEP == 4, FA>(p, f, stk);
         from_fray(f, r);
         if (BS == 64 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every lane
         if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
@@ -748,7 +754,7 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
 // P = o + (t / 64) d, origin P + 0.001 n, direction -L.  An occluded pixel gets
 // flag bit 3 and a black Result (:109-111).  Runs over the same 8x8 tiles as
 // the primary pass: sky tiles retire at once, so no compaction pass is needed.
-template <int MODE, int BS>
+template <int MODE, int BS, bool FA = false>
 __global__ __launch_bounds__(BS) void shadow_tile_kernel(LaunchParams p, int blocks_x) {
     extern __shared__ uint2 stk_base[];
     const int tid = threadIdx.x;
@@ -794,7 +800,7 @@ __global__ __launch_bounds__(BS) void shadow_tile_kernel(LaunchParams p, int blo
     FRay f;   // the primary rays' lean loop (one wave of shadow rays per tile, parallel directions)
     to_fray(r, f);
     if (p.guard) trace_lean<MODE, BS, true, false, true>(p, f, stk);
-    else trace_lean<MODE, BS, false, false, true>(p, f, stk);
+    else trace_lean<MODE, BS, false, false, true, FA>(p, f, stk);
     from_fray(f, r);
     if (p.shadow_cost) p.shadow_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every tracing lane
     if (r.scale < S_MAX) {   // occluded
@@ -886,7 +892,10 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
             const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
             const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
             const dim3 grid((unsigned)(bx * by)), block(64);
-            if (p.flat == 4)
+            if (p.flat == 4 && !COUNT && p.fetch_all && !p.guard)
+                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64, true>), grid, block, lds64, stream, p, bx,
+                                   p.xcd_remap);
+            else if (p.flat == 4)
                 hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
             else if (p.flat == 3)
                 hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
@@ -1127,7 +1136,10 @@ template <int MODE>
 static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
     const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
     const size_t lds = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
-    hipLaunchKernelGGL((shadow_tile_kernel<MODE, 64>), dim3((unsigned)(bx * by)), dim3(64), lds, stream, p, bx);
+    if (p.fetch_all && !p.guard)
+        hipLaunchKernelGGL((shadow_tile_kernel<MODE, 64, true>), dim3((unsigned)(bx * by)), dim3(64), lds, stream, p, bx);
+    else
+        hipLaunchKernelGGL((shadow_tile_kernel<MODE, 64>), dim3((unsigned)(bx * by)), dim3(64), lds, stream, p, bx);
     return hipGetLastError();
 }
 

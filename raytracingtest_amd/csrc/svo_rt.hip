@@ -92,6 +92,7 @@ struct svo_ctx {
     int tile_order = 1;              // env SVO_TILE_ORDER=0 disables
     int prio = 1;                    // env SVO_PRIO=0: no issue priority by cost class
     int shadow_order_enabled = 1;    // env SVO_SHADOW_ORDER=0: shadow tiles in plain strip order
+    int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
     int order_every = 8;             // env SVO_ORDER_EVERY: rebuild the order every k-th launch (~20 us one-CU kernel)
     unsigned long long order_launches = 0;
     uint16_t *d_tile_cost = nullptr;
@@ -252,6 +253,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // (and the lean loop's 32-bit node byte offsets need fewer than 2^29 nodes)
     p.guard = !ctx->depth_exact || (stack_mode == 0 && ctx->n_nodes > ((size_t)1 << 24)) ||
               ctx->n_nodes >= ((size_t)1 << 29);
+    // unpredicated node loads pay off on pools below 2^24 nodes (C2, C3: 5-9 %) and
+    // cost 6-12 % on the 25 M / 100 M-node C4 / C5 pools (svo_kernel.hip trace_lean)
+    p.fetch_all = ctx->fetch_all >= 0 ? ctx->fetch_all : (ctx->n_nodes < ((size_t)1 << 24) ? 1 : 0);
     p.hits = reinterpret_cast<svo::Hit *>(d_hits);
     p.rgba = reinterpret_cast<float4 *>(d_rgba);
     p.fetches = d_fetch;
@@ -433,6 +437,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SHADOW_ORDER")) ctx->shadow_order_enabled = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_FETCH_ALL")) ctx->fetch_all = std::atoi(k) != 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_BLOCK")) { const int b = std::atoi(k); ctx->block = (b == 256 || b == 128) ? b : 64; }
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));

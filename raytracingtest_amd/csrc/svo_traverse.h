@@ -62,6 +62,7 @@ struct LaunchParams {
     uint16_t *tile_cost;
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
+    int fetch_all;                // lean loop (!guard): every lane loads its node every trip
     int strip_w;                  // xcd_remap 2: tile columns per super-column
     // The same cost-ordered dispatch for the shadow pass (its own costs and order).
     const uint32_t *shadow_order;
