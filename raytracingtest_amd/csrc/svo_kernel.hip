@@ -1039,7 +1039,8 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
                                                                      uint32_t *__restrict__ order, int n, int tiles_x,
                                                                      int g) {
     __shared__ uint32_t red[ORDER_THREADS / 64];
-    __shared__ uint32_t cnt[4], base[4];
+    constexpr int NC = 6;
+    __shared__ uint32_t cnt[NC], base[NC];
     const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int len = n / 8, tiles_y = n / tiles_x;
     // position e of this XCD's list is (column c = e / tiles_y, row e % tiles_y) of its
@@ -1062,20 +1063,25 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
     if (lane == 0) red[wave] = mx;
-    if (tid < 4) cnt[tid] = 0;
+    if (tid < NC) cnt[tid] = 0;
     __syncthreads();
     mx = 0;
 #pragma unroll
     for (int w = 0; w < ORDER_THREADS / 64; ++w) mx = max(mx, red[w]);
-    auto cls = [mx](uint32_t k) { return 2 * k >= mx ? 0 : 4 * k >= mx ? 1 : 8 * k >= mx ? 2 : 3; };
+    // six classes, the top half split three ways so the very heaviest tiles are the
+    // XCD's first dispatches (they bound the launch); the render kernel's s_setprio
+    // classes are >= 1/2, >= 1/4, >= 1/8 of the XCD's max and the rest
+    auto cls = [mx](uint32_t k) {
+        return 8 * k >= 7 * mx ? 0 : 4 * k >= 3 * mx ? 1 : 2 * k >= mx ? 2 : 4 * k >= mx ? 3 : 8 * k >= mx ? 4 : 5;
+    };
     for (Walk w = start(); w.e < len; next(w)) atomicAdd(&cnt[cls(cost[tile_of(w)])], 1u);
     __syncthreads();
     if (tid == 0) {
         uint32_t run = 0;
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < NC; ++c) {
             base[c] = run;
             run += cnt[c];
-            order[n + 4 + 4 * x + c] = run;
+            if (c >= 2) order[n + 4 + 4 * x + (c - 2)] = run;   // prio class ends
         }
         if (x == 0) for (int c = 0; c < 4; ++c) order[n + c] = 0;   // global bounds unused in this mode
     }
