@@ -592,21 +592,18 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     if (LM_ON(ovf)) r.flags |= 4u;
 }
 
-// N:158-186 hit decode; R:93-127 Shade; R:167 store
-__device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r_in, size_t out) {
-    Ray r = r_in;
-    uint32_t w0, w1, w2, w3, w4, w5;
-    float rgb0, rgb1, rgb2;
+// The hit record words and the Shade colour of a finished ray.
+__device__ __forceinline__ void record(const LaunchParams &p, const Ray &r, uint32_t w[6], float rgb[3]) {
     if (r.scale >= S_MAX) {
-        w0 = 0xFFFFFFFFu;
-        w1 = (r.flags & 0xFFFFu) << 16;
-        w2 = 0x7F800000u;
-        w3 = 0u; w4 = 0u; w5 = 0u;
+        w[0] = 0xFFFFFFFFu;
+        w[1] = (r.flags & 0xFFFFu) << 16;
+        w[2] = 0x7F800000u;
+        w[3] = 0u; w[4] = 0u; w[5] = 0u;
         // procedural sky (the reference's skybox assets are missing), == orc_sky
         const float k = 0.5f * r.dir_y + 0.5f;
-        rgb0 = 0.25f + 0.5f * k;
-        rgb1 = 0.35f + 0.55f * k;
-        rgb2 = 0.6f + 0.4f * k;
+        rgb[0] = 0.25f + 0.5f * k;
+        rgb[1] = 0.35f + 0.55f * k;
+        rgb[2] = 0.6f + 0.4f * k;
     } else {
         const float t_min = r.t_min * 32.0f;
         const int hit_idx = r.idx ^ r.octant_mask ^ 7;
@@ -614,13 +611,13 @@ __device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r_in, s
         float n[3];
         decode_normal(a.y >> 16, n);
         normalize3(n);
-        w0 = r.parent;
-        w1 = (uint32_t)hit_idx | ((uint32_t)r.scale << 8) | (((r.flags | 1u) & 0xFFFFu) << 16);
-        w2 = (uint32_t)__float_as_int(t_min * 64.0f);
-        w3 = (uint32_t)__float_as_int(n[0]);
-        w4 = (uint32_t)__float_as_int(n[1]);
-        w5 = (uint32_t)__float_as_int(n[2]);
-        rgb0 = rgb1 = rgb2 = 0.0f;
+        w[0] = r.parent;
+        w[1] = (uint32_t)hit_idx | ((uint32_t)r.scale << 8) | (((r.flags | 1u) & 0xFFFFu) << 16);
+        w[2] = (uint32_t)__float_as_int(t_min * 64.0f);
+        w[3] = (uint32_t)__float_as_int(n[0]);
+        w[4] = (uint32_t)__float_as_int(n[1]);
+        w[5] = (uint32_t)__float_as_int(n[2]);
+        rgb[0] = rgb[1] = rgb[2] = 0.0f;
         if (p.rgba) {
             float alb[3];
             decode_dxt(a.x, a.y, hit_idx, alb);
@@ -630,16 +627,44 @@ __device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r_in, s
             float s = d * -1.0f;
             s = fminf(fmaxf(s, 0.0f), 1.0f);
             s = s * p.cam.light[3];
-            rgb0 = s * alb[0]; rgb1 = s * alb[1]; rgb2 = s * alb[2];
+            rgb[0] = s * alb[0]; rgb[1] = s * alb[1]; rgb[2] = s * alb[2];
         }
     }
+}
+
+__device__ __forceinline__ void store_record(const LaunchParams &p, size_t out, const uint32_t w[6], const float rgb[3]) {
     if (p.hits) {
         uint2 *dst = reinterpret_cast<uint2 *>(p.hits + out);
-        dst[0] = make_uint2(w0, w1);
-        dst[1] = make_uint2(w2, w3);
-        dst[2] = make_uint2(w4, w5);
+        dst[0] = make_uint2(w[0], w[1]);
+        dst[1] = make_uint2(w[2], w[3]);
+        dst[2] = make_uint2(w[4], w[5]);
     }
-    if (p.rgba) p.rgba[out] = make_float4(rgb0, rgb1, rgb2, 1.0f);
+    if (p.rgba) p.rgba[out] = make_float4(rgb[0], rgb[1], rgb[2], 1.0f);
+}
+
+// N:158-186 hit decode; R:93-127 Shade; R:167 store
+__device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r, size_t out) {
+    uint32_t w[6];
+    float rgb[3];
+    record(p, r, w, rgb);
+    store_record(p, out, w, rgb);
+}
+
+// Shadow ray of a primary hit (the reference's test is commented
+// out at RaytraceCompute.compute:105-112): world hit point P = o + (t / 64) d (t =
+// the record's 2048 t_svo), origin P + 0.001 n, direction -L.  == orc_shadow_ray.
+__device__ __forceinline__ void shadow_ray(const LaunchParams &p, int x, int y, uint32_t w_t, uint32_t w_nx,
+                                           uint32_t w_ny, uint32_t w_nz, float so[3], float sd[3]) {
+    float org[3], dir[3];
+    camera_ray(p, x, y, org, dir);
+    const float tw = __int_as_float((int32_t)w_t) * (1.0f / 64.0f);
+    const float n[3] = { __int_as_float((int32_t)w_nx), __int_as_float((int32_t)w_ny), __int_as_float((int32_t)w_nz) };
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float pk = org[k] + tw * dir[k];
+        so[k] = pk + n[k] * 0.001f;
+        sd[k] = -p.cam.light[k];
+    }
 }
 
 __device__ __forceinline__ int global_row(const LaunchParams &p, int lr) {
@@ -683,7 +708,11 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, bool remap) {
 // FA: the lean V2 loop's unpredicated node loads (p.fetch_all) -- a separate
 // instantiation, so each form keeps its own register allocation (both loops in
 // one kernel took 82 SGPRs: 7 waves/SIMD, MI355X_MICROARCH.md occupancy table)
-template <int MODE, bool COUNT, int STEP, int BS, bool FA = false>
+// SH: the shadow pass fused into the same wave -- after its primary rays the wave
+// traces one shadow ray per hit lane (the separate shadow_tile_kernel's work), and
+// the tile's recorded cost is the sum of both, so one cost-ordered launch balances
+// the whole frame (one ramp and one tail instead of two, no second launch).
+template <int MODE, bool COUNT, int STEP, int BS, bool FA = false, bool SH = false>
 __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blocks_x, int remap) {
     // BS = 256: a block is 16x16 pixels (4 waves of 8x8); 128: 16x8 (2 waves); 64: one 8x8 wave.
     extern __shared__ uint2 stk_base[];   // [p.slots + 1][BS]
@@ -717,13 +746,44 @@ __global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blo
         FRay f;
         to_fray(r, f);
         LeanDiag dg;
-        if (p.wave_log) {
+        if (!SH && p.wave_log) {
             if (p.guard) trace_lean<MODE, BS, true, true, STEP == 4>(p, f, stk, &dg);
             else trace_lean<MODE, BS, false, true, STEP == 4>(p, f, stk, &dg);
         }
         else if (p.guard) trace_lean<MODE, BS, true, false, STEP == 4>(p, f, stk);
         else trace_lean<MODE, BS, false, false, STEP == 4, FA>(p, f, stk);
         from_fray(f, r);
+        if (SH) {
+            const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
+            uint32_t w[6];
+            float rgb[3];
+            record(p, r, w, rgb);
+            const bool hit = r.scale < S_MAX;
+            const uint64_t hits = __ballot(hit);
+            int trips = f.trips;
+            if (hits) {
+                if (hit) {   // exec = the hit lanes: the lean loop's lanes are exactly these
+                    float so[3], sd[3];
+                    shadow_ray(p, x, global_row(p, lr), w[2], w[3], w[4], w[5], so, sd);
+                    Ray rs;
+                    setup_ray(so, sd, rs);
+                    FRay fs;
+                    to_fray(rs, fs);
+                    if (p.guard) trace_lean<MODE, BS, true, false, true>(p, fs, stk);
+                    else trace_lean<MODE, BS, false, false, true, FA>(p, fs, stk);
+                    from_fray(fs, rs);
+                    if (rs.scale < S_MAX) {   // occluded: flag bit 3, black Result (R:109-111)
+                        w[1] |= 8u << 16;
+                        rgb[0] = rgb[1] = rgb[2] = 0.0f;
+                    }
+                    trips += fs.trips;
+                }
+                trips = __shfl(trips, __ffsll((long long)hits) - 1);   // primary + shadow trips of the wave
+            }
+            if (BS == 64 && p.tile_cost && lane == 0) p.tile_cost[t] = (uint16_t)min(trips, 65535);
+            store_record(p, out, w, rgb);
+            return;
+        }
         if (BS == 64 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every lane
         if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
             uint32_t *w = p.wave_log + 8 * ((size_t)blockIdx.x * (BS / 64) + wave);
@@ -783,17 +843,8 @@ __global__ __launch_bounds__(BS) void shadow_tile_kernel(LaunchParams p, int blo
     if (p.shadow_cost && lane == 0 && !any_hit) p.shadow_cost[t] = 0;
     if (!hit) return;
     const uint2 w23 = rec[1], w45 = rec[2];
-    float org[3], dir[3];
-    camera_ray(p, x, global_row(p, lr), org, dir);
-    const float tw = __int_as_float((int32_t)w23.x) * (1.0f / 64.0f);
-    const float n[3] = { __int_as_float((int32_t)w23.y), __int_as_float((int32_t)w45.x), __int_as_float((int32_t)w45.y) };
     float so[3], sd[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float pk = org[k] + tw * dir[k];
-        so[k] = pk + n[k] * 0.001f;
-        sd[k] = -p.cam.light[k];
-    }
+    shadow_ray(p, x, global_row(p, lr), w23.x, w23.y, w45.x, w45.y, so, sd);
     Ray r;
     setup_ray(so, sd, r);
     uint2 *stk = stk_base + tid;
@@ -892,7 +943,14 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int 
             const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
             const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
             const dim3 grid((unsigned)(bx * by)), block(64);
-            if (p.flat == 4 && !COUNT && p.fetch_all && !p.guard)
+            if (p.flat == 4 && !COUNT && p.shadows == 2) {   // shadow pass fused into the primary launch
+                if (p.fetch_all && !p.guard)
+                    hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64, true, true>), grid, block, lds64, stream, p,
+                                       bx, p.xcd_remap);
+                else
+                    hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64, false, true>), grid, block, lds64, stream,
+                                       p, bx, p.xcd_remap);
+            } else if (p.flat == 4 && !COUNT && p.fetch_all && !p.guard)
                 hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64, true>), grid, block, lds64, stream, p, bx,
                                    p.xcd_remap);
             else if (p.flat == 4)
@@ -1163,7 +1221,7 @@ hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stre
                   : launch_variant<1, false>(p, stream, kernel, counter, num_cus);
     if (e != hipSuccess) return e;
     if (primary_end && (e = hipEventRecord(primary_end, stream)) != hipSuccess) return e;
-    if (!count && p.shadows && p.hits) return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
+    if (!count && p.shadows == 1 && p.hits) return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
     return hipSuccess;
 }
 

@@ -93,6 +93,7 @@ struct svo_ctx {
     int prio = 1;                    // env SVO_PRIO=0: no issue priority by cost class
     int shadow_order_enabled = 1;    // env SVO_SHADOW_ORDER=0: shadow tiles in plain strip order
     int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
+    int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
     int order_every = 8;             // env SVO_ORDER_EVERY: rebuild the order every k-th launch (~20 us one-CU kernel)
     unsigned long long order_launches = 0;
     uint16_t *d_tile_cost = nullptr;
@@ -267,8 +268,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.flat = ctx->flat;
     p.block = ctx->block;
     p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? 1 : 0;
+    // fused shadow pass: the 64-thread lean V2 tile kernel with cost ordering (env SVO_FUSED_SHADOWS=0: two passes)
+    if (p.shadows && ctx->fused_shadows && ctx->kernel == 0 && ctx->block == 64 && ctx->flat == 4) p.shadows = 2;
     if (p.local_rows == 0) return SVO_OK;
-    if (p.shadows && !p.hits && !p.fetches) {   // the shadow pass reads the primary hit records
+    if (p.shadows == 1 && !p.hits && !p.fetches) {   // the second shadow pass reads the primary hit records
         int rc2 = ensure_out(ctx, (size_t)p.local_rows * (size_t)width);
         if (rc2) return rc2;
         p.hits = reinterpret_cast<svo::Hit *>(ctx->d_out_hits);
@@ -329,7 +332,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             p.tile_order = ctx->order_key == key ? ctx->d_tile_order : nullptr;
         }
         if (!std::getenv("SVO_ORDER_FILE")) p.tile_cost = ctx->d_tile_cost;
-        if (p.shadows && ctx->shadow_order_enabled) {
+        if (p.shadows == 1 && ctx->shadow_order_enabled) {
             p.shadow_cost = ctx->d_shadow_cost;
             p.shadow_order = ctx->shadow_order_key == key ? ctx->d_shadow_order : nullptr;
         }
@@ -438,6 +441,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SHADOW_ORDER")) ctx->shadow_order_enabled = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_FETCH_ALL")) ctx->fetch_all = std::atoi(k) != 0 ? 1 : 0;
+    if (const char *k = std::getenv("SVO_FUSED_SHADOWS")) ctx->fused_shadows = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_BLOCK")) { const int b = std::atoi(k); ctx->block = (b == 256 || b == 128) ? b : 64; }
     if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));

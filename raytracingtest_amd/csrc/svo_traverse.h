@@ -53,7 +53,7 @@ struct LaunchParams {
     int xcd_remap;        // tile kernel: give each XCD a contiguous screen band
     int flat;             // 1: branch-flattened iteration (default), 0: branchy reference form
     int block;            // tile kernel workgroup size: 64 (one 8x8 wave) or 256 (16x16 pixels)
-    int shadows;          // 1: second pass, one shadow ray per primary hit (needs hits)
+    int shadows;          // one shadow ray per primary hit: 1 = second pass (needs hits), 2 = fused into the primary launch
     uint32_t *wave_log;   // diagnostics (env SVO_WAVE_LOG): per wave {t0, t1, HW_ID, XCC_ID | trips << 8,
                           //   loop cycles, fetch-wait cycles, fetch trips, pop trips} (instrumented loop)
     // Cost-ordered dispatch (64-thread tile kernel): block b traces 8x8 tile

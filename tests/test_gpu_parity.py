@@ -233,6 +233,30 @@ def test_shadow_rays_parity(rm, oracle_mod, mode):
     _compare(hits, rgba, ref_hits, ref_rgba)
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_shadow_pass_forms_identical(oracle_mod, monkeypatch, fused):
+    """The shadow rays as a second cost-ordered launch (SVO_FUSED_SHADOWS=0) and
+    fused into the primary launch (default) give the oracle's frame, over repeated
+    launches (the dispatch order is rebuilt from recorded costs) and with RGBA only."""
+    monkeypatch.setenv("SVO_FUSED_SHADOWS", fused)
+    svo = build_menger(8)
+    cam = overview_camera()
+    w, h = 480, 272
+    ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, svo, cam, w, h, 0, shadows=True)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        m.SetShadowRays(True)
+        for _ in range(10):
+            rgba, hits = m.Render(w, h)
+            _compare(hits, rgba, ref_hits, ref_rgba)
+        rgba, _ = m.Render(w, h, want_hits=False)     # shadows without a caller hit buffer
+        np.testing.assert_allclose(rgba.reshape(-1, 4), ref_rgba, rtol=RTOL, atol=1e-7)
+    finally:
+        m.close()
+
+
 def test_accumulate_matches_oracle(rm, oracle_mod):
     """svo_accumulate (AddShader blend) == the C restatement, bit for bit, over a
     sequence of samples; currentSample advances per blit and resets when the
