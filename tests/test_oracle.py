@@ -1,10 +1,13 @@
 """Pin the CPU oracle: reference fixtures (decode KATs) + independent brute force."""
+import os
+
 import numpy as np
 import pytest
 
 from raytracingtest_amd.camera import main_camera, main_light, overview_camera
 from raytracingtest_amd.svo_data import SVOData
 from tests.bruteforce import entry_exit, first_hits, svo_space_ray
+from tests.conftest import GOLDEN
 
 
 def _cam(oracle_mod, camera, w, h, off=(0.5, 0.5)):
@@ -217,3 +220,21 @@ def test_accumulate_known_answers(oracle_mod):
     for n, f in enumerate(frames):
         oracle_mod.accumulate(acc, np.ascontiguousarray(f), n)
     np.testing.assert_allclose(acc[..., :3], frames[..., :3].mean(0), rtol=1e-5)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("camera_name", ["main", "overview"])
+def test_oracle_reproduces_c1_golden_frames(oracle_mod, text_svo, mode, camera_name):
+    """The oracle's C1 frames (Text SVO, 256x256) are bit-identical to the committed
+    golden vectors (tests/golden/make_c1_golden.py): a compiler, flag or code change
+    that moves any bit of a hit record or Result pixel is caught here."""
+    from raytracingtest_amd.camera import main_camera, main_light, overview_camera
+    z = np.load(os.path.join(GOLDEN, "c1_text_frames.npz"))
+    key = f"{camera_name}_{'hlsl' if mode == 0 else 'exact'}"
+    cam = main_camera() if camera_name == "main" else overview_camera()
+    c2w, inv_proj = cam.uniforms(256, 256)
+    ocam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
+    hits, rgba, _ = oracle_mod.render(oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments),
+                                      ocam, 256, 256, mode)
+    assert hits.tobytes() == z[key + "_hits"].tobytes()
+    assert rgba.astype(np.float32).tobytes() == z[camera_name + "_rgba"].tobytes()
