@@ -367,6 +367,13 @@ __device__ __forceinline__ float vmin(float a, float b) {
     return r;
 }
 
+#ifndef SVO_FMA_CENTER
+#define SVO_FMA_CENTER 1
+#endif
+__device__ __forceinline__ float center(float half, float coef, float corner) {
+    return SVO_FMA_CENTER ? __builtin_fmaf(half, coef, corner) : half * coef + corner;
+}
+
 // 3-bit per-lane integer b0 | b1 << 1 | b2 << 2 from three lane masks.
 __device__ __forceinline__ int lanes_to_idx(uint64_t b0, uint64_t b1, uint64_t b2) {
     // three independent selects + one or: two dependent levels and no SGPR
@@ -474,9 +481,13 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const float tc_max = fminf(fminf(tx, ty), tz);
         const float tv_max = vmin(r.t_max, tc_max);
         const float half = r.sexp * 0.5f;                // N:111-116
-        const lmask cx = LM_OF(half * r.cx + tx > r.t_min);
-        const lmask cy = LM_OF(half * r.cy + ty > r.t_min);
-        const lmask cz = LM_OF(half * r.cz + tz > r.t_min);
+        // tx_center = half * tx_coef + tx_corner (N:111-113) as one fma: half is a power of
+        // two >= 2^-23 and |tx_coef| >= 1, so half * tx_coef is exact (no rounding, no
+        // underflow) and the fused result equals the two-rounding HLSL form bit for bit
+        // (NaN payloads aside, which only meet the comparison)
+        const lmask cx = LM_OF(center(half, r.cx, tx) > r.t_min);
+        const lmask cy = LM_OF(center(half, r.cy, ty) > r.t_min);
+        const lmask cz = LM_OF(center(half, r.cz, tz) > r.t_min);
         const lmask lx = LM_OF(tx <= tc_max), ly = LM_OF(ty <= tc_max), lz = LM_OF(tz <= tc_max);
         const lmask in_span = LM_OF(r.t_min <= tv_max), below_h = LM_OF(tc_max < r.h);
         const uint32_t cm = r.cd16 << sh;                // valid bit -> bit 31, leaf bit -> bit 23
