@@ -1,7 +1,7 @@
 #!/bin/bash
 # Compile-flag A/B of libsvo_rt.so.
 #   build (CPU):  bash tools/ab_lib.sh build NAME [hipcc flags...]   -> build/ab/libsvo_rt_NAME.so
-#   run   (GPU):  bash tools/ab_lib.sh run NAME...                   (two interleaved rounds, one process each)
+#   run   (GPU):  [AB_ARGS="--camera overview"] bash tools/ab_lib.sh run NAME...   (two interleaved rounds, one process each)
 set -o pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 if [ "$1" = build ]; then
@@ -16,7 +16,7 @@ shift
 mkdir -p gpurun_out/ab
 for rep in 1 2; do
   for name in "$@"; do
-    SVO_RT_LIB="$ROOT/build/ab/libsvo_rt_$name.so" timeout -k 10 200 python bench.py --steps 40 --warmup 5 --cpu-seconds 0 \
+    SVO_RT_LIB="$ROOT/build/ab/libsvo_rt_$name.so" timeout -k 10 200 python bench.py --steps 40 --warmup 5 --cpu-seconds 0 $AB_ARGS \
       > gpurun_out/ab/out.json 2>>gpurun_out/ab/err.log || exit $?
     python3 -c "import json; d=json.load(open('gpurun_out/ab/out.json')); print('$name', d['roofline']['kernel_ms'], d['value'], d['roofline']['frac'])"
   done
