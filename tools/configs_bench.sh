@@ -1,9 +1,9 @@
 #!/bin/bash
 # One bench line per BASELINE.json config on one GPU (C4/C5 on ONE GPU here;
-# their 4/8-GPU split is the driver's multi-GPU run).  Usage: bash tools/configs_bench.sh <tag>
+# their 4/8-GPU split is the driver's multi-GPU run).  Usage: [CPU_SECONDS=5] bash tools/configs_bench.sh <tag>
 set -o pipefail
 OUT=gpurun_out/$1; mkdir -p $OUT
 for c in C1 C2 C4 C5; do
-  timeout -k 10 300 python bench.py --config $c --steps 30 --warmup 3 --cpu-seconds 0 > $OUT/config_$c.json 2>> $OUT/configs.err || exit $?
+  timeout -k 10 300 python bench.py --config $c --steps 30 --warmup 3 --cpu-seconds ${CPU_SECONDS:-0} > $OUT/config_$c.json 2>> $OUT/configs.err || exit $?
 done
 echo done
