@@ -449,7 +449,12 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     // per-lane values from here on (works round an LLVM uniformity-analysis bug that
     // otherwise rejects the SGPR trip counter below: "illegal VGPR to SGPR copy")
     if (V2) asm volatile("" : "+v"(r.parent), "+v"(r.cd16), "+v"(r.first));
-    while (act != 0 && it < MAX_ITERS) {   // one exit: the cap is part of the loop test
+    // one exit (no per-trip phi copies), the cap part of the test; a do-while with the
+    // continue mask built in asm (s_cmp + s_cselect, then s_cmp_lg + branch: 4 SALU instead of
+    // the 7 LLVM makes of `act != 0 && it < MAX_ITERS`; kernel -1 to -2 %).  On entry act != 0
+    // (every lane of the wave traces) and it == 0.
+    lmask go;
+    do {
         // wave-uniform trip count kept in an SGPR (LLVM otherwise counts down in a VGPR)
         asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
         // N:60-62.  FETCH_ALL (V2, !GUARD, pools below 2^24 nodes -- svo_rt.hip):
@@ -594,7 +599,8 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         }
         ovf |= of;
         act &= ~(hit | of | out);
-    }
+        asm volatile("s_cmp_lt_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(go) : "s"(it), "n"(MAX_ITERS), "s"(act) : "scc");
+    } while (go != 0);
     capped = act;                          // still tracing after MAX_ITERS trips
     if (DIAG) diag->loop_cycles = __builtin_amdgcn_s_memtime() - tl0;
     r.idx = sh ^ oct;
