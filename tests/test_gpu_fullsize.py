@@ -2,10 +2,8 @@
 
 Each config's SVO is built by the native builder exactly as bench.py builds it,
 rendered on cuda:0 through the C-ABI, and checked against the CPU oracle on the
-same SVO and camera: every ray of the frame for C2-C4, an evenly spread sample
-of full rows for C5 (33 M rays), plus size-independent properties on the whole
-C5 frame (hit records self-consistent, the RGBA frame equal to the shading of
-its own records).  C4/C5 pools exceed 2^24 descriptors and trace in the exact
+same SVO and camera: every ray of the frame for C2-C5 (C5: 33 M rays), plus
+size-independent properties of every frame (hit records self-consistent).  C4/C5 pools exceed 2^24 descriptors and trace in the exact
 stack mode (bench.py CONFIGS); C3 is also checked with the '+1 shadow ray' pass.
 """
 import os
@@ -117,17 +115,16 @@ def test_c3_with_shadow_rays_full_frame(gpu, oracle_mod):
     _assert_same(hits, rgba, ref_hits, ref_rgba, "C3 + shadow rays")
 
 
-def test_c5_rows_parity_and_properties(gpu, oracle_mod):
+def test_c5_full_frame_parity_and_properties(gpu, oracle_mod):
     cfg = CONFIGS["C5"]
     svo = _svo(cfg)
     assert len(svo) > (1 << 24)   # beyond the HLSL float2 stack's exact parent range
     cam = CAMERAS[cfg["camera"]]()
     rgba, hits = _render(svo, cfg, cam)
     _self_consistent(hits, rgba, cfg["max_level"] - 1)
-    w, h = cfg["width"], cfg["height"]
-    ys = np.unique(np.linspace(0, h - 1, 96).astype(np.int64))
-    pix = (ys[:, None] * w + np.arange(w)[None, :]).reshape(-1).astype(np.uint32)
-    ref_rgba, ref_hits = _oracle(oracle_mod, svo, cfg, cam, pixels=pix)
-    assert np.count_nonzero(ref_hits["flags"] & 1) > 1000
-    _assert_same(hits[pix], rgba[pix], ref_hits, ref_rgba, "C5 rows")
+    # every ray of the 7680 x 4320 frame (the oracle traces it in well under a second on
+    # the box's 16 threads; the overview pose is sky-heavy)
+    ref_rgba, ref_hits = _oracle(oracle_mod, svo, cfg, cam)
+    assert np.count_nonzero(ref_hits["flags"] & 1) > 100000
+    _assert_same(hits, rgba, ref_hits, ref_rgba, "C5 full frame")
     _svo_cache.clear()
