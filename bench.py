@@ -10,21 +10,32 @@ IntersectSVO, hit decode, Shade, RGBA + 24-byte hit record written to HBM.
 Inputs (node pool, camera) are resident before the timed region.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one rank per
-GPU, SVO replicated per GPU, each rank traces one full 1920x1080 jittered
-sample per step (_PixelOffset from a seeded sequence, RaytracingMaster.cs:35):
-weak scaling, no data-path collective in the step.  `--split bands` instead
-splits ONE frame into 8-row bands across ranks and gathers the hit records to
-rank 0 over RCCL every step (strong scaling).
+GPU, the SVO replicated per GPU (each rank builds the same bytes on its GPU),
+the frame split into 8-row bands dealt round-robin to the ranks (SURVEY.md
+8(e)), and every step ends with the north-star gather: each rank's RGBA8 band
+payload goes to rank 0 over RCCL (one gather) and rank 0's plugin rebuilds the
+display frame (svo_assemble_frame).  The gather of frame k overlaps the render
+of frame k+1 (two streams, double-buffered payloads).  For C1-C3 the frame is
+the same camera at sqrt(N) times the linear resolution, so every GPU traces
+~1920x1080 rays per step (weak scaling); C4 / C5 keep their configured frame
+(strong scaling over their 4 / 8 GPUs).  Without torchrun, --gpus N > 1 drives
+N GPUs from one process through the plugin's multi-device context (the Unity
+host's form).
 
 roofline: algorithmic bytes per launch = sum over rays of
-  8 * F (8-byte node fetches) + 8 * [hit] (attachment) + 24 (hit record) + 16 (RGBA)
-with F counted per ray by the instrumented kernel; divided by the average
-kernel duration from HIP events on the launch stream.  peak = 8 TB/s HBM.
+  8 * F (8-byte V2 node fetches) + 8 * [hit] (attachment) + 24 (hit record) + 16 (RGBA)
+with F counted per ray by the instrumented kernel; divided by the render
+kernel's mean duration from HIP events on its launch stream.  peak = 8 TB/s HBM.
+The kernel is bound by its dependent node-fetch chain (latency), not by HBM:
+`bound` says so and `hbm_frac` gives the PMC-measured fabric bytes' fraction.
 cpu_baseline: the strict-IEEE C oracle (oracle/, "port") on the host cores.
 """
 import argparse
 import json
+import math
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -34,23 +45,26 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+L2_PEAK_GBS = 34500.0        # MI355X_MICROARCH.md "L2 (per XCD)": aggregate L2 bandwidth
 METRIC = "Mrays/sec + achieved HBM GB/s, 1920x1080 primary rays, depth-10 SVO"
 
 
 # BASELINE.json configs; C3 is the metric's workload.  C1-C3
 # trace in the HLSL stack mode, C4-C5 (> 2^24 nodes) in the exact one.
+# gpus: the GPU count the config is defined on (C4: 4, C5: 8); per-GPU configs
+# (gpus 1) scale their frame with the GPU count (weak scaling).
 CONFIGS = {
-    "C1": dict(width=256, height=256, max_level=7, sampler=4, camera="main", svo="sampler", stack_mode=0),
-    "C2": dict(width=1920, height=1080, max_level=9, sampler=-1, camera="overview", svo="menger", stack_mode=0),
-    "C3": dict(width=1920, height=1080, max_level=11, sampler=4, camera="flyover", svo="sampler", stack_mode=0),
-    "C4": dict(width=3840, height=2160, max_level=13, sampler=4, camera="overview", svo="sampler", stack_mode=1),
-    "C5": dict(width=7680, height=4320, max_level=14, sampler=4, camera="overview", svo="sampler", stack_mode=1),
+    "C1": dict(width=256, height=256, max_level=7, sampler=4, camera="main", svo="sampler", stack_mode=0, gpus=1),
+    "C2": dict(width=1920, height=1080, max_level=9, sampler=-1, camera="overview", svo="menger", stack_mode=0, gpus=1),
+    "C3": dict(width=1920, height=1080, max_level=11, sampler=4, camera="flyover", svo="sampler", stack_mode=0, gpus=1),
+    "C4": dict(width=3840, height=2160, max_level=13, sampler=4, camera="overview", svo="sampler", stack_mode=1, gpus=4),
+    "C5": dict(width=7680, height=4320, max_level=14, sampler=4, camera="overview", svo="sampler", stack_mode=1, gpus=8),
 }
 
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--gpus", type=int, default=None, help="GPUs (default: WORLD_SIZE under torchrun, else 1)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", choices=sorted(CONFIGS), default="C3",
@@ -60,46 +74,95 @@ def parse():
     p.add_argument("--max-level", type=int, default=None, help="NaiveCreator maxLevel (depth + 1)")
     p.add_argument("--sampler", type=int, default=None, help="SampleFunctions.Type (4 = Custom1)")
     p.add_argument("--stack-mode", type=int, default=None, help="0 = HLSL float2 stack, 1 = exact")
-    p.add_argument("--split", choices=["samples", "bands"], default="samples")
+    p.add_argument("--frame-scaling", choices=["weak", "strong"], default=None,
+                   help="N > 1: weak = frame grows with N (default for C1-C3), strong = configured frame")
+    p.add_argument("--payload", choices=["rgba8", "compact"], default="rgba8",
+                   help="N > 1: what moves to the display rank: RGBA8 display words (4 B/px) or compact "
+                        "records (12 B/px, rank 0 rebuilds hit records + Result)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--no-rgba", action="store_true")
-    p.add_argument("--camera", choices=["flyover", "overview", "main"], default=None)
+    p.add_argument("--camera", choices=["flyover", "overview", "main", "terrain"], default=None)
     p.add_argument("--shadows", action="store_true", help="C3 '+1 shadow ray' pass after the primary rays")
-    p.add_argument("--accumulate", action="store_true",
-                   help="samples mode: all-reduce the RGBA samples (progressive accumulation) every step")
+    p.add_argument("--extra-poses", action="store_true",
+                   help="N = 1: also time the frame from the other camera poses (reported beside value)")
     a = p.parse_args()
     cfg = CONFIGS[a.config]
     for k in ("width", "height", "max_level", "sampler", "camera", "stack_mode"):
         if getattr(a, k) is None:
             setattr(a, k, cfg[k])
     a.svo = cfg["svo"]
+    a.cfg_gpus = cfg["gpus"]
     return a
+
+
+def host_cpu_info():
+    """CPU model, sockets, logical CPUs and the CPUs this job may use (affinity
+    and cgroup quota): the cpu_baseline runs on all of the latter."""
+    info = {"model": platform.processor() or None, "logical_cpus": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "Model name":
+                info["model"] = v
+            elif k == "Socket(s)":
+                info["sockets"] = int(v)
+            elif k == "Core(s) per socket":
+                info["cores_per_socket"] = int(v)
+            elif k == "Thread(s) per core":
+                info["threads_per_core"] = int(v)
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    avail = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    info["affinity_cpus"] = avail
+    info["cgroup_cpu_quota"] = quota
+    info["usable_cpus"] = max(1, min(avail, int(math.floor(quota)) if quota else avail))
+    return info
 
 
 def main():
     args = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is None:
+        args.gpus = world_env
+    if world_env > 1 and args.gpus != world_env:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but torchrun started WORLD_SIZE={world_env} ranks")
+    mode = "ranks" if world_env > 1 else ("multidevice" if args.gpus > 1 else "single")
     import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if torch.cuda.device_count() < (args.gpus if mode == "multidevice" else 1):
+        raise SystemExit(f"bench.py: {args.gpus} GPUs requested, {torch.cuda.device_count()} visible")
+    world = args.gpus
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one rank per GPU over RCCL; SVO_BENCH_BACKEND=gloo + ranks sharing a GPU is
-    # only for rehearsing the N>1 plumbing on a one-GPU box
-    backend = os.environ.get("SVO_BENCH_BACKEND", "nccl")
+    import torch.distributed as dist
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
-    if world > 1:
+    if mode == "ranks":
+        # one rank per GPU over RCCL; SVO_BENCH_BACKEND=gloo + ranks sharing a GPU is
+        # only for rehearsing the N>1 plumbing on a one-GPU box
+        backend = os.environ.get("SVO_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
 
-    from raytracingtest_amd import RaytracingMaster, band_rows
-    from raytracingtest_amd.camera import CAMERAS, jitter_offsets
+    from raytracingtest_amd import RaytracingMaster, _lib
+    from raytracingtest_amd import distributed as D
+    from raytracingtest_amd.camera import CAMERAS
     from raytracingtest_amd.native_builder import build_sampler_svo
 
     W, H = args.width, args.height
+    scaling = args.frame_scaling or ("weak" if args.cfg_gpus == 1 else "strong")
+    if world > 1 and scaling == "weak":
+        W, H = D.weak_frame(W, H, world)
     t0 = time.time()
     if args.svo == "menger":   # SURVEY.md 8(d) C2: 256^3 Menger sponge surface voxels
         from raytracingtest_amd.builder import build_menger
@@ -108,40 +171,36 @@ def main():
         svo = build_sampler_svo(args.sampler, args.max_level, device=dev.index)
     build_s = time.time() - t0
     n_nodes = len(svo)
+    cam = CAMERAS[args.camera]()
+
+    if mode == "multidevice":
+        return bench_multidevice(args, svo, cam, W, H, scaling, build_s)
 
     rm = RaytracingMaster(device=dev.index, capacity_nodes=n_nodes)
     rm.SetSVOBuffer(svo)
-    cam = CAMERAS[args.camera]()
-    if args.split == "samples":
-        off = (0.5, 0.5) if rank == 0 else tuple(float(v) for v in jitter_offsets(world)[rank])
-        band = None
-        rows = H
-    else:
-        off = (0.5, 0.5)
-        band = (8, rank, world)
-        rows = len(band_rows(H, band))   # == D.rank_band(rank, world)
-    rm.UpdateShaderParameters(cam, W, H, pixel_offset=off)
+    rm.UpdateShaderParameters(cam, W, H)
     if args.shadows:
         rm.SetShadowRays(True)
-
+    band = D.rank_band(rank, world) if world > 1 else None
+    rows = D.band_len(H, rank, world) if world > 1 else H
     n_px = W * rows
+
     hits = torch.empty(n_px * 24, dtype=torch.uint8, device=dev)
     rgba = None if args.no_rgba else torch.empty(n_px * 4, dtype=torch.float32, device=dev)
     # a dedicated (non-null) stream: the kernel and the timing events share it
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
-    from raytracingtest_amd import distributed as D
-    gather = args.split == "bands" and world > 1
-    accumulate = args.split == "samples" and args.accumulate and world > 1 and rgba is not None
+    gather = None
+    if world > 1:
+        gather = Gather(rm, W, H, rank, world, dev, args.payload, stream)
 
     def step():
-        rm.render_device(W, H, rgba_ptr=None if rgba is None else rgba.data_ptr(), hits_ptr=hits.data_ptr(),
-                         stack_mode=args.stack_mode, band=band, stream=sptr)
-        if gather:       # hit-record bands -> every rank (RCCL all_gather over xGMI)
-            D.gather_bands(hits, H, W, world, rank, 24, dist=dist)
-        if accumulate:   # AddShader progressive accumulation across the ranks' samples
-            D.accumulate_samples(rgba, world, dist=dist)
+        if gather is None:
+            rm.render_device(W, H, rgba_ptr=None if rgba is None else rgba.data_ptr(), hits_ptr=hits.data_ptr(),
+                             stack_mode=args.stack_mode, stream=sptr)
+        else:
+            gather.step(hits, rgba, args.stack_mode)
 
     # instrumented pass (outside the timed region): per-ray fetch counts
     fetch = torch.zeros(n_px, dtype=torch.int32, device=dev)
@@ -149,16 +208,18 @@ def main():
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize(dev)
-    host_hits = hits.cpu().numpy().view(np.dtype([("parent", "<u4"), ("hit_idx", "u1"), ("hit_scale", "u1"),
-                                                  ("flags", "<u2"), ("t", "<f4"), ("nx", "<f4"), ("ny", "<f4"),
-                                                  ("nz", "<f4")]))
+    host_hits = hits.cpu().numpy().view(_lib.HIT_DTYPE)
     n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
     F = int(fetch.to(torch.int64).sum().item())
     bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if rgba is None else 16 * n_px)
+    if gather is not None:
+        bytes_per_launch += 4 * n_px   # the RGBA8 (or 12-B compact) band payload the kernel also writes
+        if args.payload == "compact":
+            bytes_per_launch += 8 * n_px
 
     # timed region: K steps between barrier + synchronize.  HIP events around each
     # step only with SVO_STEP_EVENTS=1 (diagnostics): their stream markers add
-    # ~8 us to every step they bracket (measured 0.1265 vs 0.1182 ms per step)
+    # ~8 us to every step they bracket
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -187,14 +248,21 @@ def main():
         step()
     kern_ms, n_timed = rm.kernel_time()
     rm.set_kernel_timing(False)
+    torch.cuda.synchronize(dev)
     if n_timed != args.steps:
         raise RuntimeError(f"kernel timing: {n_timed} launches recorded, {args.steps} expected")
+    stages = gather.stage_times(hits, rgba, args.stack_mode, max(3, args.steps // 2)) if gather else None
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
+        per_rank = [torch.zeros(3, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(per_rank, torch.tensor([kern_ms, stages["gather_ms"], stages["assemble_ms"]],
+                                               dtype=torch.float64, device=dev))
+        per_rank = [[round(float(v), 4) for v in t.tolist()] for t in per_rank]
     else:
         kern_ms_max = kern_ms
+        per_rank = None
 
     # C3's '+1 shadow ray' (BASELINE.json configs[2]): the same frame with the
     # shadow pass, timed separately on one GPU (reported beside, not as `value`)
@@ -215,20 +283,26 @@ def main():
                   "Mrays_per_s": round((n_px + n_hit) / (sh_ms * 1e-3) / 1e6, 2),
                   "note": "primary pass + one shadow ray per primary hit (RaytraceCompute.compute:105-112), "
                           "whole step on the host clock between synchronizes, like value"}
+    poses = None
+    if world == 1 and args.extra_poses and args.svo != "menger":
+        poses = extra_poses(rm, args, W, H, hits, rgba, sptr, dev)
 
-    rays_per_step = n_px * world
+    rays_per_step = W * H
     ms_per_step = elapsed / args.steps * 1e3
     mrays = rays_per_step / (ms_per_step * 1e-3) / 1e6
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
 
     if rank == 0:
-        cpu = cpu_baseline(args, svo, cam, off, host_hits) if (world == 1 and args.cpu_seconds > 0) else None
+        cpu = cpu_baseline(args, svo, cam, host_hits) if (world == 1 and args.cpu_seconds > 0) else None
         kind = "Menger" if args.svo == "menger" else "Custom1"
         workload = (f"{args.config} depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) {kind} SVO, "
                     f"{W}x{H} primary rays" + (" + 1 shadow ray per hit" if args.shadows else "") +
                     f", {args.camera} camera")
-        # the committed PMC figure is per launch of the full-frame workload (not a band of it)
-        traffic = pmc_traffic(workload) if band is None else None
+        from raytracingtest_amd.build import source_digest
+        digest = source_digest()
+        pmc = pmc_traffic(workload, digest) if band is None else None
+        traffic = pmc["hbm_bytes_per_launch"] if pmc else None
+        par = "single" if world == 1 else f"bands{world}x8rows+rccl_gather({args.payload})"
         out = {
             "metric": METRIC,
             "value": round(mrays, 2),
@@ -238,7 +312,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak" if args.split == "samples" else "strong",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": ("synthetic: 256^3 Menger sponge surface SVO (SURVEY.md 8(d) C2)" if args.svo == "menger" else
@@ -246,49 +320,245 @@ def main():
             "config": {"workload": workload,
                        "svo_nodes": n_nodes, "svo_format": "V%d" % svo.format, "svo_leaves": getattr(svo, "n_leaves", None),
                        "build_s": round(build_s, 2), "stack_mode": "hlsl" if args.stack_mode == 0 else "exact",
-                       "rays_per_gpu_step": n_px, "hit_fraction": round(n_hit / n_px, 4),
-                       "fetches_per_ray": round(F / n_px, 3), "parallelism": f"{args.split}{world}" + ("+allreduce" if accumulate else "") + ("+allgather" if gather else "")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "rays_per_step": rays_per_step, "rays_per_gpu_step": n_px,
+                       "hit_fraction_rank0": round(n_hit / n_px, 4),
+                       "fetches_per_ray_rank0": round(F / n_px, 3), "parallelism": par},
+            "roofline": {"bound": "latency", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
+                         "hbm_frac": None if traffic is None else round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                         "l2_frac": round(achieved / L2_PEAK_GBS, 5),
                          "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
-                         "kernel": "render_tile_kernel (primary rays; library HIP events around that kernel alone, K steps after the timed region)",
+                         "kernel": "render_tile_kernel (primary rays; library HIP events around that kernel alone, "
+                                   "K steps after the timed region)",
+                         "bound_note": "dependent node-fetch chain at 8 waves/SIMD (DESIGN.md 5.1); frac is the "
+                                       "metric's algorithmic-bytes fraction of HBM peak, hbm_frac the PMC fabric "
+                                       "bytes' (FETCH_SIZE x2 + WRITE_SIZE), l2_frac algorithmic bytes vs L2 peak",
                          "step_ms_events": None if step_ms is None else round(step_ms, 4),
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "bytes_formula": "8*F + 8*hits + 24*rays + 16*rays(rgba)" +
-                                          (" (primary pass only; kernel_ms covers both passes)" if args.shadows else "")},
+                                          (" + payload" if world > 1 else "") +
+                                          " (8 = the V2 node width; 4-byte reference descriptors would give 4*F)" +
+                                          (" (primary pass only; kernel_ms covers both passes)" if args.shadows else ""),
+                         "kernel_source_sha1": digest,
+                         "traffic_source": None if pmc is None else pmc.get("source")},
             "cpu_baseline": cpu,
             "c3_plus_shadow_ray": shadow,
         }
+        if world > 1:
+            out["multi_gpu"] = {
+                "frame": f"{W}x{H}", "band_rows": 8, "payload": args.payload,
+                "per_rank_kernel_gather_assemble_ms": per_rank,
+                "render_only_Mrays": round(rays_per_step / (kern_ms_max * 1e-3) / 1e6, 2),
+                "gather_ms_rank0": round(stages["gather_ms"], 4), "assemble_ms_rank0": round(stages["assemble_ms"], 4),
+                "payload_bytes_per_rank": stages["payload_bytes"],
+                "note": "value overlaps the gather of frame k with the render of frame k+1; render_only_Mrays is "
+                        "the frame's rays over the slowest rank's render kernel alone; gather/assemble from a "
+                        "serialized pass (events on the gather stream)"}
+        if poses:
+            out["extra_poses"] = poses
         print(json.dumps(out), flush=True)
     rm.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def pmc_traffic(workload):
-    """HBM bytes per launch of the render kernel from the committed rocprofv3 PMC
-    summary (profiles/pmc_summary.json, tools/pmc_summary.py) when it was taken
-    on this same workload, else None."""
+class Gather:
+    """One rank's render + gather + assemble pipeline (bench's N > 1 step).
+
+    Render on the caller's stream R into the rank's band buffers and a
+    double-buffered payload; gather stream G waits for it, gathers the payloads
+    to rank 0 over RCCL and rank 0 rebuilds the frame; the next render into the
+    same payload slot waits for that gather (two frames in flight)."""
+
+    def __init__(self, rm, W, H, rank, world, dev, payload, stream):
+        import torch
+        from raytracingtest_amd import _lib
+        from raytracingtest_amd import distributed as D
+        self.torch, self._lib, self.D = torch, _lib, D
+        self.rm, self.W, self.H, self.rank, self.world, self.dev = rm, W, H, rank, world, dev
+        self.payload = payload
+        self.band = D.rank_band(rank, world)
+        self.elem = 4 if payload == "rgba8" else 12
+        per = D.max_band_len(H, world) * W * self.elem // 4
+        self.R = stream
+        self.G = torch.cuda.Stream(dev)
+        self.send = [torch.zeros(per, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.parts = [[torch.empty(per, dtype=torch.int32, device=dev) for _ in range(world)] if rank == 0 else None
+                      for _ in range(2)]
+        self.frame8 = torch.empty(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
+        self.frame_hits = torch.empty(W * H * 24, dtype=torch.uint8, device=dev) if rank == 0 and payload == "compact" else None
+        self.frame_rgba = torch.empty(W * H * 4, dtype=torch.float32, device=dev) if rank == 0 and payload == "compact" else None
+        self.ev_r = [torch.cuda.Event() for _ in range(2)]
+        self.ev_g = [torch.cuda.Event() for _ in range(2)]
+        self.used = [False, False]
+        self.k = 0
+        self.payload_bytes = D.band_len(H, rank, world) * W * self.elem
+
+    def render(self, k, hits, rgba, stack_mode):
+        if self.used[k]:
+            self.R.wait_event(self.ev_g[k])
+        ptr = self.send[k].data_ptr()
+        self.rm.render_frame(self.W, self.H, hits=hits.data_ptr(), rgba=None if rgba is None else rgba.data_ptr(),
+                             rgba8=ptr if self.payload == "rgba8" else None,
+                             compact=ptr if self.payload == "compact" else None,
+                             stack_mode=stack_mode, band=self.band, stream=self.R.cuda_stream)
+        self.ev_r[k].record(self.R)
+
+    def gather(self, k):
+        self.G.wait_event(self.ev_r[k])
+        with self.torch.cuda.stream(self.G):
+            self.D.gather_parts(self.send[k], self.parts[k], dst=0)
+
+    def assemble(self, k):
+        if self.rank != 0:
+            return
+        ptrs = [p.data_ptr() for p in self.parts[k]]
+        if self.payload == "rgba8":
+            self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_RGBA8, rgba8=self.frame8.data_ptr(),
+                                   stream=self.G.cuda_stream)
+        else:
+            self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_COMPACT, hits=self.frame_hits.data_ptr(),
+                                   rgba=self.frame_rgba.data_ptr(), rgba8=self.frame8.data_ptr(),
+                                   stream=self.G.cuda_stream)
+
+    def step(self, hits, rgba, stack_mode):
+        k = self.k
+        self.k ^= 1
+        self.render(k, hits, rgba, stack_mode)
+        self.gather(k)
+        self.assemble(k)
+        self.ev_g[k].record(self.G)
+        self.used[k] = True
+
+    def stage_times(self, hits, rgba, stack_mode, n):
+        """Serialized render -> gather -> assemble, events on the gather stream."""
+        torch = self.torch
+        g_ms, a_ms = [], []
+        for _ in range(n):
+            torch.cuda.synchronize(self.dev)
+            self.render(0, hits, rgba, stack_mode)
+            self.R.synchronize()
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(self.G)
+            self.gather(0)
+            e1.record(self.G)
+            self.assemble(0)
+            e2.record(self.G)
+            self.ev_g[0].record(self.G)
+            self.used[0] = True
+            self.G.synchronize()
+            g_ms.append(e0.elapsed_time(e1))
+            a_ms.append(e1.elapsed_time(e2))
+        return {"gather_ms": float(np.median(g_ms)), "assemble_ms": float(np.median(a_ms)),
+                "payload_bytes": self.payload_bytes}
+
+
+def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
+    """One process, N GPUs through the plugin's multi-device context (the Unity
+    host's form): the display frame (RGBA8) of W x H rays per step on device 0."""
+    import torch
+    from raytracingtest_amd import RaytracingMaster
+    n = args.gpus
+    rm = RaytracingMaster(devices=list(range(n)), capacity_nodes=len(svo))
+    rm.SetSVOBuffer(svo)
+    rm.UpdateShaderParameters(cam, W, H)
+    dev0 = torch.device("cuda", 0)
+    frame8 = torch.empty(W * H, dtype=torch.int32, device=dev0)
+    s = torch.cuda.Stream(dev0)
+
+    def step():
+        rm.render_frame(W, H, rgba8=frame8.data_ptr(), layout=1, stack_mode=args.stack_mode, stream=s.cuda_stream)
+
+    def sync_all():
+        for d in range(n):
+            torch.cuda.synchronize(d)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    sync_all()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync_all()
+    elapsed = time.perf_counter() - t
+    rm.set_kernel_timing(True)
+    rm.stage_time(0)
+    rm.stage_time(1)
+    for _ in range(args.steps):
+        step()
+    sync_all()
+    kern = [rm.member(i).kernel_time()[0] for i in range(n)]
+    asm_ms = rm.stage_time(1)[0]
+    rm.close()
+    ms = elapsed / args.steps * 1e3
+    print(json.dumps({
+        "metric": METRIC, "value": round(W * H / (ms * 1e-3) / 1e6, 2), "unit": "Mrays/s", "n_gpus": n,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement",
+        "config": {"workload": f"{args.config} {W}x{H} primary rays, {args.camera} camera, display RGBA8 frame",
+                   "parallelism": f"multidevice{n}x8rows+xgmi_pull", "build_s": round(build_s, 2)},
+        "multi_gpu": {"per_device_kernel_ms": [round(k, 4) for k in kern], "assemble_ms": round(asm_ms, 4)},
+    }), flush=True)
+
+
+def extra_poses(rm, args, W, H, hits, rgba, sptr, dev):
+    """Kernel time and ray rate of the same frame from the other camera poses
+    (overview and the Main.unity pose; plus a terrain-facing one)."""
+    import torch
+    from raytracingtest_amd.camera import CAMERAS
+    out = {}
+    for name in ("overview", "main", "terrain", "flyover"):
+        if name == args.camera:
+            continue
+        rm.UpdateShaderParameters(CAMERAS[name](), W, H)
+        for _ in range(10):
+            rm.render_device(W, H, rgba_ptr=None if rgba is None else rgba.data_ptr(), hits_ptr=hits.data_ptr(),
+                             stack_mode=args.stack_mode, stream=sptr)
+        rm.set_kernel_timing(True)
+        rm.kernel_time()
+        for _ in range(20):
+            rm.render_device(W, H, rgba_ptr=None if rgba is None else rgba.data_ptr(), hits_ptr=hits.data_ptr(),
+                             stack_mode=args.stack_mode, stream=sptr)
+        ms, _ = rm.kernel_time()
+        rm.set_kernel_timing(False)
+        torch.cuda.synchronize(dev)
+        h = hits.cpu().numpy().view(np.dtype([("parent", "<u4"), ("m", "<u4"), ("r", "<u4", 4)]))
+        hit_frac = float(np.count_nonzero((h["m"] >> 16) & 1)) / (W * H)
+        out[name] = {"kernel_ms": round(ms, 4), "Mrays_per_s_kernel": round(W * H / (ms * 1e-3) / 1e6, 1),
+                     "hit_fraction": round(hit_frac, 4)}
+    rm.UpdateShaderParameters(CAMERAS[args.camera](), W, H)
+    return out
+
+
+def pmc_traffic(workload, digest):
+    """The committed rocprofv3 PMC summary (profiles/pmc_summary.json,
+    tools/pmc_summary.py) when it was taken on this workload AND this kernel
+    build (source digest), else None."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
         return None
-    return d.get("hbm_bytes_per_launch") if d.get("workload") == workload else None
+    if d.get("workload") != workload or d.get("kernel_source_sha1") != digest:
+        return None
+    return d
 
 
-def cpu_baseline(args, svo, cam, off, gpu_hits):
-    """Oracle ("port") on the host cores over rows of the same frame, bounded by
-    --cpu-seconds; the rows it traces are also compared with the GPU records."""
+def cpu_baseline(args, svo, cam, gpu_hits):
+    """Oracle ("port") on every CPU this job may use, over rows of the same
+    frame, bounded by --cpu-seconds; the rows it traces are also compared with
+    the GPU records.  Plus a 1-thread figure."""
     from oracle import oracle as orc
     from raytracingtest_amd.camera import main_light
 
     W, H = args.width, args.height
-    threads = min(16, os.cpu_count() or 1)
+    info = host_cpu_info()
+    threads = info["usable_cpus"]
     c2w, inv_proj = cam.uniforms(W, H)
-    ocam = orc.make_camera(c2w, inv_proj, off, main_light())
+    ocam = orc.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
     osvo = orc.OracleSVO(nodes=svo.to_v2(), attachments=svo.attachments)
     # calibrate on 8 rows spread over the frame, then a bounded number of rows;
     # a frame that takes less than the budget is traced repeatedly
@@ -317,8 +587,9 @@ def cpu_baseline(args, svo, cam, off, gpu_hits):
     one_core = len(pix1) / (time.perf_counter() - t) / 1e6
     return {"value": round(reps * len(pix) / secs / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{len(ys)} full rows ({len(pix)} rays) spread over the same {W}x{H} frame x {reps} passes, "
-                      f"{threads} threads, {secs:.1f} s; 1-thread rate on 8 rows: {one_core:.3f} Mrays/s",
-            "one_core_mrays": round(one_core, 4),
+                      f"{threads} threads (every CPU this job may use: affinity {info['affinity_cpus']}, cgroup quota "
+                      f"{info['cgroup_cpu_quota']}), {secs:.1f} s; 1-thread rate on 8 rows: {one_core:.3f} Mrays/s",
+            "one_core_mrays": round(one_core, 4), "host": info,
             "parity_rays_checked": int(len(pix)), "parity_rays_mismatched": mism}
 
 

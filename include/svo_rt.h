@@ -48,6 +48,16 @@ typedef struct svo_hit {
     float    nx, ny, nz; /* normalize(decodeNormal(att[2*parent+1] >> 16)) (:177-182) */
 } svo_hit;
 
+/* Compact per-pixel record, 12 bytes = the first 12 bytes of svo_hit: what moves
+ * between devices when a frame is split.  The display device rebuilds the normal
+ * and the Result colour from it with its own SVO replica and camera (the normal
+ * is a function of `parent` alone, NVIDIASVO.compute:177-182). */
+typedef struct svo_hit_compact {
+    uint32_t parent;
+    uint32_t meta;       /* hit_idx | hit_scale << 8 | flags << 16 (svo_hit bytes 4..7) */
+    float    t;
+} svo_hit_compact;
+
 /* Row split of one frame across ranks/GPUs: rows are grouped in bands of
  * `band_rows`; band b belongs to rank b % band_count.  A rank's output holds
  * only its own rows, in increasing y.  {1, 0, 1} (or NULL) = whole frame. */
@@ -57,10 +67,44 @@ typedef struct svo_band {
     int band_count;
 } svo_band;
 
+/* Every per-pixel output of one render (device pointers on the context's
+ * device, each nullable).  layout SVO_LAYOUT_BAND: buffers hold only the rows of
+ * the render's band, in increasing y (the whole frame without a band);
+ * SVO_LAYOUT_FRAME: full-frame buffers, this band's rows written in place. */
+enum { SVO_LAYOUT_BAND = 0, SVO_LAYOUT_FRAME = 1 };
+typedef struct svo_frame {
+    svo_hit *hits;             /* 24-byte hit records */
+    float *rgba;               /* RGBA32F Result (RaytraceCompute.compute:167) */
+    uint32_t *rgba8;           /* display RGBA8: R | G << 8 | B << 16 | 255 << 24, each
+                                  channel (uint)(saturate(c) * 255 + 0.5) */
+    svo_hit_compact *compact;  /* 12-byte records */
+    float *position;           /* float4 per pixel: bestHit.position (NVIDIASVO.compute:165-174),
+                                  w = 0; misses 0 (CreateRayHit, RaytraceCompute.compute:33-41) */
+    uint64_t *voxel;           /* voxel key x | y << 21 | z << 42 of the hit leaf (integer voxel
+                                  coordinates at the leaf scale, un-mirrored; unique for depth <= 21);
+                                  misses all ones */
+    int layout;
+} svo_frame;
+
 /* ~ RaytracingMaster.InitializeSVOBuffer (RaytracingMaster.cs:111-116):
  * allocate a node pool of `capacity_nodes` descriptors (+2 attachment words
  * each) on HIP device `device`. */
 int svo_create(int device, size_t capacity_nodes, svo_ctx **out);
+
+/* Multi-device context (north star: the image sharded into screen bands over
+ * the GPUs of one node, the SVO replicated per GPU, the bands gathered to the
+ * display GPU over xGMI).  devices[0] is the display device; the same index may
+ * repeat (one GPU then renders several members' bands: the test form).  Every
+ * other entry point accepts the result: uploads and camera go to every device;
+ * svo_render / svo_render_device / svo_render_frame render the whole frame in
+ * `band_rows`-row bands dealt round-robin over the devices and leave it on
+ * devices[0] (outputs are devices[0] pointers, frame layout).  The reference
+ * dispatches one grid over the whole frame (RaytracingMaster.cs:66-68). */
+int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes, int band_rows, svo_ctx **out);
+int svo_num_devices(svo_ctx *ctx, int *num_devices);
+/* The per-device context `index` of a multi-device context (the context itself
+ * for index 0 of a single-device one): owned by the group, not destroyed alone. */
+int svo_get_member(svo_ctx *ctx, int index, svo_ctx **member);
 
 /* ~ RaytracingMaster.SetSVOBuffer(RT.SVOData data, int offset)
  * (RaytracingMaster.cs:118-135, CompactSVO.cs:22-35): upload `n_desc` reference
@@ -96,6 +140,25 @@ int svo_render(svo_ctx *ctx, int width, int height, int stack_mode,
 int svo_render_device(svo_ctx *ctx, int width, int height, int stack_mode,
                       const svo_band *band, void *d_rgba, void *d_hits, void *stream);
 
+/* General render: every output of svo_frame, for the rows of `band` (NULL = the
+ * whole frame; a multi-device context requires NULL).  Asynchronous. */
+int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band,
+                     const svo_frame *frame, void *stream);
+
+/* Rebuild a split frame on this context's device from its band parts: part m
+ * holds the rows of bands b with b % n_parts == m (svo_band {band_rows, m,
+ * n_parts}), band layout, as svo_hit_compact records (SVO_PART_COMPACT: frame
+ * outputs hits / rgba / rgba8 / compact, the normal and colour rebuilt from this
+ * context's SVO replica and camera) or RGBA8 words (SVO_PART_RGBA8: frame output
+ * rgba8 only).  Part pointers must be readable from this device (its own memory,
+ * or a peer's with peer access).  skip_part (or -1): a part already rendered in
+ * place.  `frame` must use the frame layout.  This is the display-side half of
+ * the one-process-per-GPU split (parts received over RCCL); multi-device
+ * contexts use it internally.  Asynchronous. */
+enum { SVO_PART_COMPACT = 0, SVO_PART_RGBA8 = 1 };
+int svo_assemble_frame(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, const void *const *parts,
+                       int part_format, int skip_part, const svo_frame *frame, void *stream);
+
 /* Instrumented trace: per-ray descriptor-fetch counts (device uint32 array,
  * NVIDIASVO.compute:60-62 executions), used for the algorithmic-bytes figure
  * of the roofline.  Same arguments as svo_render_device plus d_fetches. */
@@ -117,6 +180,10 @@ int svo_set_options(svo_ctx *ctx, uint32_t options);
  * forgets them.  Measurement only (bench.py's roofline); no reference
  * counterpart. */
 int svo_kernel_time(svo_ctx *ctx, double *mean_ms, uint64_t *launches);
+/* The same for a stage: SVO_STAGE_KERNEL (= svo_kernel_time) or SVO_STAGE_ASSEMBLE
+ * (the assemble kernel of svo_assemble_frame / a multi-device frame). */
+enum { SVO_STAGE_KERNEL = 0, SVO_STAGE_ASSEMBLE = 1 };
+int svo_stage_time(svo_ctx *ctx, int stage, double *mean_ms, uint64_t *launches);
 
 /* ~ Graphics.Blit(Result, destination, AddMaterial) with _Sample = `sample`
  * (RaytracingMaster.cs:70-73, AddShader.shader:10,44-47): progressive

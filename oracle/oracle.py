@@ -56,6 +56,8 @@ def lib():
         L.orc_intersect.restype = i
         L.orc_render.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp, vp]
         L.orc_render_pixels.argtypes = [vp, vp, i, i, vp, sz, i, i, vp, vp, vp]
+        L.orc_render_ex.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp, vp, vp, vp]
+        L.orc_pack_rgba8.argtypes = [vp, sz, vp]
         L.orc_v1_to_v2.argtypes = [vp, sz, vp]
         L.orc_accumulate.argtypes = [vp, vp, sz, ctypes.c_uint32]
         _lib = L
@@ -137,6 +139,29 @@ def render(svo, cam, width, height, stack_mode=STACK_HLSL, y0=0, y1=None, nthrea
     lib().orc_render(ctypes.byref(svo.s), ctypes.byref(cam), width, height, y0, y1, stack_mode,
                      nthreads, hits.ctypes.data, _ptr(rgba), _ptr(fet))
     return hits, rgba, fet
+
+
+def render_ex(svo, cam, width, height, stack_mode=STACK_HLSL, y0=0, y1=None, nthreads=None):
+    """render() plus per-pixel bestHit.position (float4, w = 0) and voxel keys."""
+    y1 = height if y1 is None else y1
+    n = (y1 - y0) * width
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    hits = np.zeros(n, HIT_DTYPE)
+    rgba = np.zeros((n, 4), np.float32)
+    fet = np.zeros(n, np.uint32)
+    pos = np.zeros((n, 4), np.float32)
+    vox = np.zeros(n, np.uint64)
+    lib().orc_render_ex(ctypes.byref(svo.s), ctypes.byref(cam), width, height, y0, y1, stack_mode, nthreads,
+                        hits.ctypes.data, rgba.ctypes.data, fet.ctypes.data, pos.ctypes.data, vox.ctypes.data)
+    return hits, rgba, fet, pos, vox
+
+
+def pack_rgba8(rgba):
+    """Display RGBA8 words of RGBA32F pixels (svo_frame.rgba8)."""
+    rgba = np.ascontiguousarray(rgba, np.float32).reshape(-1, 4)
+    out = np.zeros(len(rgba), np.uint32)
+    lib().orc_pack_rgba8(rgba.ctypes.data, len(rgba), out.ctypes.data)
+    return out
 
 
 def render_pixels(svo, cam, width, height, pixels, stack_mode=STACK_HLSL, nthreads=None,

@@ -131,9 +131,11 @@ static inline int fetch_node(const orc_svo *svo, uint32_t parent, uint32_t *lo, 
     }
 }
 
-/* NVIDIASVO.compute:12-198.  Returns 1 on hit. */
-int orc_intersect(const orc_svo *svo, const float origin[3], const float dir[3], int stack_mode,
-                  orc_hit *hit, float albedo[3], uint32_t *fetches_out, uint32_t *iters_out) {
+/* NVIDIASVO.compute:12-198.  Returns 1 on hit.  pos_out / voxel_out (nullable):
+ * bestHit.position (:165-174) and the voxel key of the hit leaf (see svo_oracle.h). */
+int orc_intersect_ex(const orc_svo *svo, const float origin[3], const float dir[3], int stack_mode,
+                     orc_hit *hit, float albedo[3], uint32_t *fetches_out, uint32_t *iters_out,
+                     float pos_out[3], uint64_t *voxel_out) {
     int32_t stack_p[32];   /* parent, as stored (int2.x) */
     int32_t stack_t[32];   /* asint(t_max), as stored (int2.y) */
     memset(stack_p, 0, sizeof stack_p);   /* never-written entries read as zero */
@@ -259,10 +261,33 @@ int orc_intersect(const orc_svo *svo, const float origin[3], const float dir[3],
         hit->parent = 0xFFFFFFFFu; hit->hit_idx = 0; hit->hit_scale = 0; hit->flags = flags;
         hit->t = INFINITY; hit->nx = 0.0f; hit->ny = 0.0f; hit->nz = 0.0f;
         if (albedo) { albedo[0] = albedo[1] = albedo[2] = 0.0f; }
+        if (pos_out) { pos_out[0] = pos_out[1] = pos_out[2] = 0.0f; }   /* CreateRayHit: position 0 */
+        if (voxel_out) *voxel_out = ~(uint64_t)0;
         return 0;
     }
     /* :163-186 */
     t_min = t_min * 32.0f;
+    {
+        /* :165-168 undo the mirroring */
+        if ((octant_mask & 1) == 0) px = 3.0f - scale_exp2 - px;
+        if ((octant_mask & 2) == 0) py = 3.0f - scale_exp2 - py;
+        if ((octant_mask & 4) == 0) pz = 3.0f - scale_exp2 - pz;
+        /* :172-174: ray.origin is the SVO-space origin, t_min the x32-scaled one
+         * (reference quirk), clamped into the voxel [pos + eps, pos + size - eps] */
+        const float o3[3] = { ox, oy, oz }, d3[3] = { dx, dy, dz }, p3[3] = { px, py, pz };
+        uint64_t key = 0;
+        for (int k = 0; k < 3; ++k) {
+            float hp = o3[k] + t_min * d3[k];
+            float lo = p3[k] + EPSILON_F;
+            float hi = p3[k] + scale_exp2 - EPSILON_F;
+            float c = fminf(fmaxf(hp, lo), hi);
+            if (pos_out) pos_out[k] = (c - 1.5f) * 64.0f;
+            /* integer voxel coordinate at the leaf scale: the mantissa of the
+             * un-mirrored corner (pos in [1, 2), dyadic) shifted by scale */
+            key |= (uint64_t)(((uint32_t)f2i_bits(p3[k]) & 0x7FFFFFu) >> scale) << (21 * k);
+        }
+        if (voxel_out) *voxel_out = key;
+    }
     int hit_idx = idx ^ octant_mask ^ 7;
     uint32_t blockA = svo->att[(size_t)parent * 2];
     uint32_t blockB = svo->att[(size_t)parent * 2 + 1];
@@ -277,6 +302,11 @@ int orc_intersect(const orc_svo *svo, const float origin[3], const float dir[3],
     hit->nx = n[0]; hit->ny = n[1]; hit->nz = n[2];
     if (albedo) orc_decode_dxt_color(blockA, blockB, hit_idx, albedo);
     return 1;
+}
+
+int orc_intersect(const orc_svo *svo, const float origin[3], const float dir[3], int stack_mode,
+                  orc_hit *hit, float albedo[3], uint32_t *fetches_out, uint32_t *iters_out) {
+    return orc_intersect_ex(svo, origin, dir, stack_mode, hit, albedo, fetches_out, iters_out, NULL, NULL);
 }
 
 /* RaytraceCompute.compute:93-127 (hit branch :115) + :159-167.  The bounce
@@ -317,12 +347,13 @@ int orc_shadow_ray(const orc_svo *svo, const orc_camera *cam, const float o[3], 
 
 static void trace_pixel(const orc_svo *svo, const orc_camera *cam, int width, int height,
                         uint32_t x, uint32_t y, int mode, orc_hit *hit_out, float *rgba_out,
-                        uint32_t *fetch_out) {
-    float o[3], d[3], alb[3];
+                        uint32_t *fetch_out, float *pos_out, uint64_t *voxel_out) {
+    float o[3], d[3], alb[3], pos[3];
     orc_hit h;
     uint32_t f = 0, it = 0;
     orc_camera_ray(cam, x, y, width, height, o, d);
-    orc_intersect(svo, o, d, mode & 0xFF, &h, alb, &f, &it);
+    orc_intersect_ex(svo, o, d, mode & 0xFF, &h, alb, &f, &it, pos, voxel_out);
+    if (pos_out) { pos_out[0] = pos[0]; pos_out[1] = pos[1]; pos_out[2] = pos[2]; pos_out[3] = 0.0f; }
     if (mode & ORC_COUNT_ITERS) f = it;   /* diagnostics: loop iterations instead of fetches */
     int shadowed = 0;
     if ((mode & ORC_SHADOW_RAYS) && (h.flags & 1)) {
@@ -341,7 +372,7 @@ typedef struct {
     const orc_svo *svo; const orc_camera *cam;
     int width, height, y0, y1, mode;
     const uint32_t *pixels; size_t n;
-    orc_hit *hits; float *rgba; uint32_t *fetches;
+    orc_hit *hits; float *rgba; uint32_t *fetches; float *pos; uint64_t *voxel;
     atomic_long next;
 } job_t;
 
@@ -354,7 +385,8 @@ static void *row_worker(void *arg) {
             size_t k = (size_t)(y - j->y0) * (size_t)j->width + (size_t)x;
             trace_pixel(j->svo, j->cam, j->width, j->height, (uint32_t)x, (uint32_t)y, j->mode,
                         j->hits ? &j->hits[k] : NULL, j->rgba ? &j->rgba[4 * k] : NULL,
-                        j->fetches ? &j->fetches[k] : NULL);
+                        j->fetches ? &j->fetches[k] : NULL, j->pos ? &j->pos[4 * k] : NULL,
+                        j->voxel ? &j->voxel[k] : NULL);
         }
     }
     return NULL;
@@ -371,7 +403,8 @@ static void *pixel_worker(void *arg) {
             uint32_t p = j->pixels[k];
             trace_pixel(j->svo, j->cam, j->width, j->height, p % (uint32_t)j->width,
                         p / (uint32_t)j->width, j->mode, j->hits ? &j->hits[k] : NULL,
-                        j->rgba ? &j->rgba[4 * k] : NULL, j->fetches ? &j->fetches[k] : NULL);
+                        j->rgba ? &j->rgba[4 * k] : NULL, j->fetches ? &j->fetches[k] : NULL,
+                        j->pos ? &j->pos[4 * k] : NULL, j->voxel ? &j->voxel[k] : NULL);
         }
     }
     return NULL;
@@ -388,16 +421,37 @@ static void run_threads(job_t *job, int nthreads, void *(*fn)(void *)) {
     for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
 }
 
-void orc_render(const orc_svo *svo, const orc_camera *cam, int width, int height,
-                int y0, int y1, int stack_mode, int nthreads,
-                orc_hit *hits, float *rgba, uint32_t *fetches) {
+void orc_render_ex(const orc_svo *svo, const orc_camera *cam, int width, int height,
+                   int y0, int y1, int stack_mode, int nthreads,
+                   orc_hit *hits, float *rgba, uint32_t *fetches, float *pos4, uint64_t *voxel) {
     job_t job;
     memset(&job, 0, sizeof job);
     job.svo = svo; job.cam = cam; job.width = width; job.height = height;
     job.y0 = y0; job.y1 = y1; job.mode = stack_mode;
-    job.hits = hits; job.rgba = rgba; job.fetches = fetches;
+    job.hits = hits; job.rgba = rgba; job.fetches = fetches; job.pos = pos4; job.voxel = voxel;
     atomic_init(&job.next, 0);
     run_threads(&job, nthreads, row_worker);
+}
+
+void orc_render(const orc_svo *svo, const orc_camera *cam, int width, int height,
+                int y0, int y1, int stack_mode, int nthreads,
+                orc_hit *hits, float *rgba, uint32_t *fetches) {
+    orc_render_ex(svo, cam, width, height, y0, y1, stack_mode, nthreads, hits, rgba, fetches, NULL, NULL);
+}
+
+/* Display RGBA8 of Result colours: each channel (uint)(saturate(c) * 255 + 0.5),
+ * alpha 255 (svo_rt.h svo_frame.rgba8; the reference blits RGBA32F to the screen
+ * format, RaytracingMaster.cs:72). */
+void orc_pack_rgba8(const float *rgba, size_t n_px, uint32_t *out) {
+    for (size_t i = 0; i < n_px; ++i) {
+        uint32_t w = 255u << 24;
+        for (int c = 0; c < 3; ++c) {
+            float v = fminf(fmaxf(rgba[4 * i + c], 0.0f), 1.0f);
+            v = v * 255.0f;
+            w |= (uint32_t)(v + 0.5f) << (8 * c);
+        }
+        out[i] = w;
+    }
 }
 
 void orc_render_pixels(const orc_svo *svo, const orc_camera *cam, int width, int height,

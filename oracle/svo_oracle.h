@@ -82,6 +82,14 @@ void orc_camera_ray(const orc_camera *cam, uint32_t px, uint32_t py, int width, 
 int  orc_intersect(const orc_svo *svo, const float origin[3], const float dir[3], int stack_mode,
                    orc_hit *hit, float albedo[3], uint32_t *fetches, uint32_t *iters);
 
+/* orc_intersect plus bestHit.position (NVIDIASVO.compute:165-174: un-mirrored
+ * voxel corner, (clamp(o' + 32 t * d, pos + eps, pos + size - eps) - 1.5) * 64;
+ * misses 0) and the voxel key x | y << 21 | z << 42 (integer voxel coordinates
+ * at the leaf scale = (bits(pos) & 0x7FFFFF) >> scale; misses all ones). */
+int  orc_intersect_ex(const orc_svo *svo, const float origin[3], const float dir[3], int stack_mode,
+                      orc_hit *hit, float albedo[3], uint32_t *fetches, uint32_t *iters,
+                      float pos[3], uint64_t *voxel);
+
 void orc_sky(const float dir[3], float out[3]);
 
 /* Shadow ray toward -L from a primary hit; 1 if occluded (see svo_oracle.c). */
@@ -93,6 +101,14 @@ int  orc_shadow_ray(const orc_svo *svo, const orc_camera *cam, const float o[3],
 void orc_render(const orc_svo *svo, const orc_camera *cam, int width, int height,
                 int y0, int y1, int stack_mode, int nthreads,
                 orc_hit *hits, float *rgba, uint32_t *fetches);
+
+/* orc_render plus float4 positions (w = 0) and voxel keys per pixel (nullable). */
+void orc_render_ex(const orc_svo *svo, const orc_camera *cam, int width, int height,
+                   int y0, int y1, int stack_mode, int nthreads,
+                   orc_hit *hits, float *rgba, uint32_t *fetches, float *pos4, uint64_t *voxel);
+
+/* Display RGBA8 words of n RGBA32F pixels (svo_frame.rgba8). */
+void orc_pack_rgba8(const float *rgba, size_t n_px, uint32_t *out);
 
 /* Render an explicit list of pixel indices (y * width + x). */
 void orc_render_pixels(const orc_svo *svo, const orc_camera *cam, int width, int height,

@@ -24,18 +24,33 @@ HIT_DTYPE = np.dtype([("parent", "<u4"), ("hit_idx", "u1"), ("hit_scale", "u1"),
                       ("nz", "<f4")])
 assert HIT_DTYPE.itemsize == 24
 
+COMPACT_DTYPE = np.dtype([("parent", "<u4"), ("meta", "<u4"), ("t", "<f4")])   # svo_hit_compact
+assert COMPACT_DTYPE.itemsize == 12
+
+ABI_VERSION = 2
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
            "svo_destroy", "svo_last_error", "svo_abi_version", "svo_set_options", "svo_accumulate",
-           "svo_kernel_time")
+           "svo_kernel_time", "svo_create_multi", "svo_num_devices", "svo_get_member", "svo_render_frame",
+           "svo_assemble_frame", "svo_stage_time")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
+LAYOUT_BAND, LAYOUT_FRAME = 0, 1
+PART_COMPACT, PART_RGBA8 = 0, 1
+STAGE_KERNEL, STAGE_ASSEMBLE = 0, 1
 
 
 class SvoBand(ctypes.Structure):
     _fields_ = [("band_rows", ctypes.c_int), ("band_rank", ctypes.c_int),
                 ("band_count", ctypes.c_int)]
+
+
+class SvoFrame(ctypes.Structure):
+    """svo_frame: device pointers (ints) of every per-pixel output, each nullable."""
+    _fields_ = [("hits", ctypes.c_void_p), ("rgba", ctypes.c_void_p), ("rgba8", ctypes.c_void_p),
+                ("compact", ctypes.c_void_p), ("position", ctypes.c_void_p), ("voxel", ctypes.c_void_p),
+                ("layout", ctypes.c_int)]
 
 
 class SvoError(RuntimeError):
@@ -61,25 +76,37 @@ def lib():
     _load_torch_first()
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     vp, sz, i, f = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_float
-    L.svo_create.argtypes = [i, sz, ctypes.POINTER(vp)]
-    L.svo_set_buffer.argtypes = [vp, vp, sz, vp, sz, sz]
-    L.svo_set_buffer_v2.argtypes = [vp, vp, sz, vp, sz, sz]
-    L.svo_set_camera.argtypes = [vp, vp, vp, f, f, vp]
-    L.svo_render.argtypes = [vp, i, i, i, vp, vp]
-    L.svo_render_device.argtypes = [vp, i, i, i, vp, vp, vp, vp]
-    L.svo_count_fetches.argtypes = [vp, i, i, i, vp, vp, vp]
-    L.svo_set_options.argtypes = [vp, ctypes.c_uint32]
-    L.svo_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
-    L.svo_accumulate.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, vp]
-    L.svo_get_info.argtypes = [vp, ctypes.POINTER(sz), ctypes.POINTER(i), ctypes.POINTER(i)]
-    L.svo_synchronize.argtypes = [vp]
-    L.svo_destroy.argtypes = [vp]
-    L.svo_last_error.restype = ctypes.c_char_p
-    L.svo_last_error.argtypes = []
-    L.svo_abi_version.restype = i
+    sig = {
+        "svo_create": [i, sz, ctypes.POINTER(vp)],
+        "svo_set_buffer": [vp, vp, sz, vp, sz, sz],
+        "svo_set_buffer_v2": [vp, vp, sz, vp, sz, sz],
+        "svo_set_camera": [vp, vp, vp, f, f, vp],
+        "svo_render": [vp, i, i, i, vp, vp],
+        "svo_render_device": [vp, i, i, i, vp, vp, vp, vp],
+        "svo_count_fetches": [vp, i, i, i, vp, vp, vp],
+        "svo_set_options": [vp, ctypes.c_uint32],
+        "svo_kernel_time": [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)],
+        "svo_accumulate": [vp, vp, vp, sz, ctypes.c_uint32, vp],
+        "svo_get_info": [vp, ctypes.POINTER(sz), ctypes.POINTER(i), ctypes.POINTER(i)],
+        "svo_create_multi": [ctypes.POINTER(i), i, sz, i, ctypes.POINTER(vp)],
+        "svo_num_devices": [vp, ctypes.POINTER(i)],
+        "svo_get_member": [vp, i, ctypes.POINTER(vp)],
+        "svo_render_frame": [vp, i, i, i, vp, ctypes.POINTER(SvoFrame), vp],
+        "svo_assemble_frame": [vp, i, i, i, i, ctypes.POINTER(vp), i, i, ctypes.POINTER(SvoFrame), vp],
+        "svo_stage_time": [vp, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)],
+        "svo_synchronize": [vp],
+        "svo_destroy": [vp],
+        "svo_last_error": [],
+        "svo_abi_version": [],
+    }
+    # SVO_RT_LIB (A/B diagnostics) may name an older build: bind what it has
+    strict = not os.environ.get("SVO_RT_LIB")
     for name in EXPORTS:
-        getattr(L, name).restype = getattr(L, name).restype or i
-    L.svo_last_error.restype = ctypes.c_char_p
+        if not strict and not hasattr(L, name):
+            continue
+        fn = getattr(L, name)
+        fn.argtypes = sig[name]
+        fn.restype = ctypes.c_char_p if name == "svo_last_error" else i
     _lib = L
     return L
 

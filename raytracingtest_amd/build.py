@@ -40,6 +40,21 @@ def _stale(out, srcs):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def source_digest(name="libsvo_rt.so"):
+    """sha1 over a library's sources, the headers and the compile flags: the key
+    under which profiling evidence (profiles/pmc_summary.json) is valid."""
+    import hashlib
+    h = hashlib.sha1(" ".join(COMMON + [ARCH]).encode())
+    files = [os.path.join(CSRC, s) for s in TARGETS[name]]
+    files += sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
+    files += sorted(os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE))
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode())
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def build(force=False, verbose=False):
     built = []
     for name, srcs in TARGETS.items():

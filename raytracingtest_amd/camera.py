@@ -32,6 +32,11 @@ OVERVIEW_TARGET = (0.0, 0.0, 0.0)
 # terrain; the rest leave the cube (sky).
 FLYOVER_EYE = (0.0, 15.0, -10.0)
 FLYOVER_TARGET = (0.0, -6.0, 6.0)
+# Terrain-facing camera (the large configs were benched only on
+# the sky-heavy overview pose): above the middle of the cube looking steeply down,
+# so nearly every primary ray ends on the terrain.
+TERRAIN_EYE = (0.0, 14.0, -3.0)
+TERRAIN_TARGET = (0.0, -10.0, 3.0)
 
 
 def perspective(fov_deg, aspect, near, far):
@@ -109,7 +114,12 @@ def flyover_camera():
     return overview_camera(FLYOVER_EYE, FLYOVER_TARGET)
 
 
-CAMERAS = {"main": main_camera, "overview": overview_camera, "flyover": flyover_camera}
+def terrain_camera():
+    """Terrain-facing pose: nearly all primary rays hit (C4 / C5 beside 'overview')."""
+    return overview_camera(TERRAIN_EYE, TERRAIN_TARGET)
+
+
+CAMERAS = {"main": main_camera, "overview": overview_camera, "flyover": flyover_camera, "terrain": terrain_camera}
 
 
 def main_light():

@@ -3,19 +3,14 @@
 // Line references are to the reference repo: NVIDIASVO.compute (N:),
 // RaytraceCompute.compute (R:), AttachmentLookup.compute (A:).
 //
-// Two launch shapes over one traversal core:
-//   * tile kernel (default): one lane per pixel, a wave64 = an 8x8 pixel tile;
-//   * persistent kernel: resident waves pull rays from a global counter in
-//     64-ray 8x8 tiles; whenever fewer than p.refill_at lanes of a wave are
-//     still tracing, the idle lanes take new rays (ballot + one atomicAdd per
-//     wave + mbcnt rank) -- active-ray compaction within the wave.
-//     Measured on MI355X (C3 flyover): 8x8 primary-ray tiles are
-//     already ~90% SIMD-efficient and one global counter serialises at ~88
-//     dequeues/us, so this shape is 2-8x SLOWER here; it is kept for
-//     incoherent ray sets (secondary rays) and as the A/B reference.
-// The loop body is written branch-light: PUSH and ADVANCE differ only in
-// selected addends, so divergent lanes share one instruction stream; only the
-// node fetch, the stack store, POP and termination are predicated regions.
+// One launch shape: one lane per pixel, a wave64 (= a 64-thread workgroup) is
+// an 8x8 pixel tile, tiles dispatched heaviest-first from the previous launch's
+// recorded trip counts.  The traversal is the "lean" loop below, written for
+// the wave: per-lane branch conditions are 64-bit lane masks in SGPRs, so
+// divergent lanes share one instruction stream.  Forms measured slower in
+// round 1 (branchy and branch-flattened per-lane steps, 128/256-thread blocks,
+// a persistent kernel refilling lanes from a global counter, row-band XCD
+// placement) were removed (DESIGN.md 5.1 keeps their numbers).
 #include "svo_traverse.h"
 
 namespace svo {
@@ -79,35 +74,69 @@ __device__ __forceinline__ int32_t cvt_i32(float f) {
     return r;
 }
 
+// Display RGBA8 of a Result colour (alpha 1): saturate, * 255, round half up.
+// == orc_pack_rgba8.
+__device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b) {
+    auto q = [](float c) {
+        c = fminf(fmaxf(c, 0.0f), 1.0f);
+        c = c * 255.0f;
+        return (uint32_t)(c + 0.5f);
+    };
+    return q(r) | (q(g) << 8) | (q(b) << 16) | (255u << 24);
+}
+
+// Procedural sky (the reference's skybox assets are missing), == orc_sky.
+__device__ __forceinline__ void sky(float dir_y, float rgb[3]) {
+    const float k = 0.5f * dir_y + 0.5f;
+    rgb[0] = 0.25f + 0.5f * k;
+    rgb[1] = 0.35f + 0.55f * k;
+    rgb[2] = 0.6f + 0.4f * k;
+}
+
+// R:93-127 hit branch (:115): saturate(-dot(n, L)) * L.w * albedo.  == shade_pixel.
+__device__ __forceinline__ void shade_hit(const Camera &cam, const float n[3], const float alb[3], float rgb[3]) {
+    float d = n[0] * cam.light[0];
+    d = d + n[1] * cam.light[1];
+    d = d + n[2] * cam.light[2];
+    float s = d * -1.0f;
+    s = fminf(fmaxf(s, 0.0f), 1.0f);
+    s = s * cam.light[3];
+    rgb[0] = s * alb[0]; rgb[1] = s * alb[1]; rgb[2] = s * alb[2];
+}
+
 struct Ray {
     float tx_coef, ty_coef, tz_coef, tx_bias, ty_bias, tz_bias;
     float t_min, t_max, h;
     float px, py, pz, scale_exp2;
     float dir_y;               // for the sky colour
-    uint32_t parent, cd, first;
-    uint32_t written;          // bit s: stack slot s written by this ray
+    uint32_t parent;
     uint32_t fetches;
-    int idx, octant_mask, scale, iters;
+    int idx, octant_mask, scale;
     uint32_t flags;
-    bool cached;
 };
 
 // R:151 uv, R:129-141 CreateCameraRay
-__device__ __forceinline__ void camera_ray(const LaunchParams &p, int x, int y, float org[3], float dir[3]) {
-    const float u = ((float)x + p.cam.px_off[0]) / (float)p.width * 2.0f - 1.0f;
-    const float v = ((float)y + p.cam.px_off[1]) / (float)p.height * 2.0f - 1.0f;
+__device__ __forceinline__ void camera_ray(const Camera &cam, int width, int height, int x, int y, float org[3],
+                                           float dir[3]) {
+    const float u = ((float)x + cam.px_off[0]) / (float)width * 2.0f - 1.0f;
+    const float v = ((float)y + cam.px_off[1]) / (float)height * 2.0f - 1.0f;
     float pd[3];
-    mul4(p.cam.c2w, 0.0f, 0.0f, 0.0f, 1.0f, org);
-    mul4(p.cam.inv_proj, u, v, 0.0f, 1.0f, pd);
-    mul4(p.cam.c2w, pd[0], pd[1], pd[2], 0.0f, dir);
+    mul4(cam.c2w, 0.0f, 0.0f, 0.0f, 1.0f, org);
+    mul4(cam.inv_proj, u, v, 0.0f, 1.0f, pd);
+    mul4(cam.c2w, pd[0], pd[1], pd[2], 0.0f, dir);
     normalize3(dir);
+}
+
+// N:15-19 world -> SVO cube [1, 2]^3
+__device__ __forceinline__ float to_svo(float w) {
+    const float s = w * (1.0f / 32.0f);
+    return s + 1.5f;
 }
 
 // N:15-54 setup for a ray (origin, direction) in world space
 __device__ __forceinline__ void setup_ray(const float org[3], const float dir[3], Ray &r) {
     r.dir_y = dir[1];
-    float ox = org[0] * (1.0f / 32.0f), oy = org[1] * (1.0f / 32.0f), oz = org[2] * (1.0f / 32.0f);
-    ox = ox + 1.5f; oy = oy + 1.5f; oz = oz + 1.5f;
+    const float ox = to_svo(org[0]), oy = to_svo(org[1]), oz = to_svo(org[2]);
     r.tx_coef = 1.0f / -fabsf(dir[0]);
     r.ty_coef = 1.0f / -fabsf(dir[1]);
     r.tz_coef = 1.0f / -fabsf(dir[2]);
@@ -122,8 +151,7 @@ __device__ __forceinline__ void setup_ray(const float org[3], const float dir[3]
     r.t_max = fminf(fminf(r.tx_coef - r.tx_bias, r.ty_coef - r.ty_bias), r.tz_coef - r.tz_bias);
     r.h = r.t_max;
     r.t_min = fmaxf(r.t_min, 0.0f);
-    r.parent = 0; r.cd = 0; r.first = 0;
-    r.cached = false;
+    r.parent = 0;
     r.idx = 0;
     r.px = 1.0f; r.py = 1.0f; r.pz = 1.0f;
     r.scale = S_MAX - 1;
@@ -131,212 +159,12 @@ __device__ __forceinline__ void setup_ray(const float org[3], const float dir[3]
     if (1.5f * r.tx_coef - r.tx_bias > r.t_min) { r.idx ^= 1; r.px = 1.5f; }
     if (1.5f * r.ty_coef - r.ty_bias > r.t_min) { r.idx ^= 2; r.py = 1.5f; }
     if (1.5f * r.tz_coef - r.tz_bias > r.t_min) { r.idx ^= 4; r.pz = 1.5f; }
-    r.written = 0; r.fetches = 0; r.iters = 0; r.flags = 0;
-}
-
-__device__ __forceinline__ void init_ray(const LaunchParams &p, int x, int y, Ray &r) {
-    float org[3], dir[3];
-    camera_ray(p, x, y, org, dir);
-    setup_ray(org, dir, r);
-}
-
-// One iteration of N:57-156.  Returns true when the ray is finished: a leaf hit
-// (r.scale < S_MAX) or a miss (r.scale >= S_MAX).
-template <int MODE, bool COUNT, int STRIDE = BLOCK>
-__device__ __forceinline__ bool step(const LaunchParams &p, Ray &r, uint2 *__restrict__ stk, int scale_lo) {
-    if (r.scale >= S_MAX) return true;
-    if (++r.iters > MAX_ITERS) { r.flags |= 2u; r.scale = S_MAX; return true; }
-    if (!r.cached) {                                       // N:60-62
-        const uint2 nd = r.parent < p.n_nodes ? p.nodes[r.parent] : make_uint2(0u, 0u);   // out of range reads 0
-        r.cd = nd.x;
-        r.first = nd.y;
-        r.cached = (nd.x | nd.y) != 0u;
-        if (COUNT) ++r.fetches;
-    }
-    const float tx_corner = r.px * r.tx_coef - r.tx_bias;
-    const float ty_corner = r.py * r.ty_coef - r.ty_bias;
-    const float tz_corner = r.pz * r.tz_coef - r.tz_bias;
-    const float tc_max = fminf(fminf(tx_corner, ty_corner), tz_corner);
-    const uint32_t child_masks = r.cd << (r.idx ^ r.octant_mask);
-    const float tv_max = fminf(r.t_max, tc_max);
-    const bool descend = (child_masks & 0x8000u) != 0u && r.t_min <= r.t_max && r.t_min <= tv_max;
-    if (descend && (child_masks & 0x0080u) == 0u) return true;   // leaf hit (N:93-94)
-
-    const float half = r.scale_exp2 * 0.5f;
-    int new_idx;
-    float ax, ay, az;
-    if (descend) {
-        // PUSH (N:97-117)
-        if (tc_max < r.h) {
-            const int s = r.scale - scale_lo;
-            if (s < 0) { r.flags |= 4u; r.scale = S_MAX; return true; }
-            uint2 e;
-            if (MODE == 0) {   // int2 <- float2((int)parent, asint(t_max))
-                e.x = (uint32_t)cvt_i32((float)(int32_t)r.parent);
-                e.y = (uint32_t)cvt_i32((float)__float_as_int(r.t_max));
-            } else {
-                e.x = r.parent;
-                e.y = (uint32_t)__float_as_int(r.t_max);
-            }
-            stk[s * STRIDE] = e;
-            r.written |= 1u << s;
-        }
-        r.h = tc_max;
-        r.parent = r.first + (uint32_t)__builtin_popcount(child_masks & 0x7Fu);
-        const float tx_center = half * r.tx_coef + tx_corner;
-        const float ty_center = half * r.ty_coef + ty_corner;
-        const float tz_center = half * r.tz_coef + tz_corner;
-        new_idx = (tx_center > r.t_min ? 1 : 0) | (ty_center > r.t_min ? 2 : 0) | (tz_center > r.t_min ? 4 : 0);
-        ax = (new_idx & 1) ? half : 0.0f;
-        ay = (new_idx & 2) ? half : 0.0f;
-        az = (new_idx & 4) ? half : 0.0f;
-        r.scale -= 1;
-        r.scale_exp2 = half;
-        r.t_max = tv_max;
-        r.cached = false;
-    } else {
-        // ADVANCE (N:122-128)
-        const int step_mask = (tx_corner <= tc_max ? 1 : 0) | (ty_corner <= tc_max ? 2 : 0) |
-                              (tz_corner <= tc_max ? 4 : 0);
-        ax = (step_mask & 1) ? -r.scale_exp2 : 0.0f;
-        ay = (step_mask & 2) ? -r.scale_exp2 : 0.0f;
-        az = (step_mask & 4) ? -r.scale_exp2 : 0.0f;
-        r.t_min = tc_max;
-        new_idx = r.idx ^ step_mask;
-        if ((new_idx & step_mask) != 0) {
-            // POP (N:134-154): positions after the step, then the highest differing bit
-            const float qx = r.px + ax, qy = r.py + ay, qz = r.pz + az;
-            uint32_t differing = 0;
-            if (step_mask & 1) differing |= (uint32_t)(__float_as_int(qx) ^ __float_as_int(qx + r.scale_exp2));
-            if (step_mask & 2) differing |= (uint32_t)(__float_as_int(qy) ^ __float_as_int(qy + r.scale_exp2));
-            if (step_mask & 4) differing |= (uint32_t)(__float_as_int(qz) ^ __float_as_int(qz + r.scale_exp2));
-            const int scale = (__float_as_int((float)differing) >> 23) - 127;
-            r.scale = scale;
-            r.scale_exp2 = __int_as_float((scale - S_MAX + 127) << 23);
-            const int s = scale - scale_lo;
-            uint2 e = make_uint2(0u, 0u);
-            if (s >= 0 && s < 32 && ((r.written >> s) & 1u)) e = stk[s * STRIDE];
-            r.parent = e.x;
-            r.t_max = __int_as_float((int32_t)e.y);
-            const int32_t shx = __float_as_int(qx) >> scale;
-            const int32_t shy = __float_as_int(qy) >> scale;
-            const int32_t shz = __float_as_int(qz) >> scale;
-            r.px = __int_as_float((int32_t)((uint32_t)shx << scale));
-            r.py = __int_as_float((int32_t)((uint32_t)shy << scale));
-            r.pz = __int_as_float((int32_t)((uint32_t)shz << scale));
-            r.idx = (shx & 1) | ((shy & 1) << 1) | ((shz & 1) << 2);
-            r.h = 0.0f;
-            r.cached = false;
-            return r.scale >= S_MAX;
-        }
-    }
-    r.px = r.px + ax;
-    r.py = r.py + ay;
-    r.pz = r.pz + az;
-    r.idx = new_idx;
-    return false;
-}
-
-// Branch-flattened iteration (default): identical results to step(), but PUSH
-// and ADVANCE are both evaluated and selected per lane, and the stack store is
-// unconditional (non-pushing lanes write a per-lane dummy slot), leaving only
-// the node fetch, POP and termination as divergent regions.  This removes most
-// of the exec-mask SALU traffic that dominated the branchy loop (SQ_INSTS_SALU
-// ~0.73 x SQ_INSTS_VALU on MI355X).
-template <int MODE, bool COUNT, int STRIDE = BLOCK>
-__device__ __forceinline__ bool step_flat(const LaunchParams &p, Ray &r, uint2 *__restrict__ stk, int scale_lo,
-                                          int dummy) {
-    if (++r.iters > MAX_ITERS) { r.flags |= 2u; r.scale = S_MAX; return true; }
-    if (!r.cached) {                                       // N:60-62
-        const uint2 nd = r.parent < p.n_nodes ? p.nodes[r.parent] : make_uint2(0u, 0u);   // out of range reads 0
-        r.cd = nd.x;
-        r.first = nd.y;
-        r.cached = (nd.x | nd.y) != 0u;
-        if (COUNT) ++r.fetches;
-    }
-    const float tx_corner = r.px * r.tx_coef - r.tx_bias;
-    const float ty_corner = r.py * r.ty_coef - r.ty_bias;
-    const float tz_corner = r.pz * r.tz_coef - r.tz_bias;
-    const float tc_max = fminf(fminf(tx_corner, ty_corner), tz_corner);
-    const uint32_t child_masks = r.cd << (r.idx ^ r.octant_mask);
-    const float tv_max = fminf(r.t_max, tc_max);
-    const bool descend = (child_masks & 0x8000u) != 0u && r.t_min <= r.t_max && r.t_min <= tv_max;
-    const bool do_store = descend && tc_max < r.h;
-    const int s_push = r.scale - scale_lo;
-    if ((descend && (child_masks & 0x0080u) == 0u) || (do_store && s_push < 0)) {
-        if (!(descend && (child_masks & 0x0080u) == 0u)) { r.flags |= 4u; r.scale = S_MAX; }
-        return true;                                       // leaf hit (N:93-94) or stack overflow
-    }
-    const float half = r.scale_exp2 * 0.5f;
-    // PUSH candidate (N:83-117)
-    const float tx_center = half * r.tx_coef + tx_corner;
-    const float ty_center = half * r.ty_coef + ty_corner;
-    const float tz_center = half * r.tz_coef + tz_corner;
-    const int cidx = (tx_center > r.t_min ? 1 : 0) | (ty_center > r.t_min ? 2 : 0) | (tz_center > r.t_min ? 4 : 0);
-    // ADVANCE candidate (N:122-128)
-    const int step_mask = (tx_corner <= tc_max ? 1 : 0) | (ty_corner <= tc_max ? 2 : 0) | (tz_corner <= tc_max ? 4 : 0);
-    // stack store (N:97-98); lanes that do not push write their dummy slot
-    uint2 e;
-    if (MODE == 0) {   // int2 <- float2((int)parent, asint(t_max))
-        e.x = (uint32_t)cvt_i32((float)(int32_t)r.parent);
-        e.y = (uint32_t)cvt_i32((float)__float_as_int(r.t_max));
-    } else {
-        e.x = r.parent;
-        e.y = (uint32_t)__float_as_int(r.t_max);
-    }
-    stk[(do_store ? s_push : dummy) * STRIDE] = e;
-    r.written |= do_store ? (1u << s_push) : 0u;
-
-    const int mx = descend ? (cidx & 1) : (step_mask & 1);
-    const int my = descend ? (cidx & 2) : (step_mask & 2);
-    const int mz = descend ? (cidx & 4) : (step_mask & 4);
-    const float delta = descend ? half : -r.scale_exp2;
-    const float qx = r.px + (mx ? delta : 0.0f);
-    const float qy = r.py + (my ? delta : 0.0f);
-    const float qz = r.pz + (mz ? delta : 0.0f);
-    const int new_idx = descend ? cidx : (r.idx ^ step_mask);
-    const uint32_t child = r.first + (uint32_t)__builtin_popcount(child_masks & 0x7Fu);
-    r.h = descend ? tc_max : r.h;
-    r.parent = descend ? child : r.parent;
-    r.t_max = descend ? tv_max : r.t_max;
-    r.t_min = descend ? r.t_min : tc_max;
-    r.cached = descend ? false : r.cached;
-    if (!descend && (new_idx & step_mask) != 0) {
-        // POP (N:134-154)
-        uint32_t differing = 0;
-        if (step_mask & 1) differing |= (uint32_t)(__float_as_int(qx) ^ __float_as_int(qx + r.scale_exp2));
-        if (step_mask & 2) differing |= (uint32_t)(__float_as_int(qy) ^ __float_as_int(qy + r.scale_exp2));
-        if (step_mask & 4) differing |= (uint32_t)(__float_as_int(qz) ^ __float_as_int(qz + r.scale_exp2));
-        const int scale = (__float_as_int((float)differing) >> 23) - 127;
-        r.scale = scale;
-        r.scale_exp2 = __int_as_float((scale - S_MAX + 127) << 23);
-        const int s = scale - scale_lo;   // in [0, slots]; slots == dummy only when leaving the root
-        const uint2 se = stk[s * STRIDE];
-        const bool ok = (r.written >> s) & 1u;
-        r.parent = ok ? se.x : 0u;
-        r.t_max = __int_as_float(ok ? (int32_t)se.y : 0);
-        const int32_t shx = __float_as_int(qx) >> scale;
-        const int32_t shy = __float_as_int(qy) >> scale;
-        const int32_t shz = __float_as_int(qz) >> scale;
-        r.px = __int_as_float((int32_t)((uint32_t)shx << scale));
-        r.py = __int_as_float((int32_t)((uint32_t)shy << scale));
-        r.pz = __int_as_float((int32_t)((uint32_t)shz << scale));
-        r.idx = (shx & 1) | ((shy & 1) << 1) | ((shz & 1) << 2);
-        r.h = 0.0f;
-        r.cached = false;
-        return r.scale >= S_MAX;
-    }
-    r.scale = descend ? r.scale - 1 : r.scale;
-    r.scale_exp2 = descend ? half : r.scale_exp2;
-    r.px = qx; r.py = qy; r.pz = qz;
-    r.idx = new_idx;
-    return false;
+    r.fetches = 0; r.flags = 0;
 }
 
 // ------------------------------------------------------- lean traversal
-// The default tile-kernel loop.  Same results as step()/step_flat() (the GPU
-// parity tests compare them all against the oracle), restructured for VALU
-// issue, which is what bounds this kernel at 8 waves/SIMD:
+// The tile-kernel loop: N:57-156 restructured for VALU issue, which is what
+// bounds this kernel at 8 waves/SIMD:
 //   * per-lane booleans (child index bits, octant mask, PUSH/ADVANCE/POP,
 //     node cached) are held explicitly as 64-bit lane masks in SGPRs
 //     (ballot / inverse_ballot), so the index algebra of N:83-154 is SALU
@@ -367,11 +195,11 @@ __device__ __forceinline__ float vmin(float a, float b) {
     return r;
 }
 
-#ifndef SVO_FMA_CENTER
-#define SVO_FMA_CENTER 1
-#endif
+// tx_center = half * tx_coef + tx_corner (N:111-113) as one fma: half is a power of
+// two >= 2^-23 and |tx_coef| >= 1, so half * tx_coef is exact (no rounding, no
+// underflow) and the fused result equals the two-rounding HLSL form bit for bit
 __device__ __forceinline__ float center(float half, float coef, float corner) {
-    return SVO_FMA_CENTER ? __builtin_fmaf(half, coef, corner) : half * coef + corner;
+    return __builtin_fmaf(half, coef, corner);
 }
 
 // 3-bit per-lane integer b0 | b1 << 1 | b2 << 2 from three lane masks.
@@ -391,8 +219,9 @@ struct FRay {
     float px, py, pz, cx, cy, cz, bx, by, bz;
     float t_min, t_max, h, sexp, dir_y;
     uint32_t parent, cd16, first, flags;
+    uint32_t fetches;       // COUNT: descriptor fetches (N:60-62 executions)
     int idx, octant_mask;   // only at entry / exit
-    int trips;              // wave-uniform loop trip count (diagnostics)
+    int trips;              // wave-uniform loop trip count
 };
 
 __device__ __forceinline__ void to_fray(const Ray &r, FRay &f) {
@@ -400,17 +229,19 @@ __device__ __forceinline__ void to_fray(const Ray &r, FRay &f) {
     f.cx = r.tx_coef; f.cy = r.ty_coef; f.cz = r.tz_coef;
     f.bx = r.tx_bias; f.by = r.ty_bias; f.bz = r.tz_bias;
     f.t_min = r.t_min; f.t_max = r.t_max; f.h = r.h; f.sexp = r.scale_exp2; f.dir_y = r.dir_y;
-    f.parent = 0; f.cd16 = 0; f.first = 0; f.flags = 0;
+    f.parent = 0; f.cd16 = 0; f.first = 0; f.flags = 0; f.fetches = 0;
     f.idx = r.idx; f.octant_mask = r.octant_mask;
 }
 
-// Back to the Ray fields finish() reads.
+// Back to the Ray fields the outputs read.
 __device__ __forceinline__ void from_fray(const FRay &f, Ray &r) {
     const bool miss = f.sexp >= 1.0f || (f.flags & 6u) != 0u;
     r.scale = miss ? S_MAX : (int)(__float_as_uint(f.sexp) >> 23) - 104;
     r.idx = f.idx;
     r.octant_mask = f.octant_mask;
     r.t_min = f.t_min; r.parent = f.parent; r.flags = f.flags; r.dir_y = f.dir_y;
+    r.px = f.px; r.py = f.py; r.pz = f.pz; r.scale_exp2 = f.sexp;
+    r.fetches = f.fetches;
 }
 
 struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
@@ -418,29 +249,30 @@ struct LeanDiag {            // DIAG instantiation only (env SVO_WAVE_LOG)
     uint32_t fetch_trips = 0, pop_trips = 0;
 };
 
-template <int MODE, int STRIDE, bool GUARD, bool DIAG = false, bool V2 = false, bool FETCH_ALL = false>
+template <int MODE, bool GUARD, bool DIAG = false, bool FETCH_ALL = false, bool COUNT = false>
 __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk,
                                            LeanDiag *diag = nullptr) {
     // GUARD = false (host-proven, svo_rt.hip launch / recompute_depth): one tree of
     // known depth, fewer than 2^29 nodes, and (HLSL stack) parent indices below
     // 2^24, so a PUSH never overflows the stack, the HLSL round trip of a parent
     // index is the identity and node byte offsets fit 32 bits.
+    constexpr int STRIDE = TILE;
     const int slots = p.slots;
     // + the spare slot: a ray that leaves the root takes its parent from there, and
-    // (V2, !GUARD) every lane, finished ones too, fetches nodes[parent] on every trip
+    // (!GUARD) every lane, finished ones too, fetches nodes[parent] on every trip
     for (int s = 0; s <= slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
     const int scale_lo = S_MAX - slots;
     const float sexp_lo = __int_as_float((scale_lo - S_MAX + 127) << 23);   // push below scale_lo overflows
     lmask act = LM_OF(true);
-    const int oct = V2 ? (r.octant_mask | 16) : r.octant_mask;   // V2: c ^ (oct | 16) == (c ^ oct) + 16
+    const int oct = r.octant_mask | 16;    // c ^ (oct | 16) == (c ^ oct) + 16
     int sh = r.idx ^ oct;                  // child index bits ^ oct: the descriptor shift (per lane, VGPR)
     lmask cached = 0, capped = 0, ovf = 0;
     const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
     constexpr uint32_t SLOT = (uint32_t)(STRIDE * sizeof(uint2));
-    constexpr int SLOT_SH = 23 - (STRIDE == 64 ? 9 : STRIDE == 128 ? 10 : 11);   // (bits >> 23) * SLOT
-    static_assert(SLOT == (1u << (23 - SLOT_SH)), "stride must be 64, 128 or 256 lanes");
+    constexpr int SLOT_SH = 23 - 9;        // (bits >> 23) * SLOT with SLOT = 512
+    static_assert(SLOT == (1u << (23 - SLOT_SH)), "stride must be 64 lanes");
     const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
-    // V2 POP: slot address from the exponent field e of float(differing), e = scale + 127
+    // POP: slot address from the exponent field e of float(differing), e = scale + 127
     const uint2 *stk_pop = stk - (127 + scale_lo) * STRIDE;   // indexed by e (never below slot 1)
     const uint32_t e_max = (uint32_t)(127 + scale_lo + slots);   // leaving the root: the spare slot
     int it = 0;
@@ -448,7 +280,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     if (DIAG) tl0 = __builtin_amdgcn_s_memtime();
     // per-lane values from here on (works round an LLVM uniformity-analysis bug that
     // otherwise rejects the SGPR trip counter below: "illegal VGPR to SGPR copy")
-    if (V2) asm volatile("" : "+v"(r.parent), "+v"(r.cd16), "+v"(r.first));
+    asm volatile("" : "+v"(r.parent), "+v"(r.cd16), "+v"(r.first));
     // one exit (no per-trip phi copies), the cap part of the test; a do-while with the
     // continue mask built in asm (s_cmp + s_cselect, then s_cmp_lg + branch: 4 SALU instead of
     // the 7 LLVM makes of `act != 0 && it < MAX_ITERS`; kernel -1 to -2 %).  On entry act != 0
@@ -457,7 +289,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     do {
         // wave-uniform trip count kept in an SGPR (LLVM otherwise counts down in a VGPR)
         asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
-        // N:60-62.  FETCH_ALL (V2, !GUARD, pools below 2^24 nodes -- svo_rt.hip):
+        // N:60-62.  FETCH_ALL (!GUARD, pools below 2^24 nodes -- svo_rt.hip):
         // every lane fetches on every trip, unpredicated; re-fetching a cached node
         // reads the same word, and a load outside a divergent branch issues at the
         // top of the trip with nothing to wait for (C3: 5 % faster, 9 % on the
@@ -465,7 +297,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         // extra loads cost 6-12 %, so those fetch only the lanes that need a node.
         // Every lane's parent is a valid index: a pool proven to be one tree, and
         // a ray that left the root holds the cleared spare slot's 0.
-        constexpr bool ALWAYS = V2 && !GUARD && FETCH_ALL;
+        constexpr bool ALWAYS = !GUARD && FETCH_ALL && !COUNT;
         const lmask need = ALWAYS ? ~(lmask)0 : act & ~cached;
         if (ALWAYS || LM_ON(need)) {
             // GUARD == false: pool below 2^29 nodes (svo_rt.hip), so the byte offset fits
@@ -474,11 +306,14 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             // reads as 0 like an out-of-range StructuredBuffer element.
             const uint2 nd = GUARD ? (r.parent < p.n_nodes ? p.nodes[r.parent] : make_uint2(0u, 0u))
                                    : *(const uint2 *)((const char *)p.nodes + (uint32_t)(r.parent << 3));
-            r.cd16 = V2 ? nd.x : nd.x << 16;
+            r.cd16 = nd.x;
             r.first = nd.y;
+            if (COUNT) r.fetches += 1u;
         }
         if (DIAG && need) diag->fetch_trips += 1;
-        cached |= need;
+        // COUNT keeps the HLSL re-fetch of a zero descriptor (N:60 `child_descriptor == 0`):
+        // re-reading the same word changes no result, only the fetch count
+        cached |= COUNT ? (need & LM_OF((r.cd16 | r.first) != 0u)) : need;
         // node-independent work first: it overlaps the fetch (waited for at the first use of cd16)
         const float tx = r.px * r.cx - r.bx;             // N:67-70
         const float ty = r.py * r.cy - r.by;
@@ -486,10 +321,6 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const float tc_max = fminf(fminf(tx, ty), tz);
         const float tv_max = vmin(r.t_max, tc_max);
         const float half = r.sexp * 0.5f;                // N:111-116
-        // tx_center = half * tx_coef + tx_corner (N:111-113) as one fma: half is a power of
-        // two >= 2^-23 and |tx_coef| >= 1, so half * tx_coef is exact (no rounding, no
-        // underflow) and the fused result equals the two-rounding HLSL form bit for bit
-        // (NaN payloads aside, which only meet the comparison)
         const lmask cx = LM_OF(center(half, r.cx, tx) > r.t_min);
         const lmask cy = LM_OF(center(half, r.cy, ty) > r.t_min);
         const lmask cz = LM_OF(center(half, r.cz, tz) > r.t_min);
@@ -509,10 +340,9 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         }
         if (LM_ON(store & ~of)) {                        // N:97-98 (raw; round trip on POP)
             // slot = scale - scale_lo = (bits(scale_exp2) >> 23) - 104 - scale_lo; two dwords by
-            // ds_write2_b32: no copy into an aligned register pair
-            // V2: scale_exp2 is an exact power of two (zero mantissa), so the shift needs no mask
-            const uint32_t a = V2 ? push_base + (__float_as_uint(r.sexp) >> SLOT_SH)
-                                  : push_base + (__float_as_uint(r.sexp) >> 23) * SLOT;
+            // ds_write2_b32: no copy into an aligned register pair.  scale_exp2 is an exact
+            // power of two (zero mantissa), so the shift needs no mask
+            const uint32_t a = push_base + (__float_as_uint(r.sexp) >> SLOT_SH);
             asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(r.t_max) : "memory");
         }
         const lmask sx = adv & lx;                       // N:122-125
@@ -548,28 +378,15 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             // bookkeeping and copies of values live on both sides); the popping
             // lanes take the results.  Other lanes read an in-range slot.
             if (DIAG) diag->pop_trips += 1;
-            uint32_t diff;
-            if (V2) {
-                // stepped axis: q + scale_exp2 == o exactly (multiples of scale_exp2 in [0.5, 2));
-                // unstepped axis: q == o, xor 0 -- N:135-137 without masks or re-adds
-                diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) | (__float_as_uint(oy) ^ __float_as_uint(qy)) |
-                       (__float_as_uint(oz) ^ __float_as_uint(qz));
-            } else {
-                const uint32_t dx = LM_ON(sx) ? (__float_as_uint(qx) ^ __float_as_uint(qx + se)) : 0u;
-                const uint32_t dy = LM_ON(sy) ? (__float_as_uint(qy) ^ __float_as_uint(qy + se)) : 0u;
-                const uint32_t dz = LM_ON(sz) ? (__float_as_uint(qz) ^ __float_as_uint(qz + se)) : 0u;
-                diff = dx | dy | dz;
-            }
+            // stepped axis: q + scale_exp2 == o exactly (multiples of scale_exp2 in [0.5, 2));
+            // unstepped axis: q == o, xor 0 -- N:135-137 without masks or re-adds
+            const uint32_t diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) |
+                                  (__float_as_uint(oy) ^ __float_as_uint(qy)) |
+                                  (__float_as_uint(oz) ^ __float_as_uint(qz));
             const uint32_t fd = __float_as_uint((float)diff);
-            const uint32_t ef = V2 ? __builtin_amdgcn_ubfe(fd, 23, 8) : fd >> 23;   // scale + 127
+            const uint32_t ef = __builtin_amdgcn_ubfe(fd, 23, 8);   // scale + 127
             const int scale = (int)ef - 127;
-            uint2 e;
-            if (V2) {
-                e = stk_pop[min(ef, e_max) * STRIDE];   // e_max: leaving the root
-            } else {
-                const int slot = min(max(scale - scale_lo, 0), slots);
-                e = stk[slot * STRIDE];                  // slot == slots only when leaving the root
-            }
+            const uint2 e = stk_pop[min(ef, e_max) * STRIDE];   // e_max: leaving the root
             uint32_t pa = e.x, tm = e.y;
             if (MODE == 0) {                             // int2 <- float2((int)parent, asint(t_max))
                 if (GUARD) pa = (uint32_t)cvt_i32((float)(int32_t)pa);
@@ -580,19 +397,14 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
             const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
             const bool pl = LM_ON(pop);
-            r.sexp = pl ? __uint_as_float(V2 ? (ef << 23) - (23u << 23) : (fd & 0x7F800000u) - (23u << 23)) : r.sexp;
+            r.sexp = pl ? __uint_as_float((ef << 23) - (23u << 23)) : r.sexp;
             r.parent = pl ? pa : r.parent;
             r.t_max = pl ? __uint_as_float(tm) : r.t_max;
-            if (V2) {   // one select of the mask, then in-place ands (r.p == q here)
-                const uint32_t k = pl ? keep : 0xFFFFFFFFu;
-                r.px = __uint_as_float(__float_as_uint(r.px) & k);
-                r.py = __uint_as_float(__float_as_uint(r.py) & k);
-                r.pz = __uint_as_float(__float_as_uint(r.pz) & k);
-            } else {
-                r.px = pl ? __uint_as_float(__float_as_uint(qx) & keep) : r.px;
-                r.py = pl ? __uint_as_float(__float_as_uint(qy) & keep) : r.py;
-                r.pz = pl ? __uint_as_float(__float_as_uint(qz) & keep) : r.pz;
-            }
+            // one select of the mask, then in-place ands (r.p == q here)
+            const uint32_t k = pl ? keep : 0xFFFFFFFFu;
+            r.px = __uint_as_float(__float_as_uint(r.px) & k);
+            r.py = __uint_as_float(__float_as_uint(r.py) & k);
+            r.pz = __uint_as_float(__float_as_uint(r.pz) & k);
             r.h = pl ? 0.0f : r.h;
             sh = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) ^ oct : sh;
             out = pop & LM_OF(scale >= S_MAX);
@@ -609,62 +421,80 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     if (LM_ON(ovf)) r.flags |= 4u;
 }
 
-// The hit record words and the Shade colour of a finished ray.
-__device__ __forceinline__ void record(const LaunchParams &p, const Ray &r, uint32_t w[6], float rgb[3]) {
+// Everything one finished primary ray writes.
+struct Record {
+    uint32_t w[6];      // the svo_hit words; w[0..2] = the compact record
+    float rgb[3];       // Result colour (alpha 1)
+    float pos[3];       // bestHit.position (misses: 0, CreateRayHit)
+    unsigned long long key;   // voxel key (misses: all ones)
+};
+
+// N:158-186 hit decode + R:93-127 Shade.  (x, gy): the pixel, for the hit
+// position's ray origin (recomputed, not kept live through the loop).
+__device__ __forceinline__ void record(const LaunchParams &p, const Ray &r, int x, int gy, Record &o) {
+    o.pos[0] = o.pos[1] = o.pos[2] = 0.0f;
+    o.key = ~0ull;
     if (r.scale >= S_MAX) {
-        w[0] = 0xFFFFFFFFu;
-        w[1] = (r.flags & 0xFFFFu) << 16;
-        w[2] = 0x7F800000u;
-        w[3] = 0u; w[4] = 0u; w[5] = 0u;
-        // procedural sky (the reference's skybox assets are missing), == orc_sky
-        const float k = 0.5f * r.dir_y + 0.5f;
-        rgb[0] = 0.25f + 0.5f * k;
-        rgb[1] = 0.35f + 0.55f * k;
-        rgb[2] = 0.6f + 0.4f * k;
-    } else {
-        const float t_min = r.t_min * 32.0f;
-        const int hit_idx = r.idx ^ r.octant_mask ^ 7;
-        const uint2 a = p.att[r.parent];
-        float n[3];
-        decode_normal(a.y >> 16, n);
-        normalize3(n);
-        w[0] = r.parent;
-        w[1] = (uint32_t)hit_idx | ((uint32_t)r.scale << 8) | (((r.flags | 1u) & 0xFFFFu) << 16);
-        w[2] = (uint32_t)__float_as_int(t_min * 64.0f);
-        w[3] = (uint32_t)__float_as_int(n[0]);
-        w[4] = (uint32_t)__float_as_int(n[1]);
-        w[5] = (uint32_t)__float_as_int(n[2]);
-        rgb[0] = rgb[1] = rgb[2] = 0.0f;
-        if (p.rgba) {
-            float alb[3];
-            decode_dxt(a.x, a.y, hit_idx, alb);
-            float d = n[0] * p.cam.light[0];
-            d = d + n[1] * p.cam.light[1];
-            d = d + n[2] * p.cam.light[2];
-            float s = d * -1.0f;
-            s = fminf(fmaxf(s, 0.0f), 1.0f);
-            s = s * p.cam.light[3];
-            rgb[0] = s * alb[0]; rgb[1] = s * alb[1]; rgb[2] = s * alb[2];
+        o.w[0] = 0xFFFFFFFFu;
+        o.w[1] = (r.flags & 0xFFFFu) << 16;
+        o.w[2] = 0x7F800000u;
+        o.w[3] = 0u; o.w[4] = 0u; o.w[5] = 0u;
+        sky(r.dir_y, o.rgb);
+        return;
+    }
+    const float t_min = r.t_min * 32.0f;                  // N:163
+    const int hit_idx = r.idx ^ r.octant_mask ^ 7;        // N:176
+    const uint2 a = p.att[r.parent];                      // N:177-178
+    float n[3];
+    decode_normal(a.y >> 16, n);
+    normalize3(n);
+    o.w[0] = r.parent;
+    o.w[1] = (uint32_t)hit_idx | ((uint32_t)r.scale << 8) | (((r.flags | 1u) & 0xFFFFu) << 16);
+    o.w[2] = (uint32_t)__float_as_int(t_min * 64.0f);    // N:171
+    o.w[3] = (uint32_t)__float_as_int(n[0]);
+    o.w[4] = (uint32_t)__float_as_int(n[1]);
+    o.w[5] = (uint32_t)__float_as_int(n[2]);
+    o.rgb[0] = o.rgb[1] = o.rgb[2] = 0.0f;
+    if (p.out.rgba || p.out.rgba8) {
+        float alb[3];
+        decode_dxt(a.x, a.y, hit_idx, alb);
+        shade_hit(p.cam, n, alb, o.rgb);
+    }
+    if (p.out.position || p.out.voxel) {
+        // N:165-174: undo the mirroring, then clamp the (x32-scaled, reference quirk)
+        // hit point into the voxel and scale it by 64.  Voxel key: the un-mirrored
+        // corner's mantissa bits at the leaf scale (exact: positions are dyadic).
+        float org[3], dir[3];
+        camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
+        const float se = r.scale_exp2;
+        float q[3] = { r.px, r.py, r.pz };
+        unsigned long long key = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (((r.octant_mask >> k) & 1) == 0) q[k] = (3.0f - se) - q[k];
+            const float hp = to_svo(org[k]) + t_min * dir[k];
+            const float lo = q[k] + 0.00000001f;
+            const float hi = (q[k] + se) - 0.00000001f;
+            const float c = fminf(fmaxf(hp, lo), hi);
+            o.pos[k] = (c - 1.5f) * 64.0f;
+            key |= (unsigned long long)((__float_as_uint(q[k]) & 0x7FFFFFu) >> r.scale) << (21 * k);
         }
+        o.key = key;
     }
 }
 
-__device__ __forceinline__ void store_record(const LaunchParams &p, size_t out, const uint32_t w[6], const float rgb[3]) {
-    if (p.hits) {
-        uint2 *dst = reinterpret_cast<uint2 *>(p.hits + out);
-        dst[0] = make_uint2(w[0], w[1]);
-        dst[1] = make_uint2(w[2], w[3]);
-        dst[2] = make_uint2(w[4], w[5]);
+__device__ __forceinline__ void store_outputs(const Outputs &out, size_t i, const Record &o) {
+    if (out.hits) {
+        uint2 *dst = reinterpret_cast<uint2 *>(out.hits + i);
+        dst[0] = make_uint2(o.w[0], o.w[1]);
+        dst[1] = make_uint2(o.w[2], o.w[3]);
+        dst[2] = make_uint2(o.w[4], o.w[5]);
     }
-    if (p.rgba) p.rgba[out] = make_float4(rgb[0], rgb[1], rgb[2], 1.0f);
-}
-
-// N:158-186 hit decode; R:93-127 Shade; R:167 store
-__device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r, size_t out) {
-    uint32_t w[6];
-    float rgb[3];
-    record(p, r, w, rgb);
-    store_record(p, out, w, rgb);
+    if (out.compact) reinterpret_cast<uint3 *>(out.compact)[i] = make_uint3(o.w[0], o.w[1], o.w[2]);
+    if (out.rgba) out.rgba[i] = make_float4(o.rgb[0], o.rgb[1], o.rgb[2], 1.0f);
+    if (out.rgba8) out.rgba8[i] = pack_rgba8(o.rgb[0], o.rgb[1], o.rgb[2]);
+    if (out.position) out.position[i] = make_float4(o.pos[0], o.pos[1], o.pos[2], 0.0f);
+    if (out.voxel) out.voxel[i] = o.key;
 }
 
 // Shadow ray of a primary hit (the reference's test is commented
@@ -673,7 +503,7 @@ __device__ __forceinline__ void finish(const LaunchParams &p, const Ray &r, size
 __device__ __forceinline__ void shadow_ray(const LaunchParams &p, int x, int y, uint32_t w_t, uint32_t w_nx,
                                            uint32_t w_ny, uint32_t w_nz, float so[3], float sd[3]) {
     float org[3], dir[3];
-    camera_ray(p, x, y, org, dir);
+    camera_ray(p.cam, p.width, p.height, x, y, org, dir);
     const float tw = __int_as_float((int32_t)w_t) * (1.0f / 64.0f);
     const float n[3] = { __int_as_float((int32_t)w_nx), __int_as_float((int32_t)w_ny), __int_as_float((int32_t)w_nz) };
 #pragma unroll
@@ -689,157 +519,129 @@ __device__ __forceinline__ int global_row(const LaunchParams &p, int lr) {
     return (band * p.band_count + p.band_rank) * p.band_rows + (lr - band * p.band_rows);
 }
 
+__device__ __forceinline__ size_t out_index(const LaunchParams &p, int lr, int gy, int x) {
+    return (size_t)(p.out.frame_layout ? gy : lr) * (size_t)p.width + (size_t)x;
+}
+
 // ------------------------------------------------------------- tile kernel
-// 1-D grid of 16x16-pixel blocks (4 waves x 8x8).  Blocks are dealt round-robin
-// over the 8 XCDs (b and b + 8 share one, MI355X_MICROARCH.md "Workgroup
-// dispatch"); with xcd_remap the blocks that share an XCD cover one contiguous
-// band of screen tiles, so each XCD's private 4 MB L2 holds the SVO nodes of
-// its own screen band instead of every XCD caching the whole visible tree.
-// Placement only changes speed, never results.
-// remap 2: interleaved column strips.  Screen tile columns are grouped into
-// super-columns of G columns; super-column sc belongs to XCD sc % 8.  Blocks
-// b with b % 8 == x land on XCD x (MI355X_MICROARCH.md "Workgroup dispatch"),
-// so XCD x's L2 only caches the nodes seen through its own super-columns, and
-// every XCD samples the whole screen (sky and terrain alike).  Needs the tile
-// columns to be a multiple of 8 G (the host checks).  e = position within the
-// XCD's share, in super-column-major, then column-major order.
-__device__ __forceinline__ int strip_tile(int x, int e, int tiles_x, int tiles_y, int g) {
-    const int per_sc = g * tiles_y, nsc8 = tiles_x / (8 * g);
-    const int m = e / per_sc, within = e - m * per_sc;
-    const int sc = m * 8 + x;
-    const int cix = within / tiles_y;
-    return (within - cix * tiles_y) * tiles_x + sc * g + cix;
-    (void)nsc8;
+// Interleaved XCD column strips (xcd_remap 2).  Workgroups b with b % 8 == x
+// land on XCD x (MI355X_MICROARCH.md "Workgroup dispatch"); tile column c
+// belongs to XCD c % 8, so XCD x's private 4 MB L2 only caches the nodes seen
+// through its own columns while every XCD samples the whole screen (sky and
+// terrain alike).  Needs the tile columns to be a multiple of 8 (the host
+// checks).  e = position within the XCD's share, column-major.
+__device__ __forceinline__ int strip_tile(int x, int e, int tiles_x, int tiles_y) {
+    const int m = e / tiles_y, row = e - m * tiles_y;
+    return row * tiles_x + m * 8 + x;
 }
 
-__device__ __forceinline__ int tile_of_block_strips(int b, int nb, int tiles_x, int g) {
-    return strip_tile(b % 8, b / 8, tiles_x, nb / tiles_x, g);
-}
-
-__device__ __forceinline__ int tile_of_block(int b, int nb, bool remap) {
-    if (!remap) return b;
-    const int q = nb / 8, rem = nb % 8, xcd = b % 8;   // bijective for any nb
-    return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + b / 8;
-}
-
-// FA: the lean V2 loop's unpredicated node loads (p.fetch_all) -- a separate
+// FA: the lean loop's unpredicated node loads (p.fetch_all) -- a separate
 // instantiation, so each form keeps its own register allocation (both loops in
 // one kernel took 82 SGPRs: 7 waves/SIMD, MI355X_MICROARCH.md occupancy table)
 // SH: the shadow pass fused into the same wave -- after its primary rays the wave
-// traces one shadow ray per hit lane (the separate shadow_tile_kernel's work), and
-// the tile's recorded cost is the sum of both, so one cost-ordered launch balances
-// the whole frame (one ramp and one tail instead of two, no second launch).
-template <int MODE, bool COUNT, int STEP, int BS, bool FA = false, bool SH = false>
-__global__ __launch_bounds__(BS) void render_tile_kernel(LaunchParams p, int blocks_x, int remap) {
-    // BS = 256: a block is 16x16 pixels (4 waves of 8x8); 128: 16x8 (2 waves); 64: one 8x8 wave.
-    extern __shared__ uint2 stk_base[];   // [p.slots + 1][BS]
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int t = (STEP >= 3 && BS == 64 && p.tile_order) ? (int)p.tile_order[blockIdx.x]
-                        : remap == 2 && BS == 64 ? tile_of_block_strips((int)blockIdx.x, (int)gridDim.x, blocks_x, p.strip_w)
-                                                 : tile_of_block((int)blockIdx.x, (int)gridDim.x, remap != 0);
-    const int bx = t % blocks_x, by = t / blocks_x;
-    const int x = BS >= 128 ? bx * 16 + (wave & 1) * 8 + (lane & 7) : bx * 8 + (lane & 7);
-    const int lr = BS == 256 ? by * 16 + (wave >> 1) * 8 + (lane >> 3) : by * 8 + (lane >> 3);
+// traces one shadow ray per hit lane, and the tile's recorded cost is the sum of
+// both, so one cost-ordered launch balances the whole frame.
+// COUNT: the instrumented launch (per-ray descriptor fetch counts, no outputs).
+template <int MODE, bool COUNT, bool FA = false, bool SH = false>
+__global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int tiles_x) {
+    extern __shared__ uint2 stk_base[];   // [p.slots + 1][64]
+    const int lane = threadIdx.x;
+    const int n_tiles = (int)gridDim.x;
+    const int t = p.tile_order ? (int)p.tile_order[blockIdx.x]
+                : p.xcd_remap == 2 ? strip_tile((int)blockIdx.x % 8, (int)blockIdx.x / 8, tiles_x, n_tiles / tiles_x)
+                                   : (int)blockIdx.x;
+    const int bx = t % tiles_x, by = t / tiles_x;
+    const int x = bx * 8 + (lane & 7);
+    const int lr = by * 8 + (lane >> 3);
     if (x >= p.width || lr >= p.local_rows) return;
-    if (STEP >= 3 && BS == 64 && p.tile_order && p.prio) {
+    if (p.tile_order && p.prio) {
         // issue priority by the previous launch's cost class: the heaviest tiles
         // bound the launch, so their waves win issue arbitration on a busy SIMD
         const uint32_t n = gridDim.x;
-        const uint32_t b = remap == 2 ? blockIdx.x / 8 : blockIdx.x;
-        const uint32_t *bound = remap == 2 ? p.tile_order + n + 4 + 4 * (blockIdx.x % 8) : p.tile_order + n;
+        const bool strips = p.xcd_remap == 2;
+        const uint32_t b = strips ? blockIdx.x / 8 : blockIdx.x;
+        const uint32_t *bound = strips ? p.tile_order + n + 4 + 4 * (blockIdx.x % 8) : p.tile_order + n;
         if (b < bound[0]) __builtin_amdgcn_s_setprio(3);
         else if (b < bound[1]) __builtin_amdgcn_s_setprio(2);
         else if (b < bound[2]) __builtin_amdgcn_s_setprio(1);
     }
+    const int gy = global_row(p, lr);
     Ray r;
-    init_ray(p, x, global_row(p, lr), r);
-    const int scale_lo = S_MAX - p.slots;
-    uint2 *stk = stk_base + tid;
-    if (STEP >= 3 && !COUNT) {
-        uint32_t t0 = 0;
-        if (p.wave_log) t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-        FRay f;
-        to_fray(r, f);
-        LeanDiag dg;
-        if (!SH && p.wave_log) {
-            if (p.guard) trace_lean<MODE, BS, true, true, STEP == 4>(p, f, stk, &dg);
-            else trace_lean<MODE, BS, false, true, STEP == 4>(p, f, stk, &dg);
-        }
-        else if (p.guard) trace_lean<MODE, BS, true, false, STEP == 4>(p, f, stk);
-        else trace_lean<MODE, BS, false, false, STEP == 4, FA>(p, f, stk);
-        from_fray(f, r);
-        if (SH) {
-            const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
-            uint32_t w[6];
-            float rgb[3];
-            record(p, r, w, rgb);
-            const bool hit = r.scale < S_MAX;
-            const uint64_t hits = __ballot(hit);
-            int trips = f.trips;
-            if (hits) {
-                if (hit) {   // exec = the hit lanes: the lean loop's lanes are exactly these
-                    float so[3], sd[3];
-                    shadow_ray(p, x, global_row(p, lr), w[2], w[3], w[4], w[5], so, sd);
-                    Ray rs;
-                    setup_ray(so, sd, rs);
-                    FRay fs;
-                    to_fray(rs, fs);
-                    if (p.guard) trace_lean<MODE, BS, true, false, true>(p, fs, stk);
-                    else trace_lean<MODE, BS, false, false, true, FA>(p, fs, stk);
-                    from_fray(fs, rs);
-                    if (rs.scale < S_MAX) {   // occluded: flag bit 3, black Result (R:109-111)
-                        w[1] |= 8u << 16;
-                        rgb[0] = rgb[1] = rgb[2] = 0.0f;
-                    }
-                    trips += fs.trips;
+    {
+        float org[3], dir[3];
+        camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
+        setup_ray(org, dir, r);
+    }
+    uint2 *stk = stk_base + lane;
+    uint32_t t0 = 0;
+    if (!COUNT && p.wave_log) t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    FRay f;
+    to_fray(r, f);
+    LeanDiag dg;
+    if (COUNT) trace_lean<MODE, true, false, false, true>(p, f, stk);
+    else if (!SH && p.wave_log) {
+        if (p.guard) trace_lean<MODE, true, true>(p, f, stk, &dg);
+        else trace_lean<MODE, false, true>(p, f, stk, &dg);
+    }
+    else if (p.guard) trace_lean<MODE, true>(p, f, stk);
+    else trace_lean<MODE, false, false, FA>(p, f, stk);
+    from_fray(f, r);
+    if (COUNT) {
+        p.out.fetches[(size_t)lr * (size_t)p.width + (size_t)x] = r.fetches;
+        return;
+    }
+    Record o;
+    record(p, r, x, gy, o);
+    int trips = f.trips;
+    if (SH) {
+        const bool hit = r.scale < S_MAX;
+        const uint64_t hits = __ballot(hit);
+        if (hits) {
+            if (hit) {   // exec = the hit lanes: the lean loop's lanes are exactly these
+                float so[3], sd[3];
+                shadow_ray(p, x, gy, o.w[2], o.w[3], o.w[4], o.w[5], so, sd);
+                Ray rs;
+                setup_ray(so, sd, rs);
+                FRay fs;
+                to_fray(rs, fs);
+                if (p.guard) trace_lean<MODE, true>(p, fs, stk);
+                else trace_lean<MODE, false, false, FA>(p, fs, stk);
+                from_fray(fs, rs);
+                if (rs.scale < S_MAX) {   // occluded: flag bit 3, black Result (R:109-111)
+                    o.w[1] |= 8u << 16;
+                    o.rgb[0] = o.rgb[1] = o.rgb[2] = 0.0f;
                 }
-                trips = __shfl(trips, __ffsll((long long)hits) - 1);   // primary + shadow trips of the wave
+                trips += fs.trips;
             }
-            if (BS == 64 && p.tile_cost && lane == 0) p.tile_cost[t] = (uint16_t)min(trips, 65535);
-            store_record(p, out, w, rgb);
-            return;
-        }
-        if (BS == 64 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every lane
-        if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
-            uint32_t *w = p.wave_log + 8 * ((size_t)blockIdx.x * (BS / 64) + wave);
-            w[0] = t0;
-            w[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-            w[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
-            w[3] = ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFFu) | ((uint32_t)f.trips << 8);
-            w[4] = (uint32_t)dg.loop_cycles;
-            w[5] = (uint32_t)dg.fetch_cycles;
-            w[6] = dg.fetch_trips;
-            w[7] = dg.pop_trips;
-        }
-    } else if (STEP == 1 || STEP >= 3) {
-        while (!step_flat<MODE, COUNT, BS>(p, r, stk, scale_lo, p.slots)) {
-        }
-    } else {
-        while (!step<MODE, COUNT, BS>(p, r, stk, scale_lo)) {
+            trips = __shfl(trips, __ffsll((long long)hits) - 1);   // primary + shadow trips of the wave
         }
     }
-    const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
-    if (COUNT) { p.fetches[out] = r.fetches; return; }
-    finish(p, r, out);
+    if (p.tile_cost && (!SH || lane == 0)) p.tile_cost[t] = (uint16_t)min(trips, 65535);
+    if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
+        uint32_t *w = p.wave_log + 8 * (size_t)blockIdx.x;
+        w[0] = t0;
+        w[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        w[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        w[3] = ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFFu) | ((uint32_t)f.trips << 8);
+        w[4] = (uint32_t)dg.loop_cycles;
+        w[5] = (uint32_t)dg.fetch_cycles;
+        w[6] = dg.fetch_trips;
+        w[7] = dg.pop_trips;
+    }
+    store_outputs(p.out, out_index(p, lr, gy, x), o);
 }
 
 // ------------------------------------------------------------- shadow pass
-// One shadow ray per primary hit (the reference's test is
-// commented out at RaytraceCompute.compute:105-112): world hit point
-// P = o + (t / 64) d, origin P + 0.001 n, direction -L.  An occluded pixel gets
-// flag bit 3 and a black Result (:109-111).  Runs over the same 8x8 tiles as
-// the primary pass: sky tiles retire at once, so no compaction pass is needed.
-template <int MODE, int BS, bool FA = false>
-__global__ __launch_bounds__(BS) void shadow_tile_kernel(LaunchParams p, int blocks_x) {
+// Two-pass form (env SVO_FUSED_SHADOWS=0): one shadow ray per primary hit, read
+// back from the primary pass's records (svo_hit or compact); an occluded pixel
+// gets flag bit 3 and a black Result (R:109-111) in every output.  Same 8x8
+// tiles as the primary pass, cost-ordered by its own recorded trip counts.
+template <int MODE, bool FA = false>
+__global__ __launch_bounds__(TILE) void shadow_tile_kernel(LaunchParams p, int tiles_x) {
     extern __shared__ uint2 stk_base[];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    // cost-ordered like the primary pass (the shadow pass's own recorded trip
-    // counts): heaviest class first, interleaved XCD column strips, s_setprio by class
+    const int lane = threadIdx.x;
     const int t = p.shadow_order ? (int)p.shadow_order[blockIdx.x]
-                : p.xcd_remap == 2 ? tile_of_block_strips((int)blockIdx.x, (int)gridDim.x, blocks_x, p.strip_w)
+                : p.xcd_remap == 2 ? strip_tile((int)blockIdx.x % 8, (int)blockIdx.x / 8, tiles_x, (int)gridDim.x / tiles_x)
                                    : (int)blockIdx.x;
     if (p.shadow_order && p.prio) {
         const bool strips = p.xcd_remap == 2;
@@ -849,160 +651,123 @@ __global__ __launch_bounds__(BS) void shadow_tile_kernel(LaunchParams p, int blo
         else if (b < bound[1]) __builtin_amdgcn_s_setprio(2);
         else if (b < bound[2]) __builtin_amdgcn_s_setprio(1);
     }
-    const int x = (t % blocks_x) * 8 + (lane & 7);
-    const int lr = (t / blocks_x) * 8 + (lane >> 3);
+    const int x = (t % tiles_x) * 8 + (lane & 7);
+    const int lr = (t / tiles_x) * 8 + (lane >> 3);
     const bool inside = x < p.width && lr < p.local_rows;
-    const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
-    uint2 *rec = reinterpret_cast<uint2 *>(p.hits + out);
-    const uint2 w01 = inside ? rec[0] : make_uint2(0u, 0u);
-    const bool hit = (w01.y >> 16) & 1u;
+    const int gy = inside ? global_row(p, lr) : 0;
+    const size_t i = out_index(p, lr, gy, x);
+    uint32_t w1 = 0, w2 = 0;
+    float n[3] = {0.0f, 0.0f, 0.0f};
+    if (inside) {
+        if (p.out.hits) {
+            const uint2 *rec = reinterpret_cast<const uint2 *>(p.out.hits + i);
+            const uint2 a = rec[0], b = rec[1], c = rec[2];
+            w1 = a.y; w2 = b.x;
+            n[0] = __uint_as_float(b.y); n[1] = __uint_as_float(c.x); n[2] = __uint_as_float(c.y);
+        } else {
+            const uint3 c = reinterpret_cast<const uint3 *>(p.out.compact)[i];
+            w1 = c.y; w2 = c.z;
+            if ((w1 >> 16) & 1u) {
+                const uint2 a = p.att[c.x];
+                decode_normal(a.y >> 16, n);
+                normalize3(n);
+            }
+        }
+    }
+    const bool hit = (w1 >> 16) & 1u;
     const bool any_hit = __ballot(hit) != 0;   // whole wave, before any lane leaves
     if (p.shadow_cost && lane == 0 && !any_hit) p.shadow_cost[t] = 0;
     if (!hit) return;
-    const uint2 w23 = rec[1], w45 = rec[2];
     float so[3], sd[3];
-    shadow_ray(p, x, global_row(p, lr), w23.x, w23.y, w45.x, w45.y, so, sd);
+    shadow_ray(p, x, gy, w2, __float_as_uint(n[0]), __float_as_uint(n[1]), __float_as_uint(n[2]), so, sd);
     Ray r;
     setup_ray(so, sd, r);
-    uint2 *stk = stk_base + tid;
+    uint2 *stk = stk_base + lane;
     FRay f;   // the primary rays' lean loop (one wave of shadow rays per tile, parallel directions)
     to_fray(r, f);
-    if (p.guard) trace_lean<MODE, BS, true, false, true>(p, f, stk);
-    else trace_lean<MODE, BS, false, false, true, FA>(p, f, stk);
+    if (p.guard) trace_lean<MODE, true>(p, f, stk);
+    else trace_lean<MODE, false, false, FA>(p, f, stk);
     from_fray(f, r);
     if (p.shadow_cost) p.shadow_cost[t] = (uint16_t)min(f.trips, 65535);   // same value from every tracing lane
     if (r.scale < S_MAX) {   // occluded
-        rec[0] = make_uint2(w01.x, w01.y | (8u << 16));
-        if (p.rgba) p.rgba[out] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+        const uint32_t nw1 = w1 | (8u << 16);
+        if (p.out.hits) reinterpret_cast<uint32_t *>(p.out.hits + i)[1] = nw1;
+        if (p.out.compact) p.out.compact[3 * i + 1] = nw1;
+        if (p.out.rgba) p.out.rgba[i] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+        if (p.out.rgba8) p.out.rgba8[i] = 255u << 24;
     }
 }
 
-// ------------------------------------------------------- persistent kernel
-
-template <int MODE, bool COUNT>
-__global__ __launch_bounds__(BLOCK) void render_persistent_kernel(LaunchParams p, uint32_t *__restrict__ counter,
-                                                                  uint32_t total_rays, int tiles_x) {
-    extern __shared__ uint2 stk_base[];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    uint2 *stk = stk_base + tid;
-    const int scale_lo = S_MAX - p.slots;
-    Ray r;
-    bool active = false;
-    int x = 0, lr = 0;
-    bool exhausted = false;
-    for (;;) {
-        // ---- refill idle lanes (wave-uniform control flow) ----
-        const uint64_t idle = __ballot(!active);
-        if (!exhausted && idle != 0ull) {
-            const uint32_t n_idle = (uint32_t)__popcll(idle);
-            const int leader = __ffsll((long long)idle) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(counter, n_idle);
-            base = (uint32_t)__shfl((int)base, leader);
-            if (base >= total_rays) exhausted = true;
-            if (!active) {
-                const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                const uint32_t ray = base + rank;
-                if (ray < total_rays) {
-                    const uint32_t tile = ray >> 6;
-                    x = (int)(tile % (uint32_t)tiles_x) * 8 + (int)(ray & 7u);
-                    lr = (int)(tile / (uint32_t)tiles_x) * 8 + (int)((ray >> 3) & 7u);
-                    if (x < p.width && lr < p.local_rows) {
-                        init_ray(p, x, global_row(p, lr), r);
-                        active = true;
-                    }
-                }
-            }
-        }
-        if (__ballot(active) == 0ull) {
-            if (exhausted) break;
-            continue;
-        }
-        // ---- trace until too few lanes remain busy ----
-        for (;;) {
-            if (active) {
-                if (step_flat<MODE, COUNT>(p, r, stk, scale_lo, p.slots)) {
-                    const size_t out = (size_t)lr * (size_t)p.width + (size_t)x;
-                    if (COUNT) p.fetches[out] = r.fetches;
-                    else finish(p, r, out);
-                    active = false;
-                }
-            }
-            const int busy = __popcll(__ballot(active));
-            if (busy == 0 || (!exhausted && busy < p.refill_at)) break;
-        }
+// ---------------------------------------------------------- frame assembly
+// svo_assemble_frame: one thread per pixel of the frame (one row per grid y).
+// Row y belongs to band b = y / band_rows, part m = b % n_parts, local row
+// (b / n_parts) * band_rows + y % band_rows of that part.  Parts are read where
+// they lie: a peer device's memory over xGMI (peer access), or this device's.
+__global__ __launch_bounds__(256) void assemble_kernel(AssembleParams a) {
+    const int x = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int y = (int)blockIdx.y;
+    if (x >= a.width) return;
+    const int band = y / a.band_rows;
+    const int m = band % a.n_parts;
+    if (m == a.skip_part) return;
+    const int lr = (band / a.n_parts) * a.band_rows + (y - band * a.band_rows);
+    const size_t src = (size_t)lr * (size_t)a.width + (size_t)x;
+    const size_t dst = (size_t)y * (size_t)a.width + (size_t)x;
+    if (a.part_format == PART_RGBA8) {
+        a.out.rgba8[dst] = reinterpret_cast<const uint32_t *>(a.parts[m])[src];
+        return;
     }
+    const uint3 c = reinterpret_cast<const uint3 *>(a.parts[m])[src];
+    if (a.out.compact) reinterpret_cast<uint3 *>(a.out.compact)[dst] = c;
+    if (!a.out.hits && !a.out.rgba && !a.out.rgba8) return;
+    const bool hit = (c.y >> 16) & 1u;
+    float n[3] = {0.0f, 0.0f, 0.0f}, rgb[3];
+    if (hit) {   // the render kernel's decode + Shade on the display device's replica
+        const uint2 at = c.x < a.n_nodes ? a.att[c.x] : make_uint2(0u, 0u);
+        decode_normal(at.y >> 16, n);
+        normalize3(n);
+        if (a.out.rgba || a.out.rgba8) {
+            if ((c.y >> 16) & 8u) {
+                rgb[0] = rgb[1] = rgb[2] = 0.0f;
+            } else {
+                float alb[3];
+                decode_dxt(at.x, at.y, (int)(c.y & 0xFFu), alb);
+                shade_hit(a.cam, n, alb, rgb);
+            }
+        }
+    } else if (a.out.rgba || a.out.rgba8) {
+        float org[3], dir[3];
+        camera_ray(a.cam, a.width, a.height, x, y, org, dir);
+        sky(dir[1], rgb);
+    }
+    if (a.out.hits) {
+        uint2 *d = reinterpret_cast<uint2 *>(a.out.hits + dst);
+        d[0] = make_uint2(c.x, c.y);
+        d[1] = make_uint2(c.z, __float_as_uint(n[0]));
+        d[2] = make_uint2(__float_as_uint(n[1]), __float_as_uint(n[2]));
+    }
+    if (a.out.rgba) a.out.rgba[dst] = make_float4(rgb[0], rgb[1], rgb[2], 1.0f);
+    if (a.out.rgba8) a.out.rgba8[dst] = pack_rgba8(rgb[0], rgb[1], rgb[2]);
 }
 
 }  // namespace
 
 template <int MODE, bool COUNT>
-static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream, int kernel, uint32_t *counter,
-                                 int max_blocks) {
-    const size_t lds = (size_t)(p.slots + 1) * BLOCK * sizeof(uint2);   // + the dummy slot
-    if (kernel == 0) {
-        if (p.block == 128) {
-            const int bx = (p.width + 15) / 16, by = (p.local_rows + 7) / 8;
-            const size_t lds128 = (size_t)(p.slots + 1) * 128 * sizeof(uint2);
-            if (p.flat == 3)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 128>), dim3((unsigned)(bx * by)), dim3(128),
-                                   lds128, stream, p, bx, p.xcd_remap);
-            else if (p.flat)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 128>), dim3((unsigned)(bx * by)), dim3(128),
-                                   lds128, stream, p, bx, p.xcd_remap);
-            else
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 128>), dim3((unsigned)(bx * by)),
-                                   dim3(128), lds128, stream, p, bx, p.xcd_remap);
-            return hipGetLastError();
-        }
-        if (p.block == 64) {
-            const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
-            const size_t lds64 = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
-            const dim3 grid((unsigned)(bx * by)), block(64);
-            if (p.flat == 4 && !COUNT && p.shadows == 2) {   // shadow pass fused into the primary launch
-                if (p.fetch_all && !p.guard)
-                    hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64, true, true>), grid, block, lds64, stream, p,
-                                       bx, p.xcd_remap);
-                else
-                    hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64, false, true>), grid, block, lds64, stream,
-                                       p, bx, p.xcd_remap);
-            } else if (p.flat == 4 && !COUNT && p.fetch_all && !p.guard)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64, true>), grid, block, lds64, stream, p, bx,
-                                   p.xcd_remap);
-            else if (p.flat == 4)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 4, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
-            else if (p.flat == 3)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
-            else if (p.flat)
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
-            else
-                hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 64>), grid, block, lds64, stream, p, bx, p.xcd_remap);
-            return hipGetLastError();
-        }
-        const int bx = (p.width + 15) / 16, by = (p.local_rows + 15) / 16;
-        if (p.flat == 3)
-            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 3, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
-                               stream, p, bx, p.xcd_remap);
-        else if (p.flat)
-            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 1, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK), lds,
-                               stream, p, bx, p.xcd_remap);
+static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
+    const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
+    const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2);   // + the spare slot
+    const dim3 grid((unsigned)(bx * by)), block(TILE);
+    if (COUNT)
+        hipLaunchKernelGGL((render_tile_kernel<MODE, true>), grid, block, lds, stream, p, bx);
+    else if (p.shadows == 2) {   // shadow pass fused into the primary launch
+        if (p.fetch_all && !p.guard)
+            hipLaunchKernelGGL((render_tile_kernel<MODE, false, true, true>), grid, block, lds, stream, p, bx);
         else
-            hipLaunchKernelGGL((render_tile_kernel<MODE, COUNT, 0, 256>), dim3((unsigned)(bx * by)), dim3(BLOCK),
-                               lds, stream, p, bx, p.xcd_remap);
-        return hipGetLastError();
-    }
-    const int tiles_x = (p.width + 7) / 8;
-    const int tiles_y = (p.local_rows + 7) / 8;
-    const uint32_t total = (uint32_t)tiles_x * (uint32_t)tiles_y * 64u;
-    hipError_t e = hipMemsetAsync(counter, 0, 16, stream);
-    if (e != hipSuccess) return e;
-    // Over-subscribe: blocks beyond the resident set start when others retire and
-    // find the counter drained (no inter-block dependency, so residency is free).
-    int blocks = (int)std::min<long long>((long long)max_blocks * p.blocks_per_cu, ((long long)total + BLOCK - 1) / BLOCK);
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((render_persistent_kernel<MODE, COUNT>), dim3(blocks), dim3(BLOCK), lds, stream, p, counter,
-                       total, tiles_x);
+            hipLaunchKernelGGL((render_tile_kernel<MODE, false, false, true>), grid, block, lds, stream, p, bx);
+    } else if (p.fetch_all && !p.guard)
+        hipLaunchKernelGGL((render_tile_kernel<MODE, false, true>), grid, block, lds, stream, p, bx);
+    else
+        hipLaunchKernelGGL((render_tile_kernel<MODE, false>), grid, block, lds, stream, p, bx);
     return hipGetLastError();
 }
 
@@ -1106,13 +871,11 @@ size_t order_cost_capacity(int n_tiles) {
     return ((size_t)n_tiles + ORDER_CHUNK - 1) / ORDER_CHUNK * ORDER_CHUNK;
 }
 
-// XCD strips (remap 2): workgroup x orders the tiles of chunk x (the strip
-// that lands on XCD x, see tile_of_block_strips) heaviest class first and
-// writes them to the block positions b = 8 j + x; the per-XCD class ends (in
-// units of j) go to order[n + 4 + 4 x + c].
+// XCD strips (remap 2): workgroup x orders the tiles of XCD x's column strips
+// (see strip_tile) heaviest class first and writes them to the block positions
+// b = 8 j + x; the per-XCD class ends (in units of j) go to order[n + 4 + 4 x + c].
 __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint16_t *__restrict__ cost,
-                                                                     uint32_t *__restrict__ order, int n, int tiles_x,
-                                                                     int g) {
+                                                                     uint32_t *__restrict__ order, int n, int tiles_x) {
     __shared__ uint32_t red[ORDER_THREADS / 64];
     constexpr int NC = 6;
     __shared__ uint32_t cnt[NC], base[NC];
@@ -1129,10 +892,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         w.e += ORDER_THREADS; w.c += dc; w.r += dr;
         if (w.r >= tiles_y) { w.r -= tiles_y; w.c += 1; }
     };
-    auto tile_of = [&](const Walk &w) {
-        const int m = g == 1 ? w.c : w.c / g, cix = g == 1 ? 0 : w.c - m * g;
-        return w.r * tiles_x + (m * 8 + x) * g + cix;
-    };
+    auto tile_of = [&](const Walk &w) { return w.r * tiles_x + w.c * 8 + x; };
     uint32_t mx = 0;
     for (Walk w = start(); w.e < len; next(w)) mx = max(mx, (uint32_t)cost[tile_of(w)]);
 #pragma unroll
@@ -1168,11 +928,9 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     }
 }
 
-hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, int strip_w,
-                               hipStream_t stream) {
+hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream) {
     if (n_tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
-                       strip_w);
+    hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x);
     return hipGetLastError();
 }
 
@@ -1213,32 +971,38 @@ hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32
     return hipGetLastError();
 }
 
-template <int MODE>
-static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
-    const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
-    const size_t lds = (size_t)(p.slots + 1) * 64 * sizeof(uint2);
-    if (p.fetch_all && !p.guard)
-        hipLaunchKernelGGL((shadow_tile_kernel<MODE, 64, true>), dim3((unsigned)(bx * by)), dim3(64), lds, stream, p, bx);
-    else
-        hipLaunchKernelGGL((shadow_tile_kernel<MODE, 64>), dim3((unsigned)(bx * by)), dim3(64), lds, stream, p, bx);
+hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
+    if (a.width <= 0 || a.height <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((a.width + 255) / 256), (unsigned)a.height);
+    hipLaunchKernelGGL(assemble_kernel, grid, dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
-hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel, uint32_t *counter,
-                         int num_cus, hipEvent_t primary_start, hipEvent_t primary_end) {
+template <int MODE>
+static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
+    const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
+    const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2);
+    if (p.fetch_all && !p.guard)
+        hipLaunchKernelGGL((shadow_tile_kernel<MODE, true>), dim3((unsigned)(bx * by)), dim3(TILE), lds, stream, p, bx);
+    else
+        hipLaunchKernelGGL((shadow_tile_kernel<MODE>), dim3((unsigned)(bx * by)), dim3(TILE), lds, stream, p, bx);
+    return hipGetLastError();
+}
+
+hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, hipEvent_t primary_start,
+                         hipEvent_t primary_end) {
     // primary_start / primary_end (nullable): events around the primary-ray kernel only
-    const bool count = p.fetches != nullptr;
+    const bool count = p.out.fetches != nullptr;
     hipError_t e = hipSuccess;
     if (primary_start && (e = hipEventRecord(primary_start, stream)) != hipSuccess) return e;
     if (stack_mode == 0)
-        e = count ? launch_variant<0, true>(p, stream, kernel, counter, num_cus)
-                  : launch_variant<0, false>(p, stream, kernel, counter, num_cus);
+        e = count ? launch_variant<0, true>(p, stream) : launch_variant<0, false>(p, stream);
     else
-        e = count ? launch_variant<1, true>(p, stream, kernel, counter, num_cus)
-                  : launch_variant<1, false>(p, stream, kernel, counter, num_cus);
+        e = count ? launch_variant<1, true>(p, stream) : launch_variant<1, false>(p, stream);
     if (e != hipSuccess) return e;
     if (primary_end && (e = hipEventRecord(primary_end, stream)) != hipSuccess) return e;
-    if (!count && p.shadows == 1 && p.hits) return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
+    if (!count && p.shadows == 1 && (p.out.hits || p.out.compact))
+        return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
     return hipSuccess;
 }
 

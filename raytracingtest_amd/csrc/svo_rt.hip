@@ -13,6 +13,14 @@
 //   att   : uint2[N]  .x = colorA565 | colorB565 << 16, .y = choices16 | normal16 << 16
 //           (NaiveCreator.cs:189-191), one 8-byte load per hit.
 //
+// Multi-device contexts (svo_create_multi): one node-pool replica per device;
+// a frame is split into band_rows-row bands dealt round-robin to the devices;
+// the display device (devices[0]) renders its bands straight into the caller's
+// frame, every other device into a band-contiguous payload (12-byte compact
+// records, or RGBA8 for display-only frames), and one assemble kernel on the
+// display device pulls the payloads over xGMI (peer access) and rebuilds the
+// frame's rows.  All of it is enqueued on streams; nothing blocks the host.
+//
 // Numerics: compiled with -ffp-contract=off and correctly rounded f32 div/sqrt
 // so every expression rounds exactly as the strict-IEEE oracle (oracle/).
 #include <hip/hip_runtime.h>
@@ -51,6 +59,14 @@ struct Upload {
     bool tree;       // every node reached once from the upload's first node (no sharing, no cycles)
 };
 
+enum { STAGE_KERNEL = 0, STAGE_ASSEMBLE = 1, N_STAGES = 2 };
+
+struct Peer {                       // one per member of a multi-device context (index 0: the display device)
+    void *buf[2] = {nullptr, nullptr};   // band payload, double-buffered across frames
+    size_t cap_bytes = 0;
+    hipEvent_t rendered[2] = {nullptr, nullptr};
+};
+
 }  // namespace
 
 struct svo_ctx {
@@ -71,20 +87,13 @@ struct svo_ctx {
     void *d_out_hits = nullptr;
     void *d_out_rgba = nullptr;
     size_t out_cap_px = 0;
-    uint32_t *d_counter = nullptr;   // persistent-kernel work counter (16 B, zeroed per launch)
     int num_cus = 256;
-    int kernel = 0;                  // 0 = tile (default), 1 = persistent; env SVO_KERNEL=tile|persistent
-    int refill_at = 40;              // env SVO_REFILL
-    int blocks_per_cu = 8;           // env SVO_BLOCKS_PER_CU
-    int xcd_remap = 2;               // env SVO_XCD_REMAP: 2 interleaved column strips (default), 1 row bands, 0 off
-    int strip_w = 1;                 // env SVO_STRIP_W: tile columns per strip (xcd_remap 2)
-    int flat = 4;                    // env SVO_FLAT: 4 lean V2 (default), 3 lean, 1 flat, 0 branchy
-    int block = 64;                  // env SVO_BLOCK (64 | 256)
+    int xcd_remap = 2;               // env SVO_XCD_REMAP: 2 interleaved column strips (default), 0 raster
     uint32_t options = 0;            // svo_set_options
-    // SVO_OPT_KERNEL_TIMING: event pairs around the primary kernel of each launch
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> timing_events;   // recorded, not yet read
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> timing_free;     // reusable
-    uint32_t *d_wave_log = nullptr;  // diagnostics: env SVO_WAVE_LOG=<file> (tile kernel, SVO_FLAT=3)
+    // SVO_OPT_KERNEL_TIMING: event pairs around the primary kernel / the assemble kernel
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timing_events[N_STAGES];   // recorded, not yet read
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timing_free;               // reusable
+    uint32_t *d_wave_log = nullptr;  // diagnostics: env SVO_WAVE_LOG=<file>
     size_t wave_log_cap = 0;
     // Cost-ordered tile dispatch: every launch records each 8x8 tile's trip
     // count; the order kernel, enqueued right behind it, turns them into the
@@ -94,21 +103,35 @@ struct svo_ctx {
     int shadow_order_enabled = 1;    // env SVO_SHADOW_ORDER=0: shadow tiles in plain strip order
     int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
     int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
-    int order_every = 8;             // env SVO_ORDER_EVERY: rebuild the order every k-th launch (~20 us one-CU kernel)
+    int order_every = 8;             // env SVO_ORDER_EVERY: rebuild the order every k-th launch
     unsigned long long order_launches = 0;
     uint16_t *d_tile_cost = nullptr;
     uint32_t *d_tile_order = nullptr;
-    uint16_t *d_shadow_cost = nullptr;   // the shadow pass's own costs and order
+    uint16_t *d_shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
     uint32_t *d_shadow_order = nullptr;
     long long shadow_order_key = -1;
     unsigned long long shadow_launches = 0;
     size_t tile_cap = 0;
     long long order_key = -1;        // geometry d_tile_order was built for (-1: none)
-    hipStream_t order_stream = nullptr;   // stream of the last order kernel (a launch elsewhere syncs it first)
-    bool order_pending = false;
+    // Work of one context is ordered across streams: the cost / order buffers,
+    // the scratch outputs and the node pool are shared by all its launches, so
+    // the first launch (or upload) on a new stream waits for everything enqueued
+    // on the previous one (an event recorded at the switch; no host sync).
+    hipStream_t last_stream = nullptr;
+    bool last_valid = false;
+    hipEvent_t switch_event = nullptr;
+    // multi-device context (svo_create_multi); empty for a single-device one
+    std::vector<svo_ctx *> members;
+    std::vector<Peer> peers;
+    hipEvent_t gathered[2] = {nullptr, nullptr};
+    bool gathered_used[2] = {false, false};
+    int parity = 0;
+    int band_rows = 8;
 };
 
 namespace {
+
+bool is_multi(const svo_ctx *ctx) { return !ctx->members.empty(); }
 
 // V1 (relative, int32) -> device node (absolute, uint2).  NaiveCreator.cs:184-187.
 __global__ void convert_v1_kernel(const int32_t *__restrict__ desc, uint2 *__restrict__ nodes,
@@ -123,8 +146,27 @@ __global__ void convert_v1_kernel(const int32_t *__restrict__ desc, uint2 *__res
     nodes[base + i] = o;
 }
 
+// Make stream s wait for all work this context enqueued on another stream.
+int order_streams(svo_ctx *ctx, hipStream_t s) {
+    if (ctx->last_valid && ctx->last_stream != s) {
+        if (!ctx->switch_event) HIP_TRY(hipEventCreateWithFlags(&ctx->switch_event, hipEventDisableTiming));
+        if (hipEventRecord(ctx->switch_event, ctx->last_stream) == hipSuccess) {
+            HIP_TRY(hipStreamWaitEvent(s, ctx->switch_event, 0));
+        } else {   // the previous stream is gone: wait for the whole device instead
+            (void)hipGetLastError();
+            HIP_TRY(hipDeviceSynchronize());
+        }
+    }
+    ctx->last_stream = s;
+    ctx->last_valid = true;
+    return SVO_OK;
+}
+
 // Host-side level walk: validates every non-leaf child index and returns the
-// number of descriptor levels reachable from the upload's first node.
+// number of descriptor levels reachable from the upload's first node.  A
+// breadth-first walk with a seen set: exact for a tree; for a DAG it is the
+// shallowest depth, so such pools are traversed with the full stack
+// (recompute_depth).
 int walk_depth(const uint32_t *lo, const uint32_t *first, size_t n, size_t base, size_t pool_n,
                int *depth_out, bool *external_out, bool *tree_out, std::string *err) {
     *tree_out = true;
@@ -165,39 +207,43 @@ int walk_depth(const uint32_t *lo, const uint32_t *first, size_t n, size_t base,
 }
 
 void recompute_depth(svo_ctx *ctx) {
-    int root_depth = 0, other = 0;
-    bool ext = false;
-    for (const Upload &u : ctx->uploads) {
+    int root_depth = 0;
+    for (const Upload &u : ctx->uploads)
         if (u.offset == 0) root_depth = std::max(root_depth, u.depth);
-        else other = std::max(other, u.depth);
-        ext = ext || u.external;
-    }
-    ctx->depth = root_depth + (ext ? other : 0);
-    if (ctx->depth > 22) ctx->depth = 22;
-    // A single self-contained tree at offset 0: every descent path has at most
-    // `depth` levels, so the traversal stack cannot overflow while parents are
-    // exact (the kernel may then drop its overflow guard).
+    // A single self-contained tree at offset 0: every descent path has exactly its
+    // walked depth, so the traversal stack needs depth - 1 slots and cannot overflow
+    // while parents are exact (the kernel may then drop its overflow guard).  Any
+    // other pool -- a DAG (the walk saw a node twice, so its depth is only the
+    // shallowest path), linked sub-pools, several uploads -- gets the full 22-slot
+    // stack of the reference (stack[s_max + 1], NVIDIASVO.compute:13).
     ctx->depth_exact = ctx->uploads.size() == 1 && ctx->uploads[0].offset == 0 && !ctx->uploads[0].external &&
-                       ctx->uploads[0].tree && ctx->depth <= 22 && root_depth == ctx->depth;
+                       ctx->uploads[0].tree && root_depth <= 22;
+    ctx->depth = ctx->depth_exact ? root_depth : 22;
 }
 
-int record_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, size_t n, size_t base) {
+int validate_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, size_t n, size_t base, Upload *out) {
     std::string err;
     int depth = 0;
     bool ext = false, tree = true;
     size_t pool_n = std::max(ctx->n_nodes, base + n);
     if (walk_depth(lo, first, n, base, pool_n, &depth, &ext, &tree, &err) != 0) return fail(SVO_ERR_FORMAT, err);
-    ctx->uploads.erase(std::remove_if(ctx->uploads.begin(), ctx->uploads.end(),
-                                      [&](const Upload &u) { return u.offset == base; }),
-                       ctx->uploads.end());
-    ctx->uploads.push_back({base, n, depth, ext, tree});
-    ctx->n_nodes = pool_n;
-    recompute_depth(ctx);
+    *out = Upload{base, n, depth, ext, tree};
     return SVO_OK;
+}
+
+// Commit an upload's metadata -- only after its device copies have completed.
+void commit_upload(svo_ctx *ctx, const Upload &u) {
+    ctx->uploads.erase(std::remove_if(ctx->uploads.begin(), ctx->uploads.end(),
+                                      [&](const Upload &v) { return v.offset == u.offset; }),
+                       ctx->uploads.end());
+    ctx->uploads.push_back(u);
+    ctx->n_nodes = std::max(ctx->n_nodes, u.offset + u.count);
+    recompute_depth(ctx);
 }
 
 int ensure_out(svo_ctx *ctx, size_t px) {
     if (px <= ctx->out_cap_px) return SVO_OK;
+    HIP_TRY(hipDeviceSynchronize());   // an earlier asynchronous launch may still use the old scratch
     if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
     ctx->d_out_hits = ctx->d_out_rgba = nullptr;
@@ -225,10 +271,43 @@ int check_band(const svo_band *band, int height, svo_band *out) {
     return SVO_OK;
 }
 
-int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band,
-           void *d_rgba, void *d_hits, uint32_t *d_fetch, hipStream_t stream) {
+int take_events(svo_ctx *ctx, int stage, hipEvent_t *ev0, hipEvent_t *ev1) {
+    *ev0 = *ev1 = nullptr;
+    if (!(ctx->options & SVO_OPT_KERNEL_TIMING)) return SVO_OK;
+    if (ctx->timing_free.empty()) {
+        HIP_TRY(hipEventCreate(ev0));
+        if (hipEventCreate(ev1) != hipSuccess) {
+            hipEventDestroy(*ev0);
+            *ev0 = nullptr;
+            return fail(SVO_ERR_HIP, "hipEventCreate");
+        }
+    } else {
+        *ev0 = ctx->timing_free.back().first;
+        *ev1 = ctx->timing_free.back().second;
+        ctx->timing_free.pop_back();
+    }
+    ctx->timing_events[stage].emplace_back(*ev0, *ev1);
+    return SVO_OK;
+}
+
+svo::Outputs outputs_of(const svo_frame *f) {
+    svo::Outputs o{};
+    if (!f) return o;
+    o.hits = reinterpret_cast<svo::Hit *>(f->hits);
+    o.rgba = reinterpret_cast<float4 *>(f->rgba);
+    o.rgba8 = f->rgba8;
+    o.compact = reinterpret_cast<uint32_t *>(f->compact);
+    o.position = reinterpret_cast<float4 *>(f->position);
+    o.voxel = reinterpret_cast<unsigned long long *>(f->voxel);
+    o.frame_layout = f->layout == SVO_LAYOUT_FRAME ? 1 : 0;
+    return o;
+}
+
+int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band, svo::Outputs out,
+           hipStream_t stream) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
     if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
+    if ((size_t)width * (size_t)height > ((size_t)1 << 31)) return fail(SVO_ERR_ARG, "frame larger than 2^31 pixels");
     if (stack_mode != SVO_STACK_HLSL && stack_mode != SVO_STACK_EXACT)
         return fail(SVO_ERR_ARG, "unknown stack mode");
     if (ctx->n_nodes == 0) return fail(SVO_ERR_STATE, "no node pool uploaded (svo_set_buffer)");
@@ -238,6 +317,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     if (rc) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
     svo::LaunchParams p;
+    std::memset(&p, 0, sizeof p);
     p.nodes = ctx->d_nodes;
     p.att = ctx->d_att;
     p.n_nodes = (uint32_t)std::min<size_t>(ctx->n_nodes, 0xFFFFFFFFu);
@@ -257,37 +337,28 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // unpredicated node loads pay off on pools below 2^24 nodes (C2, C3: 5-9 %) and
     // cost 6-12 % on the 25 M / 100 M-node C4 / C5 pools (svo_kernel.hip trace_lean)
     p.fetch_all = ctx->fetch_all >= 0 ? ctx->fetch_all : (ctx->n_nodes < ((size_t)1 << 24) ? 1 : 0);
-    p.hits = reinterpret_cast<svo::Hit *>(d_hits);
-    p.rgba = reinterpret_cast<float4 *>(d_rgba);
-    p.fetches = d_fetch;
-    p.refill_at = ctx->refill_at;
-    p.blocks_per_cu = ctx->blocks_per_cu;
+    p.out = out;
+    if (b.band_count == 1) p.out.frame_layout = 0;   // the whole frame: both layouts coincide
     p.xcd_remap = ctx->xcd_remap;
-    p.strip_w = ctx->strip_w;
-    if (p.xcd_remap == 2 && (ctx->block != 64 || ((width + 7) / 8) % (8 * p.strip_w) != 0)) p.xcd_remap = 0;
-    p.flat = ctx->flat;
-    p.block = ctx->block;
-    p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? 1 : 0;
-    // fused shadow pass: the 64-thread lean V2 tile kernel with cost ordering (env SVO_FUSED_SHADOWS=0: two passes)
-    if (p.shadows && ctx->fused_shadows && ctx->kernel == 0 && ctx->block == 64 && ctx->flat == 4) p.shadows = 2;
+    if (p.xcd_remap == 2 && ((width + 7) / 8) % 8 != 0) p.xcd_remap = 0;
+    p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? (ctx->fused_shadows ? 2 : 1) : 0;
     if (p.local_rows == 0) return SVO_OK;
-    if (p.shadows == 1 && !p.hits && !p.fetches) {   // the second shadow pass reads the primary hit records
-        int rc2 = ensure_out(ctx, (size_t)p.local_rows * (size_t)width);
+    if (out.fetches) p.shadows = 0;
+    hipStream_t s = stream ? stream : ctx->stream;
+    rc = order_streams(ctx, s);
+    if (rc) return rc;
+    if (p.shadows == 1 && !p.out.hits && !p.out.compact) {   // the second shadow pass reads the primary records
+        int rc2 = ensure_out(ctx, (size_t)(p.out.frame_layout ? height : p.local_rows) * (size_t)width);
         if (rc2) return rc2;
-        p.hits = reinterpret_cast<svo::Hit *>(ctx->d_out_hits);
+        p.out.hits = reinterpret_cast<svo::Hit *>(ctx->d_out_hits);
     }
-    p.wave_log = nullptr;
-    p.tile_order = nullptr;
-    p.tile_cost = nullptr;
-    p.shadow_order = nullptr;
-    p.shadow_cost = nullptr;
     p.prio = ctx->prio;
-    const bool ordered = ctx->tile_order && ctx->kernel == 0 && ctx->flat >= 3 && ctx->block == 64 && !p.fetches;
+    const bool ordered = ctx->tile_order && !p.out.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
     long long key = -1;
     if (ordered) {
         key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^ ((long long)b.band_rows << 8) ^
-              (long long)b.band_rank ^ ((long long)b.band_count << 4) ^ ((long long)ctx->xcd_remap << 60) ^ ((long long)ctx->strip_w << 52);
+              (long long)b.band_rank ^ ((long long)b.band_count << 4) ^ ((long long)p.xcd_remap << 60);
         if (ctx->tile_cap < (size_t)n_tiles) {
             HIP_TRY(hipDeviceSynchronize());   // a pending launch may still use the old buffers
             if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
@@ -310,87 +381,45 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             HIP_TRY(hipMalloc(&ctx->d_shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
             ctx->tile_cap = (size_t)n_tiles;
         }
-        if (const char *f = std::getenv("SVO_ORDER_FILE")) {   // experiments: a fixed host-made order
-            if (ctx->order_key != key) {
-                std::vector<uint32_t> h((size_t)n_tiles + 4, 0u);
-                FILE *fp = std::fopen(f, "rb");
-                if (!fp) return fail(SVO_ERR_ARG, std::string("SVO_ORDER_FILE: cannot open ") + f);
-                const size_t got = std::fread(h.data(), sizeof(uint32_t), (size_t)n_tiles, fp);
-                std::fclose(fp);
-                if (got != (size_t)n_tiles) return fail(SVO_ERR_ARG, "SVO_ORDER_FILE: short file");
-                std::vector<uint8_t> seen((size_t)n_tiles, 0);
-                for (size_t i = 0; i < (size_t)n_tiles; ++i) {
-                    if (h[i] >= (uint32_t)n_tiles || seen[h[i]]) return fail(SVO_ERR_ARG, "SVO_ORDER_FILE: not a permutation");
-                    seen[h[i]] = 1;
-                }
-                HIP_TRY(hipMemcpy(ctx->d_tile_order, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-                ctx->order_key = key;
-            }
-            p.tile_order = ctx->d_tile_order;
-            p.tile_cost = nullptr;
-        } else {
-            p.tile_order = ctx->order_key == key ? ctx->d_tile_order : nullptr;
-        }
-        if (!std::getenv("SVO_ORDER_FILE")) p.tile_cost = ctx->d_tile_cost;
+        p.tile_order = ctx->order_key == key ? ctx->d_tile_order : nullptr;
+        p.tile_cost = ctx->d_tile_cost;
         if (p.shadows == 1 && ctx->shadow_order_enabled) {
             p.shadow_cost = ctx->d_shadow_cost;
             p.shadow_order = ctx->shadow_order_key == key ? ctx->d_shadow_order : nullptr;
         }
     }
     const char *log_path = std::getenv("SVO_WAVE_LOG");
-    const size_t n_wave = (size_t)((width + 15) / 16) * (size_t)((p.local_rows + 15) / 16) * 4;   // >= any tiling
-    if (log_path && !p.fetches) {
+    const size_t n_wave = (size_t)n_tiles;
+    if (log_path && !p.out.fetches) {
         if (ctx->wave_log_cap < n_wave) {
+            HIP_TRY(hipDeviceSynchronize());
             if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
             ctx->d_wave_log = nullptr;
             ctx->wave_log_cap = 0;
             HIP_TRY(hipMalloc(&ctx->d_wave_log, n_wave * 32));
             ctx->wave_log_cap = n_wave;
         }
-        HIP_TRY(hipMemset(ctx->d_wave_log, 0, n_wave * 32));
+        HIP_TRY(hipMemsetAsync(ctx->d_wave_log, 0, n_wave * 32, s));
         p.wave_log = ctx->d_wave_log;
     }
-    hipStream_t s = stream ? stream : ctx->stream;
-    // the cost/order buffers are shared by all launches of the context: launches
-    // on one stream are ordered; switching streams waits for the last order kernel
-    if (p.tile_cost && ctx->order_pending && ctx->order_stream != s) {
-        HIP_TRY(hipStreamSynchronize(ctx->order_stream));
-        ctx->order_pending = false;
-    }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    if ((ctx->options & SVO_OPT_KERNEL_TIMING) && !p.fetches) {
-        if (ctx->timing_free.empty()) {
-            HIP_TRY(hipEventCreate(&ev0));
-            if (hipEventCreate(&ev1) != hipSuccess) {
-                hipEventDestroy(ev0);
-                return fail(SVO_ERR_HIP, "hipEventCreate");
-            }
-        } else {
-            ev0 = ctx->timing_free.back().first;
-            ev1 = ctx->timing_free.back().second;
-            ctx->timing_free.pop_back();
-        }
-        ctx->timing_events.emplace_back(ev0, ev1);
+    if (!p.out.fetches) {
+        rc = take_events(ctx, STAGE_KERNEL, &ev0, &ev1);
+        if (rc) return rc;
     }
-    hipError_t e = svo::launch_render(p, stack_mode, s, ctx->kernel, ctx->d_counter, ctx->num_cus, ev0, ev1);
+    hipError_t e = svo::launch_render(p, stack_mode, s, ev0, ev1);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
     const bool refresh = p.tile_cost && (ctx->order_key != key || ctx->order_launches++ % ctx->order_every == 0);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
-        e = p.xcd_remap == 2 ? svo::launch_order_strips(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, (width + 7) / 8,
-                                                        p.strip_w, s)
-                                : svo::launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, s);
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, (width + 7) / 8, s)
+                             : svo::launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, s);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
-        ctx->order_stream = s;
-        ctx->order_pending = true;
         ctx->order_key = key;
     }
     if (p.shadow_cost && (ctx->shadow_order_key != key || ctx->shadow_launches++ % ctx->order_every == 0)) {
-        e = p.xcd_remap == 2 ? svo::launch_order_strips(ctx->d_shadow_cost, ctx->d_shadow_order, n_tiles, (width + 7) / 8,
-                                                        p.strip_w, s)
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(ctx->d_shadow_cost, ctx->d_shadow_order, n_tiles, (width + 7) / 8, s)
                              : svo::launch_order_tiles(ctx->d_shadow_cost, ctx->d_shadow_order, n_tiles, s);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("shadow order launch: ") + hipGetErrorString(e));
-        ctx->order_stream = s;
-        ctx->order_pending = true;
         ctx->shadow_order_key = key;
     }
     if (p.wave_log) {   // blocking dump of the last launch's per-wave record
@@ -405,11 +434,138 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     return SVO_OK;
 }
 
+// Enqueue the assemble kernel on this context's device (svo_assemble_frame, and
+// the gather of a multi-device frame).
+int assemble(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, const void *const *parts,
+             int part_format, int skip_part, const svo::Outputs &out, hipStream_t s) {
+    svo::AssembleParams a;
+    std::memset(&a, 0, sizeof a);
+    a.att = ctx->d_att;
+    a.n_nodes = (uint32_t)std::min<size_t>(ctx->n_nodes, 0xFFFFFFFFu);
+    a.cam = ctx->cam;
+    a.width = width;
+    a.height = height;
+    a.band_rows = band_rows;
+    a.n_parts = n_parts;
+    a.part_format = part_format;
+    a.skip_part = skip_part;
+    for (int i = 0; i < n_parts; ++i) a.parts[i] = parts[i];
+    a.out = out;
+    a.out.frame_layout = 1;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int rc = take_events(ctx, STAGE_ASSEMBLE, &ev0, &ev1);
+    if (rc) return rc;
+    if (ev0) HIP_TRY(hipEventRecord(ev0, s));
+    hipError_t e = svo::launch_assemble(a, s);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("assemble launch: ") + hipGetErrorString(e));
+    if (ev1) HIP_TRY(hipEventRecord(ev1, s));
+    return SVO_OK;
+}
+
+int check_assemble_args(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, int part_format,
+                        int skip_part, const svo::Outputs &o) {
+    if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
+    if (band_rows <= 0) return fail(SVO_ERR_ARG, "band_rows must be positive");
+    if (n_parts < 1 || n_parts > svo::MAX_PARTS) return fail(SVO_ERR_ARG, "n_parts must be in [1, 64]");
+    if (skip_part < -1 || skip_part >= n_parts) return fail(SVO_ERR_ARG, "skip_part out of range");
+    if (o.position || o.voxel || o.fetches) return fail(SVO_ERR_ARG, "position / voxel outputs are not assembled");
+    if (part_format == SVO_PART_RGBA8) {
+        if (!o.rgba8 || o.hits || o.rgba || o.compact) return fail(SVO_ERR_ARG, "RGBA8 parts rebuild only an RGBA8 frame");
+    } else if (part_format == SVO_PART_COMPACT) {
+        if ((o.hits || o.rgba || o.rgba8) && ctx->n_nodes == 0)
+            return fail(SVO_ERR_STATE, "no node pool uploaded: compact parts need the SVO replica");
+        if ((o.rgba || o.rgba8) && !ctx->cam_set) return fail(SVO_ERR_STATE, "camera not set (svo_set_camera)");
+    } else {
+        return fail(SVO_ERR_ARG, "unknown part format");
+    }
+    return SVO_OK;
+}
+
+// ------------------------------------------------------ multi-device frame
+int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_frame *frame, hipStream_t stream) {
+    const int n = (int)ctx->members.size();
+    svo::Outputs out = outputs_of(frame);
+    out.frame_layout = 1;
+    if (out.position || out.voxel) return fail(SVO_ERR_ARG, "position / voxel outputs are not gathered across devices");
+    if (!out.hits && !out.rgba && !out.rgba8 && !out.compact) return fail(SVO_ERR_ARG, "no output requested");
+    const int fmt = (out.hits || out.rgba || out.compact) ? SVO_PART_COMPACT : SVO_PART_RGBA8;
+    const size_t elem = fmt == SVO_PART_COMPACT ? 12 : 4;
+    const int k = ctx->parity;
+    ctx->parity ^= 1;
+    svo_ctx *m0 = ctx->members[0];
+    hipStream_t s0 = stream ? stream : m0->stream;
+    // the display device renders its own bands straight into the caller's frame
+    svo_band b0{ctx->band_rows, 0, n};
+    int rc = launch(m0, width, height, stack_mode, &b0, out, s0);
+    if (rc) return rc;
+    std::vector<const void *> parts(n, nullptr);
+    for (int i = 1; i < n; ++i) {
+        svo_ctx *m = ctx->members[i];
+        Peer &pr = ctx->peers[i];
+        svo_band bi{ctx->band_rows, i, n};
+        const size_t bytes = (size_t)band_rows_local(height, bi) * (size_t)width * elem;
+        HIP_TRY(hipSetDevice(m->device));
+        if (pr.cap_bytes < bytes) {
+            HIP_TRY(hipSetDevice(m0->device));
+            HIP_TRY(hipStreamSynchronize(s0));     // the assemble of earlier frames reads the old payloads
+            HIP_TRY(hipSetDevice(m->device));
+            HIP_TRY(hipStreamSynchronize(m->stream));
+            for (int j = 0; j < 2; ++j) {
+                if (pr.buf[j]) hipFree(pr.buf[j]);
+                pr.buf[j] = nullptr;
+            }
+            pr.cap_bytes = 0;
+            for (int j = 0; j < 2; ++j) HIP_TRY(hipMalloc(&pr.buf[j], std::max<size_t>(bytes, 16)));
+            pr.cap_bytes = bytes;
+        }
+        if (ctx->gathered_used[k]) HIP_TRY(hipStreamWaitEvent(m->stream, ctx->gathered[k], 0));   // payload k is free
+        svo::Outputs oi{};
+        if (fmt == SVO_PART_COMPACT) oi.compact = reinterpret_cast<uint32_t *>(pr.buf[k]);
+        else oi.rgba8 = reinterpret_cast<uint32_t *>(pr.buf[k]);
+        rc = launch(m, width, height, stack_mode, &bi, oi, m->stream);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(pr.rendered[k], m->stream));
+        parts[i] = pr.buf[k];
+    }
+    HIP_TRY(hipSetDevice(m0->device));
+    for (int i = 1; i < n; ++i) HIP_TRY(hipStreamWaitEvent(s0, ctx->peers[i].rendered[k], 0));
+    rc = order_streams(m0, s0);
+    if (rc) return rc;
+    rc = assemble(m0, width, height, ctx->band_rows, n, parts.data(), fmt, 0, out, s0);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(ctx->gathered[k], s0));
+    ctx->gathered_used[k] = true;
+    return SVO_OK;
+}
+
+int destroy_single(svo_ctx *ctx) {
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->last_valid && ctx->last_stream && ctx->last_stream != ctx->stream) hipDeviceSynchronize();
+    if (ctx->d_nodes) hipFree(ctx->d_nodes);
+    if (ctx->d_att) hipFree(ctx->d_att);
+    if (ctx->d_stage) hipFree(ctx->d_stage);
+    if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
+    if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
+    if (ctx->d_shadow_cost) hipFree(ctx->d_shadow_cost);
+    if (ctx->d_shadow_order) hipFree(ctx->d_shadow_order);
+    for (auto &v : ctx->timing_events)
+        for (auto &ev : v) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+    for (auto &ev : ctx->timing_free) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+    if (ctx->switch_event) hipEventDestroy(ctx->switch_event);
+    if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
+    if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
+    if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return SVO_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
-int svo_abi_version(void) { return 1; }
+int svo_abi_version(void) { return 2; }
 
 const char *svo_last_error(void) { return g_last_error.c_str(); }
 
@@ -429,33 +585,94 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     hipError_t e = hipMalloc(&ctx->d_nodes, capacity_nodes * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&ctx->d_att, capacity_nodes * sizeof(uint2));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&ctx->d_counter, 256);
-    if (e == hipSuccess) e = hipMemset(ctx->d_counter, 0, 256);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (const char *k = std::getenv("SVO_KERNEL")) ctx->kernel = std::strcmp(k, "persistent") == 0 ? 1 : 0;
-    if (const char *k = std::getenv("SVO_REFILL")) ctx->refill_at = std::max(0, std::min(64, std::atoi(k)));
-    if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::max(0, std::min(2, std::atoi(k)));
-    if (const char *k = std::getenv("SVO_STRIP_W")) ctx->strip_w = std::max(1, std::atoi(k));
-    if (const char *k = std::getenv("SVO_FLAT")) ctx->flat = std::max(0, std::min(4, std::atoi(k)));
+    if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) == 0 ? 0 : 2;
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SHADOW_ORDER")) ctx->shadow_order_enabled = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_FETCH_ALL")) ctx->fetch_all = std::atoi(k) != 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_FUSED_SHADOWS")) ctx->fused_shadows = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
-    if (const char *k = std::getenv("SVO_BLOCK")) { const int b = std::atoi(k); ctx->block = (b == 256 || b == 128) ? b : 64; }
-    if (const char *k = std::getenv("SVO_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(64, std::atoi(k)));
     if (e != hipSuccess) {
-        svo_destroy(ctx);
+        destroy_single(ctx);
         return fail(SVO_ERR_HIP, std::string("svo_create: ") + hipGetErrorString(e));
     }
     *out = ctx;
     return SVO_OK;
 }
 
+int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes, int band_rows, svo_ctx **out) {
+    if (!out || !devices) return fail(SVO_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (num_devices < 1 || num_devices > svo::MAX_PARTS) return fail(SVO_ERR_ARG, "num_devices must be in [1, 64]");
+    if (band_rows <= 0) return fail(SVO_ERR_ARG, "band_rows must be positive");
+    svo_ctx *g = new (std::nothrow) svo_ctx();
+    if (!g) return fail(SVO_ERR_ARG, "out of host memory");
+    g->device = devices[0];
+    g->capacity = capacity_nodes;
+    g->band_rows = band_rows;
+    g->peers.resize(num_devices);
+    auto bail = [&](int rc) {
+        svo_destroy(g);
+        return rc;
+    };
+    for (int i = 0; i < num_devices; ++i) {
+        svo_ctx *m = nullptr;
+        int rc = svo_create(devices[i], capacity_nodes, &m);
+        if (rc) return bail(rc);
+        g->members.push_back(m);
+    }
+    // the display device reads every other device's payload over xGMI
+    for (int i = 1; i < num_devices; ++i) {
+        if (devices[i] == devices[0]) continue;
+        int ok = 0;
+        hipError_t e = hipDeviceCanAccessPeer(&ok, devices[0], devices[i]);
+        if (e != hipSuccess || !ok)
+            return bail(fail(SVO_ERR_HIP, "device " + std::to_string(devices[0]) + " cannot access device " +
+                                              std::to_string(devices[i]) + " (no xGMI peer access)"));
+        hipSetDevice(devices[0]);
+        e = hipDeviceEnablePeerAccess(devices[i], 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+        else if (e != hipSuccess) return bail(fail(SVO_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e)));
+    }
+    for (int i = 1; i < num_devices; ++i) {
+        hipSetDevice(devices[i]);
+        for (int j = 0; j < 2; ++j)
+            if (hipEventCreateWithFlags(&g->peers[i].rendered[j], hipEventDisableTiming) != hipSuccess)
+                return bail(fail(SVO_ERR_HIP, "hipEventCreate"));
+    }
+    hipSetDevice(devices[0]);
+    for (int j = 0; j < 2; ++j)
+        if (hipEventCreateWithFlags(&g->gathered[j], hipEventDisableTiming) != hipSuccess)
+            return bail(fail(SVO_ERR_HIP, "hipEventCreate"));
+    *out = g;
+    return SVO_OK;
+}
+
+int svo_num_devices(svo_ctx *ctx, int *n) {
+    if (!ctx || !n) return fail(SVO_ERR_ARG, "null argument");
+    *n = is_multi(ctx) ? (int)ctx->members.size() : 1;
+    return SVO_OK;
+}
+
+int svo_get_member(svo_ctx *ctx, int index, svo_ctx **member) {
+    if (!ctx || !member) return fail(SVO_ERR_ARG, "null argument");
+    const int n = is_multi(ctx) ? (int)ctx->members.size() : 1;
+    if (index < 0 || index >= n) return fail(SVO_ERR_ARG, "member index out of range");
+    *member = is_multi(ctx) ? ctx->members[index] : ctx;
+    return SVO_OK;
+}
+
 int svo_set_buffer(svo_ctx *ctx, const int32_t *desc, size_t n_desc, const uint32_t *att,
                    size_t n_att, size_t dst_offset) {
     if (!ctx || (!desc && n_desc) || (!att && n_att)) return fail(SVO_ERR_ARG, "null argument");
+    if (is_multi(ctx)) {   // one replica per device
+        for (svo_ctx *m : ctx->members) {
+            int rc = svo_set_buffer(m, desc, n_desc, att, n_att, dst_offset);
+            if (rc) return rc;
+        }
+        return SVO_OK;
+    }
     if (dst_offset + n_desc > ctx->capacity || 2 * dst_offset + n_att > 2 * ctx->capacity)
         return fail(SVO_ERR_CAPACITY, "upload exceeds node-pool capacity");
     if (n_att != 2 * n_desc) return fail(SVO_ERR_ARG, "attachments must hold 2 words per descriptor");
@@ -467,10 +684,14 @@ int svo_set_buffer(svo_ctx *ctx, const int32_t *desc, size_t n_desc, const uint3
         lo[i] = cd & 0xFFFFu;
         first[i] = cd ? (uint32_t)(dst_offset + i) + (cd >> 16) : 0u;
     }
-    int rc = record_upload(ctx, lo.data(), first.data(), n_desc, dst_offset);
+    Upload u;
+    int rc = validate_upload(ctx, lo.data(), first.data(), n_desc, dst_offset, &u);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
+    rc = order_streams(ctx, ctx->stream);   // renders on other streams may still read the pool
+    if (rc) return rc;
     if (n_desc > ctx->stage_cap) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
         if (ctx->d_stage) hipFree(ctx->d_stage);
         ctx->d_stage = nullptr;
         ctx->stage_cap = 0;
@@ -485,12 +706,20 @@ int svo_set_buffer(svo_ctx *ctx, const int32_t *desc, size_t n_desc, const uint3
     HIP_TRY(hipMemcpyAsync(ctx->d_att + dst_offset, att, n_att * sizeof(uint32_t), hipMemcpyHostToDevice,
                            ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    commit_upload(ctx, u);
     return SVO_OK;
 }
 
 int svo_set_buffer_v2(svo_ctx *ctx, const uint64_t *nodes, size_t n_nodes, const uint32_t *att,
                       size_t n_att, size_t dst_offset) {
     if (!ctx || (!nodes && n_nodes) || (!att && n_att)) return fail(SVO_ERR_ARG, "null argument");
+    if (is_multi(ctx)) {
+        for (svo_ctx *m : ctx->members) {
+            int rc = svo_set_buffer_v2(m, nodes, n_nodes, att, n_att, dst_offset);
+            if (rc) return rc;
+        }
+        return SVO_OK;
+    }
     if (dst_offset + n_nodes > ctx->capacity) return fail(SVO_ERR_CAPACITY, "upload exceeds node-pool capacity");
     if (n_att != 2 * n_nodes) return fail(SVO_ERR_ARG, "attachments must hold 2 words per node");
     if (n_nodes == 0) return SVO_OK;
@@ -500,21 +729,26 @@ int svo_set_buffer_v2(svo_ctx *ctx, const uint64_t *nodes, size_t n_nodes, const
         first[i] = (uint32_t)(nodes[i] >> 32);
         if (lo[i] > 0xFFFFu) return fail(SVO_ERR_FORMAT, "v2 node low word must only hold the two masks");
     }
-    int rc = record_upload(ctx, lo.data(), first.data(), n_nodes, dst_offset);
+    Upload u;
+    int rc = validate_upload(ctx, lo.data(), first.data(), n_nodes, dst_offset, &u);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
+    rc = order_streams(ctx, ctx->stream);
+    if (rc) return rc;
     static_assert(sizeof(uint2) == sizeof(uint64_t), "node layout");
     HIP_TRY(hipMemcpyAsync(ctx->d_nodes + dst_offset, nodes, n_nodes * sizeof(uint64_t), hipMemcpyHostToDevice,
                            ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->d_att + dst_offset, att, n_att * sizeof(uint32_t), hipMemcpyHostToDevice,
                            ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    commit_upload(ctx, u);
     return SVO_OK;
 }
 
 int svo_set_camera(svo_ctx *ctx, const float c2w[16], const float inv_proj[16], float px_off_x,
                    float px_off_y, const float light[4]) {
     if (!ctx || !c2w || !inv_proj || !light) return fail(SVO_ERR_ARG, "null argument");
+    for (svo_ctx *m : ctx->members) svo_set_camera(m, c2w, inv_proj, px_off_x, px_off_y, light);
     std::memcpy(ctx->cam.c2w, c2w, sizeof(ctx->cam.c2w));
     std::memcpy(ctx->cam.inv_proj, inv_proj, sizeof(ctx->cam.inv_proj));
     ctx->cam.px_off[0] = px_off_x;
@@ -524,70 +758,123 @@ int svo_set_camera(svo_ctx *ctx, const float c2w[16], const float inv_proj[16], 
     return SVO_OK;
 }
 
+int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band,
+                     const svo_frame *frame, void *stream) {
+    if (!ctx || !frame) return fail(SVO_ERR_ARG, "null argument");
+    if (is_multi(ctx)) {
+        if (band && band->band_count != 1) return fail(SVO_ERR_ARG, "a multi-device context splits the frame itself");
+        if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
+        return multi_render(ctx, width, height, stack_mode, frame, reinterpret_cast<hipStream_t>(stream));
+    }
+    return launch(ctx, width, height, stack_mode, band, outputs_of(frame), reinterpret_cast<hipStream_t>(stream));
+}
+
+int svo_assemble_frame(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, const void *const *parts,
+                       int part_format, int skip_part, const svo_frame *frame, void *stream) {
+    if (!ctx || !parts || !frame) return fail(SVO_ERR_ARG, "null argument");
+    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    svo::Outputs o = outputs_of(frame);
+    int rc = check_assemble_args(c, width, height, band_rows, n_parts, part_format, skip_part, o);
+    if (rc) return rc;
+    for (int i = 0; i < n_parts; ++i)
+        if (!parts[i] && i != skip_part) return fail(SVO_ERR_ARG, "null part pointer");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    rc = order_streams(c, s);
+    if (rc) return rc;
+    return assemble(c, width, height, band_rows, n_parts, parts, part_format, skip_part, o, s);
+}
+
 int svo_render(svo_ctx *ctx, int width, int height, int stack_mode, float *rgba_out, svo_hit *hits_out) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
     if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
     size_t px = (size_t)width * (size_t)height;
-    HIP_TRY(hipSetDevice(ctx->device));
-    int rc = ensure_out(ctx, px);
+    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = ensure_out(c, px);
     if (rc) return rc;
-    rc = launch(ctx, width, height, stack_mode, nullptr, rgba_out ? ctx->d_out_rgba : nullptr,
-                hits_out ? ctx->d_out_hits : nullptr, nullptr, ctx->stream);
+    svo_frame f{};
+    f.hits = hits_out ? reinterpret_cast<svo_hit *>(c->d_out_hits) : nullptr;
+    f.rgba = rgba_out ? reinterpret_cast<float *>(c->d_out_rgba) : nullptr;
+    f.layout = SVO_LAYOUT_FRAME;
+    if (is_multi(ctx)) {
+        if (!hits_out && !rgba_out) return SVO_OK;
+        rc = multi_render(ctx, width, height, stack_mode, &f, c->stream);
+    } else {
+        rc = launch(c, width, height, stack_mode, nullptr, outputs_of(&f), c->stream);
+    }
     if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
     if (hits_out)
-        HIP_TRY(hipMemcpyAsync(hits_out, ctx->d_out_hits, px * sizeof(svo_hit), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(hits_out, c->d_out_hits, px * sizeof(svo_hit), hipMemcpyDeviceToHost, c->stream));
     if (rgba_out)
-        HIP_TRY(hipMemcpyAsync(rgba_out, ctx->d_out_rgba, px * 4 * sizeof(float), hipMemcpyDeviceToHost,
-                               ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipMemcpyAsync(rgba_out, c->d_out_rgba, px * 4 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return SVO_OK;
 }
 
 int svo_render_device(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band, void *d_rgba,
                       void *d_hits, void *stream) {
-    return launch(ctx, width, height, stack_mode, band, d_rgba, d_hits, nullptr,
-                  reinterpret_cast<hipStream_t>(stream));
+    svo_frame f{};
+    f.hits = reinterpret_cast<svo_hit *>(d_hits);
+    f.rgba = reinterpret_cast<float *>(d_rgba);
+    f.layout = SVO_LAYOUT_BAND;
+    if (ctx && is_multi(ctx)) {
+        f.layout = SVO_LAYOUT_FRAME;
+        if (!d_rgba && !d_hits) return SVO_OK;
+    }
+    return svo_render_frame(ctx, width, height, stack_mode, band, &f, stream);
 }
 
 int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band,
                       void *d_fetches, void *stream) {
     if (!d_fetches) return fail(SVO_ERR_ARG, "d_fetches is null");
-    return launch(ctx, width, height, stack_mode, band, nullptr, nullptr,
-                  reinterpret_cast<uint32_t *>(d_fetches), reinterpret_cast<hipStream_t>(stream));
+    if (ctx && is_multi(ctx)) return fail(SVO_ERR_ARG, "count fetches on a member context (svo_get_member)");
+    svo::Outputs o{};
+    o.fetches = reinterpret_cast<uint32_t *>(d_fetches);
+    return launch(ctx, width, height, stack_mode, band, o, reinterpret_cast<hipStream_t>(stream));
 }
 
 int svo_set_options(svo_ctx *ctx, uint32_t options) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
     if (options & ~(uint32_t)(SVO_OPT_SHADOW_RAYS | SVO_OPT_KERNEL_TIMING)) return fail(SVO_ERR_ARG, "unknown option bits");
+    for (svo_ctx *m : ctx->members) m->options = options;
     ctx->options = options;
     return SVO_OK;
 }
 
-int svo_kernel_time(svo_ctx *ctx, double *mean_ms, uint64_t *launches) {
+int svo_stage_time(svo_ctx *ctx, int stage, double *mean_ms, uint64_t *launches) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
-    HIP_TRY(hipSetDevice(ctx->device));
+    if (stage < 0 || stage >= N_STAGES) return fail(SVO_ERR_ARG, "unknown stage");
+    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    HIP_TRY(hipSetDevice(c->device));
     double sum = 0.0;
     uint64_t n = 0;
     hipError_t err = hipSuccess;
-    for (auto &ev : ctx->timing_events) {
+    for (auto &ev : c->timing_events[stage]) {
         float ms = 0.0f;
         if (err == hipSuccess) err = hipEventSynchronize(ev.second);
         if (err == hipSuccess) err = hipEventElapsedTime(&ms, ev.first, ev.second);
         if (err == hipSuccess) { sum += ms; ++n; }
-        ctx->timing_free.push_back(ev);
+        c->timing_free.push_back(ev);
     }
-    ctx->timing_events.clear();
-    if (err != hipSuccess) return fail(SVO_ERR_HIP, std::string("svo_kernel_time: ") + hipGetErrorString(err));
+    c->timing_events[stage].clear();
+    if (err != hipSuccess) return fail(SVO_ERR_HIP, std::string("svo_stage_time: ") + hipGetErrorString(err));
     if (mean_ms) *mean_ms = n ? sum / (double)n : 0.0;
     if (launches) *launches = n;
     return SVO_OK;
 }
 
+int svo_kernel_time(svo_ctx *ctx, double *mean_ms, uint64_t *launches) {
+    return svo_stage_time(ctx, STAGE_KERNEL, mean_ms, launches);
+}
+
 int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
-    if (n_nodes) *n_nodes = ctx->n_nodes;
-    if (max_depth) *max_depth = ctx->depth;
-    if (device) *device = ctx->device;
+    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    if (n_nodes) *n_nodes = c->n_nodes;
+    if (max_depth) *max_depth = c->depth;
+    if (device) *device = c->device;
     return SVO_OK;
 }
 
@@ -597,39 +884,51 @@ int svo_accumulate(svo_ctx *ctx, void *d_accum, const void *d_sample, size_t n_p
     if (n_px == 0) return SVO_OK;
     if (!d_accum || !d_sample) return fail(SVO_ERR_ARG, "null accumulation or sample buffer");
     if (((uintptr_t)d_accum | (uintptr_t)d_sample) & 15u) return fail(SVO_ERR_ARG, "buffers must be 16-byte aligned");
-    HIP_TRY(hipSetDevice(ctx->device));
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    int rc = order_streams(c, s);
+    if (rc) return rc;
     hipError_t e = svo::launch_accumulate(reinterpret_cast<float4 *>(d_accum), reinterpret_cast<const float4 *>(d_sample),
-                                          n_px, sample, ctx->num_cus, s);
+                                          n_px, sample, c->num_cus, s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("accumulate launch: ") + hipGetErrorString(e));
     return SVO_OK;
 }
 
 int svo_synchronize(svo_ctx *ctx) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (is_multi(ctx)) {
+        for (svo_ctx *m : ctx->members) {
+            int rc = svo_synchronize(m);
+            if (rc) return rc;
+        }
+        return SVO_OK;
+    }
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->last_valid && ctx->last_stream != ctx->stream) HIP_TRY(hipStreamSynchronize(ctx->last_stream));
     return SVO_OK;
 }
 
 int svo_destroy(svo_ctx *ctx) {
     if (!ctx) return SVO_OK;
-    hipSetDevice(ctx->device);
-    if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    if (ctx->d_nodes) hipFree(ctx->d_nodes);
-    if (ctx->d_att) hipFree(ctx->d_att);
-    if (ctx->d_stage) hipFree(ctx->d_stage);
-    if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
-    if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
-    if (ctx->d_counter) hipFree(ctx->d_counter);
-    if (ctx->d_shadow_cost) hipFree(ctx->d_shadow_cost);
-    if (ctx->d_shadow_order) hipFree(ctx->d_shadow_order);
-    for (auto &ev : ctx->timing_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
-    for (auto &ev : ctx->timing_free) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
-    if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
-    if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
-    if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
-    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (!is_multi(ctx) && ctx->peers.empty()) return destroy_single(ctx);
+    for (svo_ctx *m : ctx->members) {   // drain every device first: payloads and events are shared
+        hipSetDevice(m->device);
+        hipDeviceSynchronize();
+    }
+    for (size_t i = 1; i < ctx->peers.size(); ++i) {
+        Peer &pr = ctx->peers[i];
+        if (i < ctx->members.size()) hipSetDevice(ctx->members[i]->device);
+        for (int j = 0; j < 2; ++j) {
+            if (pr.buf[j]) hipFree(pr.buf[j]);
+            if (pr.rendered[j]) hipEventDestroy(pr.rendered[j]);
+        }
+    }
+    if (!ctx->members.empty()) hipSetDevice(ctx->members[0]->device);
+    for (int j = 0; j < 2; ++j)
+        if (ctx->gathered[j]) hipEventDestroy(ctx->gathered[j]);
+    for (svo_ctx *m : ctx->members) destroy_single(m);
     delete ctx;
     return SVO_OK;
 }

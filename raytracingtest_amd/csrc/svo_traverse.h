@@ -5,9 +5,8 @@
 // Assets/Shaders/NVIDIASVO.compute:12-198 (IntersectSVO, Laine & Karras 2010)
 // of the reference.  Not a transcription of the HLSL dispatch: one wave64
 // covers an 8x8 pixel tile, the traversal stack lives in LDS laid out
-// [slot][lane] (conflict-free ds_read_b64 / ds_write_b64), a node fetch is one
-// 8-byte load, and never-written stack entries read as zero through a
-// per-lane written-slot bit mask instead of a per-ray LDS clear.
+// [slot][lane] (conflict-free ds_write2_b32 / ds_read_b64), a node fetch is one
+// 8-byte load, and the per-lane branch conditions are wave lane masks in SGPRs.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,7 +17,8 @@ namespace svo {
 
 constexpr int S_MAX = 23;          // NVIDIASVO.compute:2
 constexpr int MAX_ITERS = 65536;   // safety net, identical in oracle/svo_oracle.c
-constexpr int BLOCK = 256;         // 4 waves, 16x16 pixels
+constexpr int TILE = 64;           // one wave64 = one 8x8 pixel tile
+constexpr int MAX_PARTS = 64;      // band parts one assemble launch reads (devices / ranks)
 
 struct Camera {
     float c2w[16];        // Unity Matrix4x4, column-major
@@ -37,6 +37,19 @@ struct Hit {              // == svo_hit
 };
 static_assert(sizeof(Hit) == 24, "hit record layout");
 
+// Every per-pixel output of one launch (device pointers, each nullable).  Index =
+// local row * width + x (band layout) or global row * width + x (frame layout).
+struct Outputs {
+    Hit *hits;                 // svo_hit, 24 B
+    float4 *rgba;              // Result (RGBA32F)
+    uint32_t *rgba8;           // display RGBA8
+    uint32_t *compact;         // svo_hit_compact: 3 words = the first 12 bytes of svo_hit
+    float4 *position;          // bestHit.position (NVIDIASVO.compute:172-174), w = 0
+    unsigned long long *voxel; // voxel key
+    uint32_t *fetches;         // instrumented launch: descriptor fetches per ray
+    int frame_layout;          // 1: index by global row (full-frame buffers)
+};
+
 struct LaunchParams {
     const uint2 *nodes;
     const uint2 *att;
@@ -45,28 +58,37 @@ struct LaunchParams {
     int width, height;
     int band_rows, band_rank, band_count, local_rows;
     int slots;            // stack slots = depth - 1 (scales [23 - slots, 22])
-    Hit *hits;            // nullable
-    float4 *rgba;         // nullable
-    uint32_t *fetches;    // nullable (instrumented launch)
-    int refill_at;        // persistent kernel: refill idle lanes when fewer than this still trace
-    int blocks_per_cu;    // persistent kernel: grid = CUs x this
-    int xcd_remap;        // tile kernel: give each XCD a contiguous screen band
-    int flat;             // 1: branch-flattened iteration (default), 0: branchy reference form
-    int block;            // tile kernel workgroup size: 64 (one 8x8 wave) or 256 (16x16 pixels)
+    Outputs out;
+    int xcd_remap;        // 2: interleaved XCD column strips, 0: raster
     int shadows;          // one shadow ray per primary hit: 1 = second pass (needs hits), 2 = fused into the primary launch
     uint32_t *wave_log;   // diagnostics (env SVO_WAVE_LOG): per wave {t0, t1, HW_ID, XCC_ID | trips << 8,
                           //   loop cycles, fetch-wait cycles, fetch trips, pop trips} (instrumented loop)
-    // Cost-ordered dispatch (64-thread tile kernel): block b traces 8x8 tile
-    // tile_order[b] (null = b) and records its wave trip count in tile_cost.
-    const uint32_t *tile_order;   // n_tiles entries + 4 class boundaries
+    // Cost-ordered dispatch: block b traces 8x8 tile tile_order[b] (null = b)
+    // and records its wave trip count in tile_cost.
+    const uint32_t *tile_order;   // n_tiles entries + 36 class boundaries
     uint16_t *tile_cost;
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
     int fetch_all;                // lean loop (!guard): every lane loads its node every trip
-    int strip_w;                  // xcd_remap 2: tile columns per super-column
-    // The same cost-ordered dispatch for the shadow pass (its own costs and order).
+    // The same cost-ordered dispatch for the two-pass shadow form (its own costs and order).
     const uint32_t *shadow_order;
     uint16_t *shadow_cost;
+};
+
+// Re-interleave the band parts of a split frame on the display device
+// (svo_assemble_frame): part m holds the rows of bands b with b % n_parts == m,
+// in increasing y, as 12-byte compact records (PART_COMPACT) or RGBA8 words
+// (PART_RGBA8).  Compact parts are expanded into every requested output: the
+// normal and the Result colour are rebuilt from the display device's own SVO
+// replica and camera with the render kernel's arithmetic (bit-identical).
+enum { PART_COMPACT = 0, PART_RGBA8 = 1 };
+struct AssembleParams {
+    const uint2 *att;
+    uint32_t n_nodes;     // a parent outside the pool reads attachment words 0
+    Camera cam;
+    int width, height, band_rows, n_parts, part_format, skip_part;
+    const void *parts[MAX_PARTS];
+    Outputs out;          // frame layout
 };
 
 // Order the tiles by recorded cost, most expensive class first, into `order`
@@ -77,17 +99,15 @@ struct LaunchParams {
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream);
 size_t order_cost_capacity(int n_tiles);
 // The same per XCD strip (xcd_remap 2): order must hold n_tiles + 36 entries.
-hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, int strip_w,
-                               hipStream_t stream);
+hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream);
 
 // Progressive accumulation (AddShader blend) of an RGBA32F sample frame.
 hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32_t sample, int num_cus,
                              hipStream_t stream);
 
-// kernel: 0 = tile (one lane per pixel), 1 = persistent (wave-level ray refill).
-// counter: 16-byte device work counter (persistent kernel), num_cus: CU count.
-hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, int kernel,
-                         uint32_t *counter, int num_cus, hipEvent_t primary_start = nullptr,
+hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream);
+
+hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, hipEvent_t primary_start = nullptr,
                          hipEvent_t primary_end = nullptr);
 
 }  // namespace svo

@@ -1,21 +1,28 @@
 """Multi-GPU screen split for one 8-GPU node.
 
-One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on
-ROCm; "gloo" for the CPU tests).  The SVO is replicated per GPU (each rank
-uploads or builds its own copy) and rays are independent, so the only
-exchange is moving per-rank results to the display rank:
+Two forms share one band layout and one display-side assemble kernel:
 
-  * bands  -- one frame split into `band_rows`-row bands dealt round-robin to
-              the ranks (interleaving balances sky vs terrain rows); rank 0
-              gathers the hit records / RGBA bands and re-interleaves them.
-  * samples -- every rank traces the whole frame at its own _PixelOffset
-              jitter (RaytracingMaster.cs:35); the progressive accumulation of
-              AddShader.shader:44-47 (running mean over samples) becomes one
-              all-reduce of the RGBA frames.
+  * one process, several GPUs -- RaytracingMaster(devices=[...]) over the
+    plugin's multi-device context (svo_create_multi): the Unity host's form; the
+    display GPU pulls the other GPUs' band payloads over xGMI (peer access);
+  * one process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on
+    ROCm; "gloo" for the CPU tests) -- bench.py's form: every rank renders its
+    bands into a band-contiguous payload, `gather_parts` moves the payloads to
+    the display rank with one RCCL gather, and the display rank's plugin
+    rebuilds the frame (RaytracingMaster.assemble_frame, svo_assemble_frame).
 
-Each rank's band buffer holds only its rows, in increasing y; band_rows()
-in raytracing_master gives their global indices.
+Band layout: rows are grouped in `band_rows`-row bands dealt round-robin to the
+ranks (band b -> rank b % world), so sky and terrain rows interleave and every
+rank gets the same mix (the reference's single dispatch grid is split,
+RaytracingMaster.cs:66-68).  A rank's payload holds only its rows, in
+increasing y; band_rows() in raytracing_master gives their global indices.
+
+Payloads: 4-byte RGBA8 display words (the framebuffer the display shows) or
+12-byte compact records (svo_hit_compact) from which the display GPU rebuilds
+the full 24-byte hit records and the RGBA32F Result with its own SVO replica.
 """
+import math
+
 import numpy as np
 
 from .raytracing_master import band_rows
@@ -28,33 +35,56 @@ def rank_band(rank, world, rows=DEFAULT_BAND_ROWS):
     return (rows, rank, world)
 
 
+def band_len(height, rank, world, rows=DEFAULT_BAND_ROWS):
+    return len(band_rows(height, (rows, rank, world)))
+
+
 def max_band_len(height, world, rows=DEFAULT_BAND_ROWS):
-    return max(len(band_rows(height, (rows, r, world))) for r in range(world))
+    return max(band_len(height, r, world, rows) for r in range(world))
+
+
+def weak_frame(width, height, world):
+    """Frame of a weak-scaling run on `world` GPUs: the same camera at sqrt(world)
+    times the linear resolution, so every GPU traces about width * height rays
+    with the same per-ray cost mix as the one-GPU frame.  Width is kept a
+    multiple of 64 (whole XCD tile-column strips), height a multiple of 8."""
+    if world == 1:
+        return width, height
+    s = math.sqrt(world)
+    w = max(64, int(round(width * s / 64.0)) * 64)
+    h = max(8, int(round(height * s / 8.0)) * 8)
+    return w, h
+
+
+def gather_parts(send, parts, dst=0, dist=None, group=None):
+    """One gather of every rank's equally sized payload tensor `send` into
+    `parts` (a list of world tensors on the display rank `dst`, None elsewhere).
+    On RCCL (backend "nccl") the transfer runs on the communicator's stream,
+    ordered after the caller's current stream; on gloo it is a CPU copy."""
+    if dist is None:
+        import torch.distributed as dist
+    dist.gather(send, gather_list=parts, dst=dst, group=group)
 
 
 def gather_bands(local, height, width, world, rank, elem_bytes, rows=DEFAULT_BAND_ROWS, dist=None):
-    """All-gather every rank's band buffer (a uint8 torch tensor holding
-    len(band_rows) * width * elem_bytes bytes, on the rank's device) and return,
-    on every rank, the list of per-rank byte tensors trimmed to their true size.
-    all_gather (not gather) so the same call works on RCCL and gloo."""
+    """Gather every rank's band buffer (uint8 tensor of band_len * width *
+    elem_bytes bytes) to rank 0; returns the per-rank byte tensors trimmed to
+    their true size on rank 0, None elsewhere."""
     import torch
-    if dist is None:
-        import torch.distributed as dist
     per = max_band_len(height, world, rows) * width * elem_bytes
     send = torch.zeros(per, dtype=torch.uint8, device=local.device)
     send[:local.numel()].copy_(local.reshape(-1))
-    bufs = [torch.empty(per, dtype=torch.uint8, device=local.device) for _ in range(world)]
-    dist.all_gather(bufs, send)
-    out = []
-    for r in range(world):
-        n = len(band_rows(height, (rows, r, world))) * width * elem_bytes
-        out.append(bufs[r][:n])
-    return out
+    bufs = [torch.empty(per, dtype=torch.uint8, device=local.device) for _ in range(world)] if rank == 0 else None
+    gather_parts(send, bufs, dst=0, dist=dist)
+    if rank != 0:
+        return None
+    return [bufs[r][:band_len(height, r, world, rows) * width * elem_bytes] for r in range(world)]
 
 
 def assemble(parts, height, width, dtype, rows=DEFAULT_BAND_ROWS):
     """Re-interleave per-rank band arrays (numpy, any dtype of one pixel) into
-    a [height, width] frame."""
+    a [height, width] frame: the host restatement of the assemble kernel's
+    layout (tests)."""
     world = len(parts)
     frame = np.zeros((height, width), dtype)
     for r, part in enumerate(parts):

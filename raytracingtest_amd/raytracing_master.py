@@ -9,6 +9,14 @@ Same names and argument meaning as the reference:
   Render(width, height)          RaytracingMaster.cs:60-74   (Dispatch + result)
   accumulate_device(...)         RaytracingMaster.cs:70-73 + AddShader.shader (Blit with _Sample,
                                  then _currentSample++; reset to 0 when the camera moves, :44-47)
+Beyond the reference (one GPU, one Dispatch):
+  RaytracingMaster(devices=[0, 1, ...])  one context over several GPUs of the node
+                                 (svo_create_multi): SVO replica per GPU, the frame
+                                 rendered in row bands and gathered to devices[0]
+  render_frame(...)              every per-pixel output (hits, Result, RGBA8,
+                                 compact records, hit position, voxel key)
+  assemble_frame(...)            rebuild a frame from band parts (the display side
+                                 of the one-process-per-GPU split)
 Errors surface as SvoError (the C-ABI status + svo_last_error text) instead of
 Unity's silent shader failures.  There is no CPU fallback.
 """
@@ -17,7 +25,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import HIT_DTYPE, STACK_EXACT, STACK_HLSL, SvoBand, SvoError, check
+from ._lib import HIT_DTYPE, LAYOUT_BAND, LAYOUT_FRAME, STACK_EXACT, STACK_HLSL, SvoBand, SvoError, SvoFrame, check
 from .camera import column_major, main_camera, main_light
 from .svo_data import SVOData
 
@@ -25,9 +33,18 @@ from .svo_data import SVOData
 REFERENCE_CAPACITY = 1073741824 // 8
 
 
+def _frame(hits=None, rgba=None, rgba8=None, compact=None, position=None, voxel=None, layout=LAYOUT_BAND):
+    return SvoFrame(hits, rgba, rgba8, compact, position, voxel, layout)
+
+
 class RaytracingMaster:
-    def __init__(self, device=0, capacity_nodes=REFERENCE_CAPACITY, maxLevel=5, sampleType=4):
-        self.device = device
+    def __init__(self, device=0, capacity_nodes=REFERENCE_CAPACITY, maxLevel=5, sampleType=4, devices=None,
+                 band_rows=8):
+        """devices: list of HIP device indices for a multi-device context (devices[0]
+        displays; an index may repeat); None = the single device `device`."""
+        self.devices = None if devices is None else [int(d) for d in devices]
+        self.device = device if devices is None else self.devices[0]
+        self.band_rows = int(band_rows)
         self.capacity_nodes = int(capacity_nodes)
         self.maxLevel = maxLevel        # [Range(1, 8)] in the reference (:16-17)
         self.sampleType = sampleType    # SampleFunctions.Type.Custom1 = 4 (:18)
@@ -44,7 +61,12 @@ class RaytracingMaster:
         if self._ctx:
             L.svo_destroy(self._ctx)
             self._ctx = ctypes.c_void_p()
-        check(L.svo_create(self.device, self.capacity_nodes, ctypes.byref(self._ctx)), "svo_create")
+        if self.devices is None:
+            check(L.svo_create(self.device, self.capacity_nodes, ctypes.byref(self._ctx)), "svo_create")
+        else:
+            arr = (ctypes.c_int * len(self.devices))(*self.devices)
+            check(L.svo_create_multi(arr, len(self.devices), self.capacity_nodes, self.band_rows,
+                                     ctypes.byref(self._ctx)), "svo_create_multi")
         self._options = 0
 
     def SetSVOBuffer(self, data=None, offset=0):
@@ -107,6 +129,24 @@ class RaytracingMaster:
         check(_lib.lib().svo_kernel_time(self._ctx, ctypes.byref(ms), ctypes.byref(n)), "svo_kernel_time")
         return ms.value, n.value
 
+    def stage_time(self, stage):
+        """(mean ms, launches) of a timed stage: _lib.STAGE_KERNEL or STAGE_ASSEMBLE."""
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        check(_lib.lib().svo_stage_time(self._ctx, int(stage), ctypes.byref(ms), ctypes.byref(n)), "svo_stage_time")
+        return ms.value, n.value
+
+    def num_devices(self):
+        n = ctypes.c_int()
+        check(_lib.lib().svo_num_devices(self._ctx, ctypes.byref(n)), "svo_num_devices")
+        return n.value
+
+    def member(self, index):
+        """The per-device context `index` (owned by this one) as a RaytracingMaster view."""
+        c = ctypes.c_void_p()
+        check(_lib.lib().svo_get_member(self._ctx, int(index), ctypes.byref(c)), "svo_get_member")
+        return _MemberView(self, c)
+
     # ----------------------------------------------------------------- render
     def Render(self, width, height, stack_mode=STACK_HLSL, want_rgba=True, want_hits=True):
         """Blocking render into host arrays: (rgba[H, W, 4] float32, hits[H, W] svo_hit)."""
@@ -124,6 +164,27 @@ class RaytracingMaster:
         b = None if band is None else ctypes.byref(SvoBand(*band))
         check(_lib.lib().svo_render_device(self._ctx, width, height, stack_mode, b, rgba_ptr, hits_ptr, stream),
               "svo_render_device")
+
+    def render_frame(self, width, height, hits=None, rgba=None, rgba8=None, compact=None, position=None,
+                     voxel=None, layout=LAYOUT_BAND, stack_mode=STACK_HLSL, band=None, stream=None):
+        """Asynchronous render of every requested output (device pointers).
+        layout LAYOUT_BAND: buffers hold only `band`'s rows; LAYOUT_FRAME: full-frame
+        buffers.  A multi-device context renders the whole frame (band None) onto
+        devices[0]."""
+        b = None if band is None else ctypes.byref(SvoBand(*band))
+        f = _frame(hits, rgba, rgba8, compact, position, voxel, layout)
+        check(_lib.lib().svo_render_frame(self._ctx, width, height, stack_mode, b, ctypes.byref(f), stream),
+              "svo_render_frame")
+
+    def assemble_frame(self, width, height, parts, part_format, band_rows=None, hits=None, rgba=None, rgba8=None,
+                       compact=None, skip_part=-1, stream=None):
+        """Rebuild a frame (full-frame device buffers) from band parts: parts[m] = the
+        device pointer of rank m's band payload (compact records or RGBA8 words)."""
+        arr = (ctypes.c_void_p * len(parts))(*[p if p else None for p in parts])
+        f = _frame(hits, rgba, rgba8, compact, None, None, LAYOUT_FRAME)
+        check(_lib.lib().svo_assemble_frame(self._ctx, width, height, self.band_rows if band_rows is None else band_rows,
+                                            len(parts), arr, part_format, skip_part, ctypes.byref(f), stream),
+              "svo_assemble_frame")
 
     def count_fetches_device(self, width, height, fetch_ptr, stack_mode=STACK_HLSL, band=None, stream=None):
         b = None if band is None else ctypes.byref(SvoBand(*band))
@@ -166,6 +227,24 @@ class RaytracingMaster:
 
     def __exit__(self, *exc):
         self.close()
+
+
+class _MemberView(RaytracingMaster):
+    """One device of a multi-device context: queries and device renders on that
+    device alone (not destroyed on its own)."""
+
+    def __init__(self, owner, ctx):   # noqa: D107 -- no svo_create: the group owns the context
+        self._owner = owner
+        self._ctx = ctx
+        self._options = owner._options
+        self.currentSample = 0
+        self._c2w = None
+        self.devices = None
+        self.band_rows = owner.band_rows
+        self.device = self.info()["device"]
+
+    def close(self):
+        self._ctx = ctypes.c_void_p()
 
 
 def band_rows(height, band):

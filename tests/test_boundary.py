@@ -40,7 +40,7 @@ def test_exports_every_declared_symbol(native):
 
 
 def test_abi_version_and_error_text(native):
-    assert native.svo_abi_version() == 1
+    assert native.svo_abi_version() == 2
     assert isinstance(native.svo_last_error(), bytes)
 
 
@@ -58,9 +58,40 @@ def test_header_layout_compiles_in_c(tmp_path):
                    '_Static_assert(offsetof(svo_hit, t) == 8, "t");\n'
                    '_Static_assert(offsetof(svo_hit, nz) == 20, "nz");\n'
                    '_Static_assert(sizeof(svo_band) == 12, "band");\n'
+                   '_Static_assert(sizeof(svo_hit_compact) == 12, "compact");\n'
+                   '_Static_assert(offsetof(svo_frame, layout) == 48, "frame");\n'
+                   '_Static_assert(SVO_PART_RGBA8 == 1 && SVO_LAYOUT_FRAME == 1 && SVO_STAGE_ASSEMBLE == 1, "enums");\n'
                    'int main(void){return 0;}\n')
     subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
                     "-o", str(tmp_path / "t")], check=True)
+
+
+def test_multi_device_and_frame_entry_points_reject_bad_arguments_without_gpu(native):
+    import ctypes
+    from raytracingtest_amd._lib import SvoFrame
+    out = ctypes.c_void_p()
+    assert native.svo_create_multi(None, 2, 16, 8, ctypes.byref(out)) == -1
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert native.svo_create_multi(devs, 0, 16, 8, ctypes.byref(out)) == -1      # no device touched
+    assert native.svo_create_multi(devs, 2, 16, 0, ctypes.byref(out)) == -1      # band_rows
+    assert native.svo_render_frame(None, 8, 8, 0, None, ctypes.byref(SvoFrame()), None) == -1
+    assert native.svo_assemble_frame(None, 8, 8, 8, 1, None, 0, -1, None, None) == -1
+    assert native.svo_stage_time(None, 0, None, None) == -1
+    n = ctypes.c_int()
+    assert native.svo_num_devices(None, ctypes.byref(n)) == -1
+
+
+def test_compact_record_is_the_hit_record_prefix():
+    from raytracingtest_amd import HIT_DTYPE
+    from raytracingtest_amd._lib import COMPACT_DTYPE
+    h = np.zeros(3, HIT_DTYPE)
+    h["parent"] = [1, 0xFFFFFFFF, 7]
+    h["hit_idx"], h["hit_scale"], h["flags"] = [5, 0, 2], [13, 0, 10], [9, 0, 1]
+    h["t"] = [1.5, np.inf, 3.0]
+    c = np.frombuffer(h.view(np.uint8).reshape(3, 24)[:, :12].tobytes(), COMPACT_DTYPE)
+    assert np.array_equal(c["parent"], h["parent"]) and np.array_equal(c["t"], h["t"])
+    assert np.array_equal(c["meta"], h["hit_idx"] | (h["hit_scale"].astype(np.uint32) << 8) |
+                          (h["flags"].astype(np.uint32) << 16))
 
 
 def test_hit_dtype_matches_header():

@@ -1,10 +1,12 @@
-"""World-size-2 gloo tests of the multi-GPU path on CPU.
+"""World-size-2/3 gloo tests of the multi-GPU path on CPU.
 
 The per-rank renderer is the CPU oracle (test infrastructure) standing in for
-the HIP kernel, so the band split, the all-gather and the re-interleave of
-raytracingtest_amd.distributed are exercised exactly as bench.py uses them on
-RCCL; the GPU path of the band split itself is covered by
-test_gpu_parity.py::test_band_split_reassembles_frame."""
+the HIP kernel; the band layout, the payload formats (RGBA8 words, 12-byte
+compact records = svo_hit prefix) and the one gather to rank 0
+(distributed.gather_parts, the call bench.py's Gather makes on RCCL) run as in
+bench.py; the re-interleave is the host restatement of the assemble kernel's
+layout.  The GPU side (band render + svo_assemble_frame, the multi-device
+context) is covered by tests/test_gpu_frame.py."""
 import os
 import socket
 
@@ -40,17 +42,32 @@ def _worker(rank, world, port, mode, out_dir):
     W, H = 96, 70
     c2w, inv_proj = overview_camera().uniforms(W, H)
     osvo = orc.OracleSVO(svo.childDescriptors, svo.attachments)
-    if mode == "bands":
+    if mode in ("bands", "rgba8", "compact"):
         cam = orc.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
         band = D.rank_band(rank, world)
         ys = band_rows(H, band)
         pix = (ys[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
-        hits, _, _ = orc.render_pixels(osvo, cam, W, H, pix, nthreads=2)
-        local = torch.from_numpy(np.frombuffer(hits.tobytes(), np.uint8).copy())
-        parts = D.gather_bands(local, H, W, world, rank, 24)
-        if rank == 0:
-            frame = D.assemble([p.numpy() for p in parts], H, W, orc.HIT_DTYPE)
-            np.save(os.path.join(out_dir, "frame.npy"), frame)
+        hits, rgba, _ = orc.render_pixels(osvo, cam, W, H, pix, nthreads=2)
+        if mode == "bands":
+            local = torch.from_numpy(np.frombuffer(hits.tobytes(), np.uint8).copy())
+            parts = D.gather_bands(local, H, W, world, rank, 24)
+            if rank == 0:
+                frame = D.assemble([p.numpy() for p in parts], H, W, orc.HIT_DTYPE)
+                np.save(os.path.join(out_dir, "frame.npy"), frame)
+        else:   # bench.py's Gather: equal-size int32 payload slots, one gather to rank 0
+            elem = 1 if mode == "rgba8" else 3
+            per = D.max_band_len(H, world) * W * elem
+            send = torch.zeros(per, dtype=torch.int32)
+            payload = (orc.pack_rgba8(rgba).view(np.int32) if mode == "rgba8" else
+                       np.frombuffer(hits.view(np.uint8).reshape(-1, 24)[:, :12].tobytes(), np.int32))
+            send[:payload.size] = torch.from_numpy(payload.copy())
+            parts = [torch.empty(per, dtype=torch.int32) for _ in range(world)] if rank == 0 else None
+            D.gather_parts(send, parts, dst=0)
+            if rank == 0:
+                dt = np.uint32 if mode == "rgba8" else np.dtype([("w", "<u4", 3)])
+                trimmed = [p.numpy()[:D.band_len(H, r, world) * W * elem] for r, p in enumerate(parts)]
+                frame = D.assemble(trimmed, H, W, dt)
+                np.save(os.path.join(out_dir, "frame.npy"), frame)
     else:
         off = (0.5, 0.5) if rank == 0 else tuple(float(v) for v in jitter_offsets(world)[rank])
         cam = orc.make_camera(c2w, inv_proj, off, main_light())
@@ -63,19 +80,23 @@ def _worker(rank, world, port, mode, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["bands", "samples"])
-def test_two_rank_gloo(tmp_path, oracle_mod, text_svo, mode):
-    world = 2
+@pytest.mark.parametrize("mode,world", [("bands", 2), ("samples", 2), ("rgba8", 2), ("rgba8", 3), ("compact", 3)])
+def test_gloo_ranks(tmp_path, oracle_mod, text_svo, mode, world):
     mp.spawn(_worker, args=(world, _free_port(), mode, str(tmp_path)), nprocs=world, join=True)
     from raytracingtest_amd.camera import jitter_offsets, main_light, overview_camera
     W, H = 96, 70
     c2w, inv_proj = overview_camera().uniforms(W, H)
     osvo = oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments)
-    if mode == "bands":
+    if mode in ("bands", "rgba8", "compact"):
         cam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
-        ref, _, _ = oracle_mod.render(osvo, cam, W, H)
+        ref, ref_rgba, _ = oracle_mod.render(osvo, cam, W, H)
         got = np.load(tmp_path / "frame.npy")
-        assert got.reshape(-1).tobytes() == ref.tobytes()
+        if mode == "bands":
+            assert got.reshape(-1).tobytes() == ref.tobytes()
+        elif mode == "rgba8":
+            assert np.array_equal(got.reshape(-1), oracle_mod.pack_rgba8(ref_rgba))
+        else:
+            assert got.tobytes() == ref.view(np.uint8).reshape(-1, 24)[:, :12].tobytes()
     else:
         acc = np.zeros((W * H, 4), np.float64)
         for r in range(world):
@@ -84,6 +105,16 @@ def test_two_rank_gloo(tmp_path, oracle_mod, text_svo, mode):
             _, rgba, _ = oracle_mod.render(osvo, cam, W, H)
             acc += rgba
         np.testing.assert_allclose(np.load(tmp_path / "accum.npy"), acc / world, rtol=1e-6, atol=1e-7)
+
+
+def test_weak_frame_keeps_rays_per_gpu():
+    from raytracingtest_amd.distributed import weak_frame
+    assert weak_frame(1920, 1080, 1) == (1920, 1080)
+    assert weak_frame(1920, 1080, 4) == (3840, 2160)
+    for n in (2, 3, 4, 5, 8):
+        w, h = weak_frame(1920, 1080, n)
+        assert w % 64 == 0 and h % 8 == 0
+        assert abs(w * h / n / (1920 * 1080) - 1.0) < 0.02
 
 
 def test_band_helpers_cover_frame():

@@ -1,0 +1,386 @@
+"""GPU parity of the frame outputs and of the multi-GPU split, through the C-ABI.
+
+* every per-pixel output of svo_render_frame (hit records, Result, display
+  RGBA8, compact records, bestHit.position, voxel key) against the oracle,
+  bit for bit (NVIDIASVO.compute:158-186, RaytraceCompute.compute:93-127,167);
+* the north-star split: a multi-device context (svo_create_multi) with the
+  device index repeated -- one MI355X renders every member's bands and the
+  display member pulls the payloads exactly as it would over xGMI -- and the
+  one-process-per-GPU form (band parts rendered separately, rebuilt by
+  svo_assemble_frame), both bit-identical to the oracle's single frame;
+* the round-1 advisor cases: launches alternating between two streams, a DAG
+  pool whose shared node sits at two depths, a chain of three linked pools.
+"""
+import numpy as np
+import pytest
+
+from raytracingtest_amd import HIT_DTYPE, RaytracingMaster, band_rows
+from raytracingtest_amd import _lib
+from raytracingtest_amd.builder import build_menger
+from raytracingtest_amd.camera import Camera, look_rotation, main_camera, main_light, overview_camera
+from raytracingtest_amd.svo_data import SVOData
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    t = pytest.importorskip("torch")
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+def _oracle(oracle_mod, svo, cam, w, h, mode=0, off=(0.5, 0.5), shadows=False):
+    c2w, inv_proj = cam.uniforms(w, h)
+    ocam = oracle_mod.make_camera(c2w, inv_proj, off, main_light())
+    osvo = oracle_mod.OracleSVO(nodes=svo.to_v2(), attachments=svo.attachments)
+    if shadows:
+        hits, rgba, _ = oracle_mod.render(osvo, ocam, w, h, mode | oracle_mod.SHADOW_RAYS)
+        return hits, rgba, None, None
+    hits, rgba, _, pos, vox = oracle_mod.render_ex(osvo, ocam, w, h, mode)
+    return hits, rgba, pos, vox
+
+
+def _bufs(torch, n_px):
+    """Every output buffer, pre-filled with a pattern no render produces."""
+    t = torch
+    return {"hits": t.full((n_px * 24,), 0xA5, dtype=t.uint8, device="cuda"),
+            "rgba": t.full((n_px * 4,), -7.0, dtype=t.float32, device="cuda"),
+            "rgba8": t.full((n_px,), 0x1234567, dtype=t.int32, device="cuda"),
+            "compact": t.full((n_px * 12,), 0x5A, dtype=t.uint8, device="cuda"),
+            "position": t.full((n_px * 4,), -9.0, dtype=t.float32, device="cuda"),
+            "voxel": t.full((n_px,), 77, dtype=t.int64, device="cuda")}
+
+
+def _ptrs(b, keys=None):
+    return {k: v.data_ptr() for k, v in b.items() if keys is None or k in keys}
+
+
+def _check(b, oracle_mod, ref_hits, ref_rgba, ref_pos=None, ref_vox=None, keys=None):
+    keys = set(b) if keys is None else set(keys)
+    hits = b["hits"].cpu().numpy().view(HIT_DTYPE)
+    if "hits" in keys:
+        bad = np.flatnonzero(hits.view(np.uint8).reshape(-1, 24).any(axis=1) &
+                             (hits.tobytes() != ref_hits.tobytes()))
+        assert hits.tobytes() == ref_hits.tobytes(), f"hit records differ ({len(bad)} px)"
+    if "rgba" in keys:
+        assert b["rgba"].cpu().numpy().tobytes() == ref_rgba.astype(np.float32).tobytes(), "Result differs"
+    if "rgba8" in keys:
+        got = b["rgba8"].cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, oracle_mod.pack_rgba8(ref_rgba)), "RGBA8 differs"
+    if "compact" in keys:
+        c = b["compact"].cpu().numpy().reshape(-1, 12)
+        assert c.tobytes() == ref_hits.view(np.uint8).reshape(-1, 24)[:, :12].tobytes(), "compact differs"
+    if "position" in keys and ref_pos is not None:
+        assert b["position"].cpu().numpy().tobytes() == ref_pos.tobytes(), "position differs"
+    if "voxel" in keys and ref_vox is not None:
+        assert np.array_equal(b["voxel"].cpu().numpy().view(np.uint64), ref_vox), "voxel key differs"
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_every_output_matches_oracle(torch, oracle_mod, text_svo, mode):
+    """All six outputs of one launch, Text SVO (C1) and the 256^3 Menger (V2)."""
+    for svo, cam, (w, h) in ((text_svo, main_camera(), (256, 256)), (text_svo, overview_camera(), (300, 200)),
+                             (build_menger(8), overview_camera(), (480, 272))):
+        ref_hits, ref_rgba, ref_pos, ref_vox = _oracle(oracle_mod, svo, cam, w, h, mode)
+        assert np.count_nonzero(ref_hits["flags"] & 1) > 500
+        m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+        try:
+            m.SetSVOBuffer(svo)
+            m.UpdateShaderParameters(cam, w, h)
+            b = _bufs(torch, w * h)
+            for _ in range(3):   # cost-ordered relaunches too
+                m.render_frame(w, h, stack_mode=mode, **_ptrs(b))
+                m.synchronize()
+                _check(b, oracle_mod, ref_hits, ref_rgba, ref_pos, ref_vox)
+        finally:
+            m.close()
+
+
+def test_voxel_key_and_position_properties(torch, oracle_mod):
+    """Size-independent properties of the new outputs on the 256^3 Menger: the
+    key's voxel box contains the hit position, its scale is the leaf scale,
+    misses carry position 0 and key ~0."""
+    svo = build_menger(8)
+    cam = overview_camera()
+    w, h = 640, 360
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        b = _bufs(torch, w * h)
+        m.render_frame(w, h, **_ptrs(b, ("hits", "position", "voxel")))
+        m.synchronize()
+    finally:
+        m.close()
+    hits = b["hits"].cpu().numpy().view(HIT_DTYPE)
+    pos = b["position"].cpu().numpy().reshape(-1, 4)
+    vox = b["voxel"].cpu().numpy().view(np.uint64)
+    hit = (hits["flags"] & 1) != 0
+    assert hit.sum() > 1000 and (~hit).sum() > 1000
+    assert np.all(vox[~hit] == np.uint64(0xFFFFFFFFFFFFFFFF)) and np.all(pos[~hit] == 0)
+    depth = 23 - hits["hit_scale"][hit].astype(np.int64)
+    assert np.all(depth == 8)
+    k = np.stack([(vox[hit] >> np.uint64(21 * a)) & np.uint64((1 << 21) - 1) for a in range(3)], 1).astype(np.float64)
+    c = pos[hit, :3].astype(np.float64) / 64.0 + 1.5
+    lo = 1.0 + k / 256.0
+    assert np.all((c >= lo - 1e-6) & (c <= lo + 1.0 / 256.0 + 1e-6))
+
+
+def test_frame_layout_bands_fill_the_frame(torch, text_svo):
+    """Band renders written in place into full-frame buffers (SVO_LAYOUT_FRAME)
+    give exactly the whole-frame render, and leave other rows untouched."""
+    cam = overview_camera()
+    w, h = 200, 150
+    m = RaytracingMaster(device=0, capacity_nodes=len(text_svo))
+    try:
+        m.SetSVOBuffer(text_svo)
+        m.UpdateShaderParameters(cam, w, h)
+        full_rgba, full = m.Render(w, h)
+        b = _bufs(torch, w * h)
+        m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba8=b["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME,
+                       band=(8, 1, 3))
+        m.synchronize()
+        got = b["hits"].cpu().numpy().view(HIT_DTYPE).reshape(h, w)
+        ys = band_rows(h, (8, 1, 3))
+        other = np.setdiff1d(np.arange(h), ys)
+        assert got[ys].tobytes() == full[ys].tobytes()
+        assert np.all(got[other].view(np.uint8) == 0xA5)
+        for r in (0, 2):
+            m.render_frame(w, h, hits=b["hits"].data_ptr(), layout=_lib.LAYOUT_FRAME, band=(8, r, 3))
+        m.synchronize()
+        assert b["hits"].cpu().numpy().tobytes() == full.tobytes()
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0, 0]])
+def test_multi_device_context_matches_oracle(torch, oracle_mod, text_svo, devices):
+    """svo_create_multi with the device repeated: the bands of members 1.. are
+    rendered into double-buffered payloads and pulled by the display member's
+    assemble kernel (compact records when hit records / Result are asked for,
+    RGBA8 words for a display-only frame).  Frames alternate cameras so a stale
+    payload would show."""
+    svo = build_menger(8)
+    w, h = 333, 250
+    cams = [overview_camera(), Camera(position=(30.0, 12.0, -25.0), rotation=look_rotation((-30.0, -12.0, 25.0)))]
+    refs = [_oracle(oracle_mod, svo, c, w, h) for c in cams]
+    m = RaytracingMaster(devices=devices, capacity_nodes=len(svo))
+    try:
+        assert m.num_devices() == len(devices)
+        m.SetSVOBuffer(svo)
+        for i in range(6):
+            cam = cams[i % 2]
+            ref_hits, ref_rgba, _, _ = refs[i % 2]
+            m.UpdateShaderParameters(cam, w, h)
+            rgba, hits = m.Render(w, h)                       # host path: svo_render
+            assert hits.tobytes() == ref_hits.tobytes()
+            assert rgba.reshape(-1, 4).tobytes() == ref_rgba.tobytes()
+            b = _bufs(torch, w * h)
+            m.render_frame(w, h, rgba8=b["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME)    # display-only payload
+            m.render_frame(w, h, compact=b["compact"].data_ptr(), hits=b["hits"].data_ptr(),
+                           layout=_lib.LAYOUT_FRAME)
+            m.synchronize()
+            _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba8", "compact"))
+        for k in range(len(devices)):
+            assert m.member(k).info()["n_nodes"] == len(svo)
+    finally:
+        m.close()
+
+
+def test_multi_device_shadow_rays(torch, oracle_mod):
+    """The C3 '+1 shadow ray' frame through the multi-device context: the
+    occlusion flag travels in the compact record and the display member
+    rebuilds the black Result."""
+    svo = build_menger(8)
+    w, h = 400, 240
+    cam = overview_camera()
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h, shadows=True)
+    m = RaytracingMaster(devices=[0, 0, 0], capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        m.SetShadowRays(True)
+        rgba, hits = m.Render(w, h)
+        assert np.count_nonzero(hits.reshape(-1)["flags"] & 8) > 0
+        assert hits.tobytes() == ref_hits.tobytes()
+        assert rgba.reshape(-1, 4).tobytes() == ref_rgba.tobytes()
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_assemble_from_rank_parts(torch, oracle_mod, world):
+    """The one-process-per-GPU split: each 'rank' renders its bands (band
+    layout) into a compact and an RGBA8 payload; svo_assemble_frame rebuilds the
+    frame from the parts -- what bench.py's rank 0 does after the RCCL gather."""
+    svo = build_menger(7)
+    cam = overview_camera()
+    w, h = 256, 200
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        comp, rgb8 = [], []
+        for r in range(world):
+            n = len(band_rows(h, (8, r, world))) * w
+            comp.append(torch.zeros(max(n, 1) * 12, dtype=torch.uint8, device="cuda"))
+            rgb8.append(torch.zeros(max(n, 1), dtype=torch.int32, device="cuda"))
+            m.render_frame(w, h, compact=comp[-1].data_ptr(), rgba8=rgb8[-1].data_ptr(), band=(8, r, world))
+        b = _bufs(torch, w * h)
+        m.assemble_frame(w, h, [c.data_ptr() for c in comp], _lib.PART_COMPACT, hits=b["hits"].data_ptr(),
+                         rgba=b["rgba"].data_ptr(), compact=b["compact"].data_ptr())
+        b2 = _bufs(torch, w * h)
+        m.assemble_frame(w, h, [c.data_ptr() for c in rgb8], _lib.PART_RGBA8, rgba8=b2["rgba8"].data_ptr())
+        m.synchronize()
+        _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba", "compact"))
+        _check(b2, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+        with pytest.raises(_lib.SvoError):   # RGBA8 parts cannot rebuild hit records
+            m.assemble_frame(w, h, [c.data_ptr() for c in rgb8], _lib.PART_RGBA8, hits=b["hits"].data_ptr())
+    finally:
+        m.close()
+
+
+def test_two_streams_every_pixel_written(torch, oracle_mod):
+    """Launches of one context alternating between two streams (advisor r1): the
+    shared dispatch-order buffers are rebuilt every launch (SVO_ORDER_EVERY=1)
+    and every frame is still complete and equal to the oracle's."""
+    import os
+    os.environ["SVO_ORDER_EVERY"] = "1"
+    try:
+        svo = build_menger(8)
+        m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    finally:
+        del os.environ["SVO_ORDER_EVERY"]
+    w, h = 640, 360
+    cam = overview_camera()
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        outs = [_bufs(torch, w * h) for _ in range(6)]
+        for i, b in enumerate(outs):
+            m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(),
+                           stream=streams[i % 2].cuda_stream)
+        torch.cuda.synchronize()
+        for b in outs:
+            _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+    finally:
+        m.close()
+
+
+def _rand_subtree(rng, depth, nodes, att, p_leaf=0.5):
+    """Append a random V2 subtree of exactly `depth` descriptor levels (one
+    branch always goes to the bottom) in the builder's layout: a node's non-leaf
+    children are contiguous, in ascending slot order.  Returns its root index."""
+    root = len(nodes)
+    nodes.append(0)
+    att.extend(rng.integers(0, 1 << 32, 2, dtype=np.uint64).tolist())
+    valid = int(rng.integers(1, 256))
+    if depth == 1:
+        nodes[root] = valid << 8
+        return root
+    nonleaf = valid & int(rng.integers(0, 256))
+    if nonleaf == 0:
+        nonleaf = valid & -valid
+    kids = [c for c in range(8) if (nonleaf >> c) & 1]
+    deep = int(rng.choice(kids))
+    first = len(nodes)
+    # reserve the contiguous child block, then fill each child's subtree after it
+    for _ in kids:
+        nodes.append(0)
+        att.extend([0, 0])
+    for j, c in enumerate(kids):
+        d = depth - 1 if c == deep else int(rng.integers(1, depth))
+        sub = _rand_subtree(rng, d, nodes, att)
+        # move the subtree root's descriptor into the reserved slot: point the slot at the same children
+        nodes[first + j] = nodes[sub]
+        att[2 * (first + j):2 * (first + j) + 2] = att[2 * sub:2 * sub + 2]
+    nodes[root] = (first << 32) | (valid << 8) | nonleaf
+    return root
+
+
+def _pool(nodes, att):
+    return SVOData(nodes=np.array(nodes, np.uint64), attachments=np.array(att, np.uint64).astype(np.uint32))
+
+
+def _render_vs_oracle(torch, oracle_mod, uploads, full_nodes, full_att, cam, w=200, h=150):
+    """uploads: [(SVOData, offset)] in upload order; oracle sees the combined pool."""
+    osvo = oracle_mod.OracleSVO(nodes=full_nodes, attachments=full_att)
+    c2w, inv_proj = cam.uniforms(w, h)
+    m = RaytracingMaster(device=0, capacity_nodes=len(full_nodes))
+    try:
+        for data, off in uploads:
+            m.SetSVOBuffer(data, offset=off)
+        m.UpdateShaderParameters(cam, w, h)
+        for mode in (0, 1):
+            rgba, hits = m.Render(w, h, stack_mode=mode)
+            ref, ref_rgba, _ = oracle_mod.render(osvo, oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light()),
+                                                 w, h, mode)
+            assert hits.tobytes() == ref.tobytes()
+            assert rgba.reshape(-1, 4).tobytes() == ref_rgba.tobytes()
+        return ref
+    finally:
+        m.close()
+
+
+def test_dag_pool_shared_node_at_two_depths(torch, oracle_mod):
+    """A shared 6-level subtree reached at depth 2 and at depth 4: the walk sees
+    the shallow path first, so the pool is traced with the full stack (a stack
+    sized from the shallow depth would overflow on the deep path)."""
+    rng = np.random.default_rng(3)
+    nodes, att = [0, 0, 0, 0], [0] * 8
+    # 0: root, children 1 (slot 0) and 2 (slot 7); 1 -> S directly; 2 -> 3 -> S
+    s_root = _rand_subtree(rng, 6, nodes, att)
+    # S's descriptor must sit where its parents point: make a one-node block holding a copy
+    nodes[0] = (1 << 32) | (0x81 << 8) | 0x81
+    nodes[1] = (s_root << 32) | (0x01 << 8) | 0x01        # slot 0 -> the block starting at S
+    nodes[2] = (3 << 32) | (0x80 << 8) | 0x80
+    nodes[3] = (s_root << 32) | (0x40 << 8) | 0x40
+    data = _pool(nodes, att)
+    full = np.array(nodes, np.uint64)
+    eye = np.array([20.0, 25.0, -30.0])
+    ref = _render_vs_oracle(torch, oracle_mod, [(data, 0)], full, data.attachments,
+                            Camera(position=tuple(eye), rotation=look_rotation(-eye)))
+    assert np.count_nonzero(ref["flags"] & 1) > 100
+    assert not np.any(ref["flags"] & 6)
+
+
+def test_three_linked_pools(torch, oracle_mod):
+    """A chain of sub-pools (the getLeaf linking of NaiveCreator.cs:156-159 /
+    Clipmap.cs:153-169, generalised): pool A at 0 links into B at 5000, B into C
+    at 9000; uploaded C, B, A.  Traced with the full stack, equal to the oracle."""
+    rng = np.random.default_rng(5)
+    def sub(depth, base):
+        n, a = [], []
+        _rand_subtree(rng, depth, n, a)
+        arr = np.array(n, np.uint64)
+        nonzero_first = (arr >> np.uint64(32)) != 0
+        arr[nonzero_first] += np.uint64(base) << np.uint64(32)
+        return arr, np.array(a, np.uint64).astype(np.uint32)
+    c_nodes, c_att = sub(3, 9000)
+    b_nodes, b_att = sub(3, 5000)
+    a_nodes, a_att = sub(3, 0)
+    # turn one leaf-level node of A / B into a link: a non-leaf slot pointing at the next pool's root
+    def link(arr, target):
+        for i in range(len(arr)):
+            if (int(arr[i]) & 0xFF) == 0 and (int(arr[i]) >> 8) & 0xFF:
+                arr[i] = np.uint64((target << 32) | (0x01 << 8) | 0x01)
+                return
+        raise AssertionError("no leaf-level node")
+    link(b_nodes, 9000)
+    link(a_nodes, 5000)
+    full = np.zeros(9000 + len(c_nodes), np.uint64)
+    full_att = np.zeros(2 * len(full), np.uint32)
+    for arr, at, off in ((a_nodes, a_att, 0), (b_nodes, b_att, 5000), (c_nodes, c_att, 9000)):
+        full[off:off + len(arr)] = arr
+        full_att[2 * off:2 * off + len(at)] = at
+    uploads = [(SVOData(nodes=c_nodes, attachments=c_att), 9000), (SVOData(nodes=b_nodes, attachments=b_att), 5000),
+               (SVOData(nodes=a_nodes, attachments=a_att), 0)]
+    eye = np.array([-18.0, 30.0, -26.0])
+    ref = _render_vs_oracle(torch, oracle_mod, uploads, full, full_att,
+                            Camera(position=tuple(eye), rotation=look_rotation(-eye)))
+    assert np.count_nonzero(ref["flags"] & 1) > 100

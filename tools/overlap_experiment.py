@@ -1,0 +1,56 @@
+"""Experiment: does overlapping consecutive frames (launches on S streams, each
+with its own output buffers) raise single-GPU throughput?  The render kernel's
+frame time is close to its heaviest wave's latency, so the
+ramp-down tail leaves SIMDs idle; a second frame in flight could fill them.
+
+Usage (GPU): python tools/overlap_experiment.py [--streams 1 2 3] [--steps 60]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--streams", type=int, nargs="+", default=[1, 2, 3])
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--camera", default="flyover")
+    a = ap.parse_args()
+    import torch
+    from raytracingtest_amd import RaytracingMaster
+    from raytracingtest_amd.camera import CAMERAS
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    os.environ.setdefault("SVO_ORDER_EVERY", "1000000000")   # order built once: no shared-buffer rewrite
+    svo = build_sampler_svo(4, 11, device=0)
+    W, H = 1920, 1080
+    for S in a.streams:
+        rm = RaytracingMaster(device=0, capacity_nodes=len(svo))
+        rm.SetSVOBuffer(svo)
+        rm.UpdateShaderParameters(CAMERAS[a.camera](), W, H)
+        streams = [torch.cuda.Stream() for _ in range(S)]
+        hits = [torch.empty(W * H * 24, dtype=torch.uint8, device="cuda") for _ in range(S)]
+        rgba = [torch.empty(W * H * 4, dtype=torch.float32, device="cuda") for _ in range(S)]
+
+        def step(i):
+            k = i % S
+            rm.render_device(W, H, rgba_ptr=rgba[k].data_ptr(), hits_ptr=hits[k].data_ptr(),
+                             stream=streams[k].cuda_stream)
+
+        for i in range(10):
+            step(i)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(a.steps):
+            step(i)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t) / a.steps * 1e3
+        print(f"streams={S}: {ms:.4f} ms/frame, {W * H / ms / 1e3:.1f} Mrays/s", flush=True)
+        rm.close()
+
+
+if __name__ == "__main__":
+    main()
