@@ -75,51 +75,117 @@ def test_camera_ray_center_pixel(oracle_mod):
     assert abs(np.linalg.norm(d) - 1) < 1e-6
 
 
-def _bruteforce_check(oracle_mod, svo, camera, w, h, stack_mode):
-    cam = _cam(oracle_mod, camera, w, h)
-    osvo = oracle_mod.OracleSVO(svo.childDescriptors, svo.attachments)
-    hits, _, _ = oracle_mod.render(osvo, cam, w, h, stack_mode)
-    leaves = svo.leaf_voxels()
+_FRAME_RAYS = {}
+
+
+def _frame_rays(oracle_mod, camera_name, w, h):
+    """World-space camera rays of every pixel (the oracle's CreateCameraRay)."""
+    key = (camera_name, w, h)
+    if key not in _FRAME_RAYS:
+        cam = _cam(oracle_mod, main_camera() if camera_name == "main" else overview_camera(), w, h)
+        o = np.zeros((h * w, 3), np.float32)
+        d = np.zeros((h * w, 3), np.float32)
+        for y in range(h):
+            for x in range(w):
+                o[y * w + x], d[y * w + x] = oracle_mod.camera_ray(cam, x, y, w, h)
+        _FRAME_RAYS[key] = (cam, o, d)
+    return _FRAME_RAYS[key]
+
+
+_BRUTE = {}
+
+
+@pytest.mark.parametrize("stack_mode", [0, 1])
+@pytest.mark.parametrize("camera_name", ["main", "overview"])
+def test_traversal_matches_bruteforce_full_c1_frame(oracle_mod, text_svo, camera_name, stack_mode):
+    """Every ray of the full 256x256 C1 frame (Text SVO, both cameras, both
+    stack modes) against the double-precision brute force over all 10,464
+    leaves: the oracle's voxel is a first-hit voxel up to ties, its t is the
+    voxel's entry distance, its scale the leaf's, and a miss only skips voxels
+    the ray grazes."""
+    from tests.bruteforce import first_hits_compact
+    w = h = 256
+    cam, o, d = _frame_rays(oracle_mod, camera_name, w, h)
+    hits, _, _ = oracle_mod.render(oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments),
+                                   cam, w, h, stack_mode)
+    leaves = text_svo.leaf_voxels()
+    oo = o.astype(np.float64) / 32.0 + 1.5
+    dd = d.astype(np.float64)
+    if camera_name not in _BRUTE:
+        _BRUTE[camera_name] = first_hits_compact(leaves, oo, dd)
+    best_row, best_t, max_ov = _BRUTE[camera_name]
+    miss = hits["parent"] == 0xFFFFFFFF
+    assert not np.any(max_ov[miss] > 1e-5), "oracle miss where the brute force crosses a voxel"
+    assert not np.any(~miss & (best_row < 0) & (max_ov < -1)), "oracle hit where the ray touches no voxel"
     key = {(int(r[0]), int(r[1])): i for i, r in enumerate(leaves)}
-    origins, dirs = [], []
-    for y in range(h):
-        for x in range(w):
-            o, d = oracle_mod.camera_ray(cam, x, y, w, h)
-            oo, dd = svo_space_ray(o, d)
-            origins.append(oo)
-            dirs.append(dd)
-    best_row, best_t, te, ov = first_hits(leaves, np.array(origins), np.array(dirs))
     n_hit = 0
-    for i, hrec in enumerate(hits):
-        if hrec["parent"] == 0xFFFFFFFF:
-            # a miss may only skip voxels the ray grazes (edge/corner contact)
-            assert not np.any(ov[i] > 1e-5), f"ray {i}: oracle miss, brute force hit at {best_t[i]}"
-            continue
-        n_hit += 1
+    for i in np.flatnonzero(~miss):
+        hrec = hits[i]
         row = key[(int(hrec["parent"]), int(hrec["hit_idx"]))]
-        # float32 t-math (t = pos * coef - bias, coef = -1/|d|) carries an absolute
-        # error of a few ulp of |bias| ~ 3/|d_min|: the tie tolerance scales with it
-        nz = np.abs(dirs[i])[np.abs(dirs[i]) > 0]
+        nz = np.abs(dd[i])[np.abs(dd[i]) > 0]
         tol = 1e-6 * (1.0 + 3.0 / nz.min())
-        t_in, t_out = entry_exit(leaves[row], origins[i], dirs[i])
+        t_in, t_out = entry_exit(leaves[row], oo[i], dd[i])
         assert t_in <= t_out + tol, f"ray {i}: oracle voxel not on the ray"
-        # the oracle's voxel is a first-hit voxel up to ties
         assert t_in <= best_t[i] + tol, f"ray {i}: oracle voxel enters at {t_in} > {best_t[i]}"
         assert abs(hrec["t"] / 2048.0 - t_in) <= tol
         assert hrec["hit_scale"] == 23 - leaves[row, 2]
-    return n_hit
+        n_hit += 1
+    assert n_hit > 2000
 
 
-@pytest.mark.parametrize("stack_mode", [0, 1])
-def test_traversal_matches_bruteforce_main_camera(oracle_mod, text_svo, stack_mode):
-    n_hit = _bruteforce_check(oracle_mod, text_svo, main_camera(), 48, 48, stack_mode)
-    assert n_hit > 100
+@pytest.mark.parametrize("camera_name", ["main", "overview"])
+def test_oracle_exact_mode_matches_csharp_raystep(oracle_mod, text_fixture, text_svo, camera_name):
+    """Second independent witness of the hot loop: the reference's own C# CPU
+    tracer NVIDIAIterativeNaiveTracer.RayStep (NVIDIAIterativeTracer.cs:72-290),
+    restated in tests/cs_tracer.py over ABSOLUTE pointers (the Text dump's native
+    form), exact stack, popc8 LUT, t_max clamped to 1 (:112).  On the full 256x256
+    C1 frames the oracle's EXACT stack mode must give the same voxel (parent,
+    hit_idx, scale) and bit-identical t for every ray whose hit lies within
+    t_svo <= 1 -- the clamp cannot change any decision before such a hit, since
+    t_min only grows and stays <= 1 -- and the C# tracer must miss every other ray."""
+    from tests.cs_tracer import descriptors_absolute, ray_step
+    w = h = 256
+    cam, o, d = _frame_rays(oracle_mod, camera_name, w, h)
+    hits, _, _ = oracle_mod.render(oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments),
+                                   cam, w, h, oracle_mod.STACK_EXACT)
+    z = text_fixture
+    svo_cs = descriptors_absolute(z["abs_child_ptr"], z["valid_mask"], z["nonleaf_mask"])
+    # the HLSL world -> SVO transform (NVIDIASVO.compute:15-19) feeds the caller-space C# tracer
+    o_svo = o * np.float32(1.0 / 32.0) + np.float32(1.5)
+    r = ray_step(svo_cs, o_svo, d)
+    reach = (hits["parent"] != 0xFFFFFFFF) & (hits["t"] <= np.float32(2048.0))
+    assert np.array_equal(r["hit"], reach), f"{np.count_nonzero(r['hit'] != reach)} rays differ in hit/miss"
+    assert np.array_equal(r["parent"][reach], hits["parent"][reach].astype(np.int64))
+    assert np.array_equal(r["hit_idx"][reach], hits["hit_idx"][reach].astype(np.int32))
+    assert np.array_equal(r["scale"][reach], hits["hit_scale"][reach].astype(np.int32))
+    t_cs = (r["t_min"][reach] * np.float32(2048.0)).astype(np.float32)
+    assert t_cs.tobytes() == hits["t"][reach].astype(np.float32).tobytes()
+    assert np.count_nonzero(reach) > 2000
 
 
-@pytest.mark.parametrize("stack_mode", [0, 1])
-def test_traversal_matches_bruteforce_overview(oracle_mod, text_svo, stack_mode):
-    n_hit = _bruteforce_check(oracle_mod, text_svo, overview_camera(), 48, 48, stack_mode)
-    assert n_hit > 100
+def test_decode_dxt_color_worked_example(oracle_mod):
+    """The reference's worked attachment example (NaiveCreator.cs:260-292, printed
+    by TestDecompressAttachment :296-345 with Vector3's F1 format): NodeAColor
+    0100110001111100 and NodeBColor 1110011011101011 decode through
+    decodeDXTColor to C0 (0.5, 0.8, 0.7) and C1..C7 (0.9, 0.6, 0.3).  The printed
+    ColorChoices line is stale (all ones would make every child C0's colour);
+    the printed children need child 0's choice = 3 and the others 0, i.e.
+    bits = 3.  The raw attachment string pins the 64-bit layout A | B << 16 |
+    choices << 32 | normal << 48 (GetAttachment :247)."""
+    a, b = 0b0100110001111100, 0b1110011011101011
+    raw = "1111111111111111111111111111111111100110111010110100110001111100"
+    v = int(raw, 2)
+    assert v & 0xFFFF == a and (v >> 16) & 0xFFFF == b and (v >> 32) & 0xFFFF == 0xFFFF
+    head = a | (b << 16)
+    want = [(0.5, 0.8, 0.7)] + [(0.9, 0.6, 0.3)] * 7
+    for texel, w in enumerate(want):
+        got = oracle_mod.decode_dxt_color(head, 3, texel).astype(np.float64)
+        assert np.all(np.abs(got - w) <= 0.05 + 1e-6), (texel, got)
+    # "Partially Decompressed" (DecompressColor, :357-362): R in the low 5 bits
+    def decompress(c):
+        return np.array([(c & 31) / 31.0, ((c >> 5) & 63) / 63.0, (c >> 11) / 31.0])
+    assert np.all(np.abs(decompress(a) - (0.9, 0.6, 0.3)) <= 0.05 + 1e-6)
+    assert np.all(np.abs(decompress(b) - (0.4, 0.9, 0.9)) <= 0.05 + 1e-6)
 
 
 def test_v1_and_v2_pools_identical(oracle_mod, text_svo):
