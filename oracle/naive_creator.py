@@ -369,7 +369,14 @@ def get_attachment(node):   # NaiveCreator.cs:195-257
     return att & 0xFFFFFFFF, (att >> 32) & 0xFFFFFFFF
 
 
-def compress(root):   # CompressSVO / CompressSVOAux, NaiveCreator.cs:132-193
+def compress(root, get_leaf=None):   # CompressSVO / CompressSVOAux, NaiveCreator.cs:132-193
+    """get_leaf: NaiveCreator.GetLeaf (:28-29, used at :156-159): every leaf child
+    becomes a link -- its valid bit stays, its leaf bit is not set (so the
+    shader takes it as a non-leaf child), and the node's child pointer is
+    overwritten with get_leaf(child) - nodeIndex for each leaf child in slot
+    order (the last one wins).  The reference passes (int)position and size
+    (a Vector4Int); here the callback gets the child's integer coordinates at
+    its level and the level: get_leaf(ix, iy, iz, level)."""
     nodes = [0]
     att = [0, 0]
 
@@ -385,7 +392,12 @@ def compress(root):   # CompressSVO / CompressSVOAux, NaiveCreator.cs:132-193
                 continue
             valid |= 1 << c
             if ch.leaf:
-                leaf_mask |= 1 << c
+                if get_leaf is not None:
+                    scale = F(2) ** (ch.level - 1)
+                    ix, iy, iz = (int(F(F(ch.position[k] - F(1)) * scale)) for k in range(3))
+                    ptr = get_leaf(ix, iy, iz, ch.level) - idx
+                else:
+                    leaf_mask |= 1 << c
             else:
                 if ptr == 0:
                     ptr = len(nodes) - idx
@@ -407,8 +419,10 @@ def compress(root):   # CompressSVO / CompressSVOAux, NaiveCreator.cs:132-193
     return np.array(nodes, np.uint32).view(np.int32), np.array(att, np.uint32)
 
 
-def create(sample_kind, max_level):
-    """NaiveCreator.Create(SampleFunctions.functions[kind], maxLevel) -> (descriptors, attachments)."""
+def create(sample_kind, max_level, get_leaf=None):
+    """NaiveCreator.Create(SampleFunctions.functions[kind], maxLevel) -> (descriptors,
+    attachments); with get_leaf, the tree built that way is compressed as by
+    NaiveCreator.Create(root, getLeaf) (NaiveCreator.cs:30-42)."""
     root = Node(v3(1, 1, 1), 1, 1, False)
     build_tree(root, 1, sampler(sample_kind), max_level)
-    return compress(root)
+    return compress(root, get_leaf)

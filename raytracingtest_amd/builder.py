@@ -287,3 +287,50 @@ def build_svo_for_sampler(sample_type, max_level):
     """RaytracingMaster.SetSVOBuffer() path: NaiveCreator.Create(SampleFunctions.functions[t], maxLevel)."""
     from .native_builder import build_sampler_svo
     return build_sampler_svo(sample_type, max_level)
+
+
+# ------------------------------------------------------------ leaf linking
+def link_leaves(svo, get_leaf):
+    """NaiveCreator.Create(root, getLeaf) (NaiveCreator.cs:30-42, :156-159) on a
+    built pool: every leaf child becomes a link into a separately uploaded
+    sub-SVO (Clipmap.UpdateMasterOctree, Clipmap.cs:153-169, links every chunk
+    leaf to one sphere SVO uploaded at descriptor 10000).  The child keeps its
+    valid bit and loses its leaf bit (the traversal descends into it); the
+    node's child pointer is get_leaf(child) - node for the LAST leaf child in
+    slot order (the reference overwrites it per leaf child), so linked child k
+    of a node lands on descriptor target + rank(k).
+
+    get_leaf(ix, iy, iz, level) -> absolute descriptor index (the reference
+    passes the child's (int)position and size; see oracle/naive_creator.py).
+    A node holding both leaf and non-leaf children cannot be linked (the
+    reference would lay the non-leaf children out at the link target) and is
+    rejected.  Returns a new SVOData (V1 when every pointer fits 16 bits)."""
+    lo, first = svo.masks_and_first()
+    valid = (lo >> 8) & 0xFF
+    nonleaf = lo & 0xFF
+    leaves = svo.leaf_voxels()                      # (node, slot, L, ix, iy, iz)
+    if len(leaves) == 0:
+        return svo
+    nodes = np.unique(leaves[:, 0])
+    mixed = nodes[nonleaf[nodes] != 0]
+    if len(mixed):
+        raise ValueError(f"node {int(mixed[0])} holds leaf and non-leaf children: cannot link its leaves")
+    # last leaf child of every node (slot order)
+    order = np.lexsort((leaves[:, 1], leaves[:, 0]))
+    rows = leaves[order]
+    last = np.concatenate([rows[1:, 0] != rows[:-1, 0], [True]])
+    new_lo = lo.copy()
+    new_first = first.astype(np.int64).copy()
+    for r in rows[last]:
+        node = int(r[0])
+        target = int(get_leaf(int(r[3]), int(r[4]), int(r[5]), int(r[2]) + 1))
+        if target <= node or target >= 1 << 32:
+            raise ValueError(f"link target {target} of node {node} must lie after the node")
+        new_lo[node] = (valid[node] << 8) | valid[node]
+        new_first[node] = target
+    nodes_v2 = (new_first.astype(np.uint64) << np.uint64(32)) | new_lo.astype(np.uint64)
+    data = SVOData(nodes=nodes_v2, attachments=svo.attachments.copy())
+    try:
+        return data.to_v1()
+    except Exception:
+        return data

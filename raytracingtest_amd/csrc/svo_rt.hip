@@ -189,7 +189,7 @@ int walk_depth(const uint32_t *lo, const uint32_t *first, size_t n, size_t base,
                 uint64_t child = (uint64_t)f + (uint64_t)rank++;
                 if (child >= pool_n) {
                     *err = "child pointer of node " + std::to_string(base + li) + " -> " +
-                           std::to_string(child) + " outside the pool (" + std::to_string(pool_n) + ")";
+                           std::to_string(child) + " outside the node-pool capacity (" + std::to_string(pool_n) + ")";
                     return -1;
                 }
                 if (child < base || child >= base + n) { external = true; continue; }
@@ -225,8 +225,11 @@ int validate_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, siz
     std::string err;
     int depth = 0;
     bool ext = false, tree = true;
-    size_t pool_n = std::max(ctx->n_nodes, base + n);
-    if (walk_depth(lo, first, n, base, pool_n, &depth, &ext, &tree, &err) != 0) return fail(SVO_ERR_FORMAT, err);
+    // links may point past what is uploaded so far (the reference uploads the trunk
+    // before the sub-SVO it links to, Clipmap.cs:158,168): any index inside the
+    // capacity is legal; the pool is zero-filled at svo_create, so a link into a
+    // region not uploaded yet reads empty descriptors
+    if (walk_depth(lo, first, n, base, ctx->capacity, &depth, &ext, &tree, &err) != 0) return fail(SVO_ERR_FORMAT, err);
     *out = Upload{base, n, depth, ext, tree};
     return SVO_OK;
 }
@@ -585,6 +588,11 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     hipError_t e = hipMalloc(&ctx->d_nodes, capacity_nodes * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&ctx->d_att, capacity_nodes * sizeof(uint2));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    // zero-filled pool: descriptors never uploaded read as empty (0), like the
+    // fresh ComputeBuffers of RaytracingMaster.InitializeSVOBuffer
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->d_nodes, 0, capacity_nodes * sizeof(uint2), ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->d_att, 0, capacity_nodes * sizeof(uint2), ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) == 0 ? 0 : 2;
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;

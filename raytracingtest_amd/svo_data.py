@@ -220,13 +220,12 @@ class SVOData:
             version, fmt, n = struct.unpack("<IIQ", head[4:])
             if version != FILE_VERSION or fmt not in (1, 2):
                 raise SVOFormatError(f"unsupported SVOP version/format {version}/{fmt}")
-            if fmt == 1:
-                body = np.frombuffer(fh.read(4 * n), "<i4")
-            else:
-                body = np.frombuffer(fh.read(8 * n), "<u8")
-            att = np.frombuffer(fh.read(8 * n), "<u4")
-            if len(body) != n or len(att) != 2 * n:
-                raise SVOFormatError("truncated SVOP file")
+            width = 4 if fmt == 1 else 8
+            raw_body, raw_att = fh.read(width * n), fh.read(8 * n)
+            if len(raw_body) != width * n or len(raw_att) != 8 * n or fh.read(1):
+                raise SVOFormatError("truncated or oversized SVOP file")
+            body = np.frombuffer(raw_body, "<i4" if fmt == 1 else "<u8")
+            att = np.frombuffer(raw_att, "<u4")
         if fmt == 1:
             return cls(childDescriptors=body.copy(), attachments=att.copy())
         return cls(nodes=body.copy(), attachments=att.copy())

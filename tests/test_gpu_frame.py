@@ -384,3 +384,52 @@ def test_three_linked_pools(torch, oracle_mod):
     ref = _render_vs_oracle(torch, oracle_mod, uploads, full, full_att,
                             Camera(position=tuple(eye), rotation=look_rotation(-eye)))
     assert np.count_nonzero(ref["flags"] & 1) > 100
+
+
+def test_clipmap_linked_sub_svo_trunk_first(torch, oracle_mod):
+    """Clipmap.UpdateMasterOctree (Clipmap.cs:153-169): a trunk built with every
+    leaf linked to descriptor 10000 (NaiveCreator.Create(root, x => 10000),
+    NaiveCreator.cs:156-159; builder.link_leaves) is uploaded FIRST, then the
+    sub-SVO at offset 10000 (SetSVOBuffer(data, 10000)).  Between the two uploads
+    the links read the zero-filled pool (empty descriptors); after the second,
+    the frame equals the oracle's over the combined pool, both stack modes."""
+    from raytracingtest_amd.builder import link_leaves
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    base = 10000
+    trunk = link_leaves(build_sampler_svo(4, 4), lambda *a: base)
+    sub = build_sampler_svo(4, 7)
+    assert trunk.format == 1 and sub.format == 1 and len(trunk) < base
+    full = np.zeros(base + len(sub), np.uint64)
+    full[:len(trunk)] = trunk.to_v2()
+    sub_v2 = sub.to_v2().copy()
+    has = (sub_v2 >> np.uint64(32)) != 0
+    sub_v2[has] += np.uint64(base) << np.uint64(32)
+    full[base:] = sub_v2
+    full_att = np.zeros(2 * len(full), np.uint32)
+    full_att[:len(trunk.attachments)] = trunk.attachments
+    full_att[2 * base:] = sub.attachments
+    trunk_only = full.copy()
+    trunk_only[base:] = 0
+    eye = np.array([26.0, 30.0, -34.0])
+    cam = Camera(position=tuple(eye), rotation=look_rotation(-eye))
+    w, h = 320, 200
+    c2w, inv_proj = cam.uniforms(w, h)
+    ocam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
+    m = RaytracingMaster(device=0, capacity_nodes=len(full))
+    try:
+        m.SetSVOBuffer(trunk)
+        m.UpdateShaderParameters(cam, w, h)
+        _, hits0 = m.Render(w, h)
+        ref0, _, _ = oracle_mod.render(oracle_mod.OracleSVO(nodes=trunk_only, attachments=full_att), ocam, w, h)
+        assert hits0.tobytes() == ref0.tobytes()
+        m.SetSVOBuffer(sub, offset=base)
+        for mode in (0, 1):
+            rgba, hits = m.Render(w, h, stack_mode=mode)
+            ref, ref_rgba, _ = oracle_mod.render(oracle_mod.OracleSVO(nodes=full, attachments=full_att), ocam, w, h,
+                                                 mode)
+            assert hits.tobytes() == ref.tobytes()
+            assert rgba.reshape(-1, 4).tobytes() == ref_rgba.tobytes()
+        linked = np.count_nonzero((ref["flags"] & 1) != 0)
+        assert linked > 500 and np.all(ref["parent"][(ref["flags"] & 1) != 0] >= base)
+    finally:
+        m.close()

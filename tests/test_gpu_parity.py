@@ -183,9 +183,9 @@ def test_errors_are_loud(rm):
     try:
         with pytest.raises(SvoError):
             m.Render(8, 8)                       # no pool uploaded
-        bad = SVOData(childDescriptors=np.array([(5 << 16) | 0x0101], np.int32))
+        bad = SVOData(childDescriptors=np.array([(100 << 16) | 0x0101], np.int32))
         with pytest.raises(SvoError):
-            m.SetSVOBuffer(bad)                  # child pointer outside the pool
+            m.SetSVOBuffer(bad)                  # child pointer outside the capacity
         with pytest.raises(SvoError):
             m.SetSVOBuffer(build_from_leaves(4, np.argwhere(np.ones((16, 16, 16))), np.ones((4096, 3), np.float32)))
     finally:
