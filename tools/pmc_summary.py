@@ -57,6 +57,7 @@ def main():
         "hbm_bytes_per_launch": 2 * fetch_b + write_b,
         "hbm_bytes_per_launch_raw": fetch_b + write_b,
         "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
+        "kernel_source_sha1": lines[0]["roofline"].get("kernel_source_sha1") if lines else None,
         "source": os.path.basename(dest),
         "note": "FETCH_SIZE x2 (gfx950 half-count correction, upper bound for 8-B gathers) + WRITE_SIZE",
     }
