@@ -79,12 +79,15 @@ def parse():
     p.add_argument("--payload", choices=["rgba8", "compact"], default="rgba8",
                    help="N > 1: what moves to the display rank: RGBA8 display words (4 B/px) or compact "
                         "records (12 B/px, rank 0 rebuilds hit records + Result)")
+    p.add_argument("--devices", default=None,
+                   help="one-process multi-device mode: comma-separated HIP device indices of the context's members "
+                        "(default 0..N-1; an index may repeat to rehearse the split on one GPU)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--no-rgba", action="store_true")
     p.add_argument("--camera", choices=["flyover", "overview", "main", "terrain"], default=None)
     p.add_argument("--shadows", action="store_true", help="C3 '+1 shadow ray' pass after the primary rays")
-    p.add_argument("--extra-poses", action="store_true",
-                   help="N = 1: also time the frame from the other camera poses (reported beside value)")
+    p.add_argument("--no-extra-poses", dest="extra_poses", action="store_false",
+                   help="N = 1: skip timing the frame from the other camera poses (reported beside value)")
     a = p.parse_args()
     cfg = CONFIGS[a.config]
     for k in ("width", "height", "max_level", "sampler", "camera", "stack_mode"):
@@ -137,7 +140,11 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but torchrun started WORLD_SIZE={world_env} ranks")
     mode = "ranks" if world_env > 1 else ("multidevice" if args.gpus > 1 else "single")
     import torch
-    if torch.cuda.device_count() < (args.gpus if mode == "multidevice" else 1):
+    args.device_list = ([int(d) for d in args.devices.split(",")] if args.devices else list(range(args.gpus)))
+    if mode == "multidevice" and len(args.device_list) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but --devices names {len(args.device_list)} devices")
+    need = max(args.device_list) + 1 if mode == "multidevice" else 1
+    if torch.cuda.device_count() < need:
         raise SystemExit(f"bench.py: {args.gpus} GPUs requested, {torch.cuda.device_count()} visible")
     world = args.gpus
     rank = int(os.environ.get("RANK", "0"))
@@ -460,10 +467,10 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
     import torch
     from raytracingtest_amd import RaytracingMaster
     n = args.gpus
-    rm = RaytracingMaster(devices=list(range(n)), capacity_nodes=len(svo))
+    rm = RaytracingMaster(devices=args.device_list, capacity_nodes=len(svo))
     rm.SetSVOBuffer(svo)
     rm.UpdateShaderParameters(cam, W, H)
-    dev0 = torch.device("cuda", 0)
+    dev0 = torch.device("cuda", args.device_list[0])
     frame8 = torch.empty(W * H, dtype=torch.int32, device=dev0)
     s = torch.cuda.Stream(dev0)
 
@@ -471,7 +478,7 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
         rm.render_frame(W, H, rgba8=frame8.data_ptr(), layout=1, stack_mode=args.stack_mode, stream=s.cuda_stream)
 
     def sync_all():
-        for d in range(n):
+        for d in sorted(set(args.device_list)):
             torch.cuda.synchronize(d)
 
     for _ in range(max(1, args.warmup)):
@@ -499,7 +506,8 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
         "data": "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement",
         "config": {"workload": f"{args.config} {W}x{H} primary rays, {args.camera} camera, display RGBA8 frame",
                    "parallelism": f"multidevice{n}x8rows+xgmi_pull", "build_s": round(build_s, 2)},
-        "multi_gpu": {"per_device_kernel_ms": [round(k, 4) for k in kern], "assemble_ms": round(asm_ms, 4)},
+        "multi_gpu": {"devices": args.device_list, "per_device_kernel_ms": [round(k, 4) for k in kern],
+                      "assemble_ms": round(asm_ms, 4)},
     }), flush=True)
 
 

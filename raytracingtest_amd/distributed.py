@@ -63,6 +63,17 @@ def gather_parts(send, parts, dst=0, dist=None, group=None):
     ordered after the caller's current stream; on gloo it is a CPU copy."""
     if dist is None:
         import torch.distributed as dist
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo gathers host tensors only: the one-GPU rehearsal of the N > 1 path
+        # (tools/rehearse_ranks.sh) stages through host memory; RCCL moves device
+        # memory over xGMI directly
+        host = send.cpu()
+        hparts = [p.cpu() for p in parts] if parts is not None else None
+        dist.gather(host, gather_list=hparts, dst=dst, group=group)
+        if parts is not None:
+            for p, h in zip(parts, hparts):
+                p.copy_(h)
+        return
     dist.gather(send, gather_list=parts, dst=dst, group=group)
 
 

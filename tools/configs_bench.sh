@@ -3,7 +3,7 @@
 # their 4/8-GPU split is the driver's multi-GPU run).  Usage: [CPU_SECONDS=5] bash tools/configs_bench.sh <tag>
 set -o pipefail
 OUT=gpurun_out/$1; mkdir -p $OUT
-for c in C1 C2 C4 C5; do
+for c in ${CONFIGS:-C1 C2 C4 C5}; do
   timeout -k 10 300 python bench.py --config $c --steps 30 --warmup 3 --cpu-seconds ${CPU_SECONDS:-0} > $OUT/config_$c.json 2>> $OUT/configs.err || exit $?
 done
 echo done

@@ -24,20 +24,22 @@ def main():
     from raytracingtest_amd import RaytracingMaster
     from raytracingtest_amd.camera import CAMERAS
     from raytracingtest_amd.native_builder import build_sampler_svo
-    os.environ.setdefault("SVO_ORDER_EVERY", "1000000000")   # order built once: no shared-buffer rewrite
     svo = build_sampler_svo(4, 11, device=0)
     W, H = 1920, 1080
     for S in a.streams:
-        rm = RaytracingMaster(device=0, capacity_nodes=len(svo))
-        rm.SetSVOBuffer(svo)
-        rm.UpdateShaderParameters(CAMERAS[a.camera](), W, H)
+        # one context per stream (own pool replica and scheduling state): nothing
+        # shared, so the library does not order the streams against each other
+        rms = [RaytracingMaster(device=0, capacity_nodes=len(svo)) for _ in range(S)]
+        for rm in rms:
+            rm.SetSVOBuffer(svo)
+            rm.UpdateShaderParameters(CAMERAS[a.camera](), W, H)
         streams = [torch.cuda.Stream() for _ in range(S)]
         hits = [torch.empty(W * H * 24, dtype=torch.uint8, device="cuda") for _ in range(S)]
         rgba = [torch.empty(W * H * 4, dtype=torch.float32, device="cuda") for _ in range(S)]
 
         def step(i):
             k = i % S
-            rm.render_device(W, H, rgba_ptr=rgba[k].data_ptr(), hits_ptr=hits[k].data_ptr(),
+            rms[k].render_device(W, H, rgba_ptr=rgba[k].data_ptr(), hits_ptr=hits[k].data_ptr(),
                              stream=streams[k].cuda_stream)
 
         for i in range(10):
@@ -49,7 +51,8 @@ def main():
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) / a.steps * 1e3
         print(f"streams={S}: {ms:.4f} ms/frame, {W * H / ms / 1e3:.1f} Mrays/s", flush=True)
-        rm.close()
+        for rm in rms:
+            rm.close()
 
 
 if __name__ == "__main__":

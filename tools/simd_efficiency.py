@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--max-level", type=int, default=11)
     ap.add_argument("--save", default=None)
     ap.add_argument("--load", default=None, help="npz written by --save (no GPU needed)")
+    ap.add_argument("--save-iters", default=None, help="npz of the per-ray iteration / fetch counts and hit flags")
     args = ap.parse_args()
     from oracle import oracle as orc
     from raytracingtest_amd.camera import CAMERAS, main_light
@@ -44,6 +45,10 @@ def main():
     hits, _, it = orc.render(osvo, ocam, W, H, orc.COUNT_ITERS, nthreads=min(16, os.cpu_count() or 1),
                              want_rgba=False)
     _, _, fe = orc.render(osvo, ocam, W, H, 0, nthreads=min(16, os.cpu_count() or 1), want_rgba=False)
+    if args.save_iters:
+        np.savez_compressed(args.save_iters, iters=it.reshape(H, W).astype(np.uint16),
+                            fetches=fe.reshape(H, W).astype(np.uint16),
+                            hit=((hits["flags"] & 1) != 0).reshape(H, W))
     it = it.reshape(H // 8, 8, W // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64).astype(np.int64)
     fe = fe.reshape(H // 8, 8, W // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64).astype(np.int64)
     hit = ((hits["flags"] & 1) != 0).reshape(H // 8, 8, W // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64)
