@@ -12,9 +12,10 @@ Inputs (node pool, camera) are resident before the timed region.
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one rank per
 GPU, the SVO replicated per GPU (each rank builds the same bytes on its GPU),
 the frame split into 8-row bands dealt round-robin to the ranks (SURVEY.md
-8(e)), and every step ends with the north-star gather: each rank's RGBA8 band
-payload goes to rank 0 over RCCL (one gather) and rank 0's plugin rebuilds the
-display frame (svo_assemble_frame).  The gather of frame k overlaps the render
+8(e)), and every step ends with the north-star gather: rank 0 (the display
+GPU) renders its own bands straight into the display frame, every other rank's
+RGBA8 band payload goes to rank 0 over RCCL (one batch of sends / receives)
+and rank 0's plugin writes their rows into the frame (svo_assemble_frame).  The gather of frame k overlaps the render
 of frame k+1 (two streams, double-buffered payloads).  For C1-C3 the frame is
 the same camera at sqrt(N) times the linear resolution, so every GPU traces
 ~1920x1080 rays per step (weak scaling); C4 / C5 keep their configured frame
@@ -192,22 +193,24 @@ def main():
     rows = D.band_len(H, rank, world) if world > 1 else H
     n_px = W * rows
 
-    hits = torch.empty(n_px * 24, dtype=torch.uint8, device=dev)
-    rgba = None if args.no_rgba else torch.empty(n_px * 4, dtype=torch.float32, device=dev)
     # a dedicated (non-null) stream: the kernel and the timing events share it
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     gather = None
     if world > 1:
-        gather = Gather(rm, W, H, rank, world, dev, args.payload, stream)
+        gather = Gather(rm, W, H, rank, world, dev, args.payload, stream, args.no_rgba)
+        hits = rgba = None
+    else:
+        hits = torch.empty(n_px * 24, dtype=torch.uint8, device=dev)
+        rgba = None if args.no_rgba else torch.empty(n_px * 4, dtype=torch.float32, device=dev)
 
     def step():
         if gather is None:
             rm.render_device(W, H, rgba_ptr=None if rgba is None else rgba.data_ptr(), hits_ptr=hits.data_ptr(),
                              stack_mode=args.stack_mode, stream=sptr)
         else:
-            gather.step(hits, rgba, args.stack_mode)
+            gather.step(args.stack_mode)
 
     # instrumented pass (outside the timed region): per-ray fetch counts
     fetch = torch.zeros(n_px, dtype=torch.int32, device=dev)
@@ -215,14 +218,14 @@ def main():
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize(dev)
-    host_hits = hits.cpu().numpy().view(_lib.HIT_DTYPE)
+    host_hits = (hits if gather is None else gather.local_hits()).cpu().numpy().view(_lib.HIT_DTYPE)
     n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
     F = int(fetch.to(torch.int64).sum().item())
-    bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if rgba is None else 16 * n_px)
+    bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if args.no_rgba else 16 * n_px)
     if gather is not None:
-        bytes_per_launch += 4 * n_px   # the RGBA8 (or 12-B compact) band payload the kernel also writes
-        if args.payload == "compact":
-            bytes_per_launch += 8 * n_px
+        # the RGBA8 display words (rank 0, in the frame) or band payload (4 B RGBA8 / 12-B compact
+        # records) the kernel also writes
+        bytes_per_launch += (12 if args.payload == "compact" and rank != 0 else 4) * n_px
 
     # timed region: K steps between barrier + synchronize.  HIP events around each
     # step only with SVO_STEP_EVENTS=1 (diagnostics): their stream markers add
@@ -258,7 +261,8 @@ def main():
     torch.cuda.synchronize(dev)
     if n_timed != args.steps:
         raise RuntimeError(f"kernel timing: {n_timed} launches recorded, {args.steps} expected")
-    stages = gather.stage_times(hits, rgba, args.stack_mode, max(3, args.steps // 2)) if gather else None
+    stages = gather.stage_times(args.stack_mode, max(3, args.steps // 2)) if gather else None
+    frame_check = gather.check_frame(args.stack_mode) if gather is not None and rank == 0 else None
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -358,7 +362,8 @@ def main():
                 "per_rank_kernel_gather_assemble_ms": per_rank,
                 "render_only_Mrays": round(rays_per_step / (kern_ms_max * 1e-3) / 1e6, 2),
                 "gather_ms_rank0": round(stages["gather_ms"], 4), "assemble_ms_rank0": round(stages["assemble_ms"], 4),
-                "payload_bytes_per_rank": stages["payload_bytes"],
+                "payload_bytes_per_sending_rank": stages["payload_bytes"],
+                "assembled_frame_check": frame_check,
                 "note": "value overlaps the gather of frame k with the render of frame k+1; render_only_Mrays is "
                         "the frame's rays over the slowest rank's render kernel alone; gather/assemble from a "
                         "serialized pass (events on the gather stream)"}
@@ -373,12 +378,15 @@ def main():
 class Gather:
     """One rank's render + gather + assemble pipeline (bench's N > 1 step).
 
-    Render on the caller's stream R into the rank's band buffers and a
-    double-buffered payload; gather stream G waits for it, gathers the payloads
-    to rank 0 over RCCL and rank 0 rebuilds the frame; the next render into the
-    same payload slot waits for that gather (two frames in flight)."""
+    Render on the caller's stream R: the display rank (0) straight into display
+    frame k (frame layout: its own bands' rows of the RGBA8 frame, and of the
+    full hit-record / Result frames for the compact payload); every other rank
+    into its band buffers and payload k.  Gather stream G waits for the render,
+    moves the payloads to rank 0 in one batch of RCCL sends / receives, and rank
+    0 rebuilds the other ranks' rows of frame k (svo_assemble_frame, skipping its
+    own part); the next render into slot k waits for that (two frames in flight)."""
 
-    def __init__(self, rm, W, H, rank, world, dev, payload, stream):
+    def __init__(self, rm, W, H, rank, world, dev, payload, stream, no_rgba):
         import torch
         from raytracingtest_amd import _lib
         from raytracingtest_amd import distributed as D
@@ -390,61 +398,104 @@ class Gather:
         per = D.max_band_len(H, world) * W * self.elem // 4
         self.R = stream
         self.G = torch.cuda.Stream(dev)
-        self.send = [torch.zeros(per, dtype=torch.int32, device=dev) for _ in range(2)]
-        self.parts = [[torch.empty(per, dtype=torch.int32, device=dev) for _ in range(world)] if rank == 0 else None
-                      for _ in range(2)]
-        self.frame8 = torch.empty(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
-        self.frame_hits = torch.empty(W * H * 24, dtype=torch.uint8, device=dev) if rank == 0 and payload == "compact" else None
-        self.frame_rgba = torch.empty(W * H * 4, dtype=torch.float32, device=dev) if rank == 0 and payload == "compact" else None
+        n_local = D.band_len(H, rank, world) * W
+        if rank == 0:   # display frames, double-buffered
+            self.frame8 = [torch.empty(W * H, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.fhits = [torch.empty(W * H * 24, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.frgba = [None if no_rgba else torch.empty(W * H * 4, dtype=torch.float32, device=dev)
+                          for _ in range(2)]
+            self.parts = [[None] + [torch.empty(per, dtype=torch.int32, device=dev) for _ in range(1, world)]
+                          for _ in range(2)]
+            self.send = None
+        else:
+            self.hits = torch.empty(n_local * 24, dtype=torch.uint8, device=dev)
+            self.rgba = None if no_rgba else torch.empty(n_local * 4, dtype=torch.float32, device=dev)
+            self.send = [torch.zeros(per, dtype=torch.int32, device=dev) for _ in range(2)]
         self.ev_r = [torch.cuda.Event() for _ in range(2)]
         self.ev_g = [torch.cuda.Event() for _ in range(2)]
         self.used = [False, False]
         self.k = 0
-        self.payload_bytes = D.band_len(H, rank, world) * W * self.elem
+        # bytes one sending rank moves per frame (rank 1's share; rank 0 sends nothing)
+        self.payload_bytes = D.band_len(H, 1, world) * W * self.elem
 
-    def render(self, k, hits, rgba, stack_mode):
+    def local_hits(self):
+        """This rank's hit records (uint8 tensor, band order) of the last render."""
+        if self.rank != 0:
+            return self.hits
+        from raytracingtest_amd import band_rows
+        rows = self.torch.as_tensor(band_rows(self.H, self.band), device=self.dev)
+        return self.fhits[self.k ^ 1].view(self.H, self.W * 24)[rows].reshape(-1)
+
+    def render(self, k, stack_mode):
         if self.used[k]:
             self.R.wait_event(self.ev_g[k])
-        ptr = self.send[k].data_ptr()
-        self.rm.render_frame(self.W, self.H, hits=hits.data_ptr(), rgba=None if rgba is None else rgba.data_ptr(),
-                             rgba8=ptr if self.payload == "rgba8" else None,
-                             compact=ptr if self.payload == "compact" else None,
-                             stack_mode=stack_mode, band=self.band, stream=self.R.cuda_stream)
+        ptr = lambda t: None if t is None else t.data_ptr()
+        if self.rank == 0:
+            self.rm.render_frame(self.W, self.H, hits=ptr(self.fhits[k]), rgba=ptr(self.frgba[k]),
+                                 rgba8=ptr(self.frame8[k]), layout=1, stack_mode=stack_mode, band=self.band,
+                                 stream=self.R.cuda_stream)
+        else:
+            sp = self.send[k].data_ptr()
+            self.rm.render_frame(self.W, self.H, hits=ptr(self.hits), rgba=ptr(self.rgba),
+                                 rgba8=sp if self.payload == "rgba8" else None,
+                                 compact=sp if self.payload == "compact" else None,
+                                 stack_mode=stack_mode, band=self.band, stream=self.R.cuda_stream)
         self.ev_r[k].record(self.R)
 
     def gather(self, k):
         self.G.wait_event(self.ev_r[k])
         with self.torch.cuda.stream(self.G):
-            self.D.gather_parts(self.send[k], self.parts[k], dst=0)
+            self.D.gather_to_root(None if self.send is None else self.send[k],
+                                  self.parts[k] if self.rank == 0 else None, root=0)
 
     def assemble(self, k):
         if self.rank != 0:
             return
-        ptrs = [p.data_ptr() for p in self.parts[k]]
+        ptrs = [None] + [p.data_ptr() for p in self.parts[k][1:]]
         if self.payload == "rgba8":
-            self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_RGBA8, rgba8=self.frame8.data_ptr(),
-                                   stream=self.G.cuda_stream)
+            self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_RGBA8, rgba8=self.frame8[k].data_ptr(),
+                                   skip_part=0, stream=self.G.cuda_stream)
         else:
-            self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_COMPACT, hits=self.frame_hits.data_ptr(),
-                                   rgba=self.frame_rgba.data_ptr(), rgba8=self.frame8.data_ptr(),
-                                   stream=self.G.cuda_stream)
+            fr = self.frgba[k]
+            self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_COMPACT, hits=self.fhits[k].data_ptr(),
+                                   rgba=None if fr is None else fr.data_ptr(), rgba8=self.frame8[k].data_ptr(),
+                                   skip_part=0, stream=self.G.cuda_stream)
 
-    def step(self, hits, rgba, stack_mode):
+    def step(self, stack_mode):
         k = self.k
         self.k ^= 1
-        self.render(k, hits, rgba, stack_mode)
+        self.render(k, stack_mode)
         self.gather(k)
         self.assemble(k)
         self.ev_g[k].record(self.G)
         self.used[k] = True
 
-    def stage_times(self, hits, rgba, stack_mode, n):
+    def check_frame(self, stack_mode):
+        """The display frame assembled from the ranks' bands vs the same frame
+        rendered whole by the display GPU alone (one launch, no split): RGBA8
+        words, and hit records for the compact payload, must be identical."""
+        torch = self.torch
+        torch.cuda.synchronize(self.dev)
+        k = self.k ^ 1   # the last frame
+        whole8 = torch.empty_like(self.frame8[k])
+        whole_hits = torch.empty_like(self.fhits[k]) if self.payload == "compact" else None
+        self.rm.render_frame(self.W, self.H, rgba8=whole8.data_ptr(),
+                             hits=None if whole_hits is None else whole_hits.data_ptr(),
+                             stack_mode=stack_mode, stream=self.R.cuda_stream)
+        torch.cuda.synchronize(self.dev)
+        bad = int((whole8 != self.frame8[k]).sum().item())
+        out = {"pixels": self.W * self.H, "rgba8_mismatches": bad}
+        if whole_hits is not None:
+            out["hit_record_mismatches"] = int((whole_hits.view(-1, 24) != self.fhits[k].view(-1, 24)).any(1).sum().item())
+        return out
+
+    def stage_times(self, stack_mode, n):
         """Serialized render -> gather -> assemble, events on the gather stream."""
         torch = self.torch
         g_ms, a_ms = [], []
         for _ in range(n):
             torch.cuda.synchronize(self.dev)
-            self.render(0, hits, rgba, stack_mode)
+            self.render(0, stack_mode)
             self.R.synchronize()
             e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
             e0.record(self.G)
@@ -457,6 +508,7 @@ class Gather:
             self.G.synchronize()
             g_ms.append(e0.elapsed_time(e1))
             a_ms.append(e1.elapsed_time(e2))
+        self.k = 1
         return {"gather_ms": float(np.median(g_ms)), "assemble_ms": float(np.median(a_ms)),
                 "payload_bytes": self.payload_bytes}
 

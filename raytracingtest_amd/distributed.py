@@ -6,10 +6,12 @@ Two forms share one band layout and one display-side assemble kernel:
     plugin's multi-device context (svo_create_multi): the Unity host's form; the
     display GPU pulls the other GPUs' band payloads over xGMI (peer access);
   * one process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on
-    ROCm; "gloo" for the CPU tests) -- bench.py's form: every rank renders its
-    bands into a band-contiguous payload, `gather_parts` moves the payloads to
-    the display rank with one RCCL gather, and the display rank's plugin
-    rebuilds the frame (RaytracingMaster.assemble_frame, svo_assemble_frame).
+    ROCm; "gloo" for the CPU tests) -- bench.py's form: the display rank renders
+    its own bands straight into the frame, every other rank into a
+    band-contiguous payload, `gather_to_root` moves those payloads to the display
+    rank in one batch of RCCL sends / receives, and the display rank's plugin
+    rebuilds the other ranks' rows (RaytracingMaster.assemble_frame,
+    svo_assemble_frame with skip_part = the display rank).
 
 Band layout: rows are grouped in `band_rows`-row bands dealt round-robin to the
 ranks (band b -> rank b % world), so sky and terrain rows interleave and every
@@ -75,6 +77,38 @@ def gather_parts(send, parts, dst=0, dist=None, group=None):
                 p.copy_(h)
         return
     dist.gather(send, gather_list=parts, dst=dst, group=group)
+
+
+def gather_to_root(send, parts, root=0, dist=None, group=None):
+    """The N > 1 step's gather without the root's own part: every rank but
+    `root` sends its payload tensor `send` to `root`, which receives rank r's
+    into parts[r] (parts[root] is unused: the display rank renders its own
+    bands straight into the frame).  One batch of point-to-point transfers
+    (RCCL: one ncclGroupStart/End of sends and receives over xGMI), waited for
+    on the caller's current stream."""
+    if dist is None:
+        import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    staged = dist.get_backend(group) == "gloo" and (send is not None and send.is_cuda)
+    ops, copies = [], []
+    if rank == root:
+        for r in range(world):
+            if r == root:
+                continue
+            buf = parts[r]
+            if staged:   # gloo moves host tensors only (one-GPU rehearsal)
+                host = buf.cpu()
+                copies.append((buf, host))
+                buf = host
+            ops.append(dist.P2POp(dist.irecv, buf, r, group))
+    else:
+        ops.append(dist.P2POp(dist.isend, send.cpu() if staged else send, root, group))
+    if not ops:
+        return
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    for dev_buf, host in copies:
+        dev_buf.copy_(host)
 
 
 def gather_bands(local, height, width, world, rank, elem_bytes, rows=DEFAULT_BAND_ROWS, dist=None):

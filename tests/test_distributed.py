@@ -3,7 +3,8 @@
 The per-rank renderer is the CPU oracle (test infrastructure) standing in for
 the HIP kernel; the band layout, the payload formats (RGBA8 words, 12-byte
 compact records = svo_hit prefix) and the one gather to rank 0
-(distributed.gather_parts, the call bench.py's Gather makes on RCCL) run as in
+(distributed.gather_to_root, the batch of sends / receives bench.py's
+Gather makes on RCCL) run as in
 bench.py; the re-interleave is the host restatement of the assemble kernel's
 layout.  The GPU side (band render + svo_assemble_frame, the multi-device
 context) is covered by tests/test_gpu_frame.py."""
@@ -54,16 +55,17 @@ def _worker(rank, world, port, mode, out_dir):
             if rank == 0:
                 frame = D.assemble([p.numpy() for p in parts], H, W, orc.HIT_DTYPE)
                 np.save(os.path.join(out_dir, "frame.npy"), frame)
-        else:   # bench.py's Gather: equal-size int32 payload slots, one gather to rank 0
+        else:   # bench.py's Gather: equal-size int32 payload slots, sent to rank 0, which keeps its own part
             elem = 1 if mode == "rgba8" else 3
             per = D.max_band_len(H, world) * W * elem
-            send = torch.zeros(per, dtype=torch.int32)
             payload = (orc.pack_rgba8(rgba).view(np.int32) if mode == "rgba8" else
                        np.frombuffer(hits.view(np.uint8).reshape(-1, 24)[:, :12].tobytes(), np.int32))
+            send = torch.zeros(per, dtype=torch.int32)
             send[:payload.size] = torch.from_numpy(payload.copy())
-            parts = [torch.empty(per, dtype=torch.int32) for _ in range(world)] if rank == 0 else None
-            D.gather_parts(send, parts, dst=0)
+            parts = [None] + [torch.full((per,), -7, dtype=torch.int32) for _ in range(1, world)] if rank == 0 else None
+            D.gather_to_root(None if rank == 0 else send, parts, root=0)
             if rank == 0:
+                parts[0] = send   # the display rank's own rows never leave it
                 dt = np.uint32 if mode == "rgba8" else np.dtype([("w", "<u4", 3)])
                 trimmed = [p.numpy()[:D.band_len(H, r, world) * W * elem] for r, p in enumerate(parts)]
                 frame = D.assemble(trimmed, H, W, dt)
