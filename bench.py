@@ -294,6 +294,7 @@ def main():
                   "Mrays_per_s": round((n_px + n_hit) / (sh_ms * 1e-3) / 1e6, 2),
                   "note": "primary pass + one shadow ray per primary hit (RaytraceCompute.compute:105-112), "
                           "whole step on the host clock between synchronizes, like value"}
+    host_path = host_path_rates(rm, W, H, args) if world == 1 and args.steps > 0 else None
     poses = None
     if world == 1 and args.extra_poses and args.svo != "menger":
         poses = extra_poses(rm, args, W, H, hits, rgba, sptr, dev)
@@ -369,6 +370,8 @@ def main():
                         "serialized pass (events on the gather stream)"}
         if poses:
             out["extra_poses"] = poses
+        if host_path:
+            out["host_path"] = host_path
         print(json.dumps(out), flush=True)
     rm.close()
     if world > 1:
@@ -561,6 +564,24 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
         "multi_gpu": {"devices": args.device_list, "per_device_kernel_ms": [round(k, 4) for k in kern],
                       "assemble_ms": round(asm_ms, 4)},
     }), flush=True)
+
+
+def host_path_rates(rm, W, H, args, n=5):
+    """PCIe-inclusive frame times of the drop-in's blocking host entry points (never
+    `value`): svo_render (RGBA32F Result + 24-B hit records to the host, 40 B/px)
+    and svo_render_progressive (sample rendered and accumulated on the GPU, the
+    display RGBA8 frame to the host, 4 B/px) -- what the Unity host pays per frame."""
+    out = {}
+    for name, fn in (("svo_render_rgba32f_hits", lambda: rm.Render(W, H, stack_mode=args.stack_mode)),
+                     ("svo_render_progressive_rgba8", lambda: rm.RenderProgressive(W, H, stack_mode=args.stack_mode))):
+        fn()
+        t = time.perf_counter()
+        for _ in range(n):
+            fn()
+        ms = (time.perf_counter() - t) / n * 1e3
+        out[name] = {"ms_per_frame": round(ms, 3), "Mrays_per_s": round(W * H / (ms * 1e-3) / 1e6, 1),
+                     "host_bytes_per_frame": W * H * (40 if name.startswith("svo_render_rgba") else 4)}
+    return out
 
 
 def extra_poses(rm, args, W, H, hits, rgba, sptr, dev):

@@ -195,6 +195,20 @@ int svo_stage_time(svo_ctx *ctx, int stage, double *mean_ms, uint64_t *launches)
 int svo_accumulate(svo_ctx *ctx, void *d_accum, const void *d_sample, size_t n_px, uint32_t sample,
                    void *stream);
 
+/* ~ RaytracingMaster.OnRenderImage end to end (RaytracingMaster.cs:55-74 with
+ * AddShader.shader:44-47): render one sample of the frame at the current camera,
+ * blend it into the context's device-resident accumulation frame with
+ * _Sample = `sample` (svo_accumulate's blend; the frame is zeroed whenever its
+ * size changes), and copy the accumulated frame to the host as display RGBA8
+ * words (4 B/px, R in the low byte = Unity TextureFormat.RGBA32; each colour
+ * channel (uint)(saturate(c) * 255 + 0.5), alpha 255) and/or RGBA32F (16 B/px); either output may be
+ * NULL, not both.  Only the accumulated frame crosses PCIe: 8.3 MB per 1080p
+ * frame as RGBA8 against 83 MB for svo_render's RGBA32F + hit records.  A
+ * multi-device context renders the sample split over its devices and
+ * accumulates on devices[0].  Blocking. */
+int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, uint32_t sample,
+                           uint32_t *rgba8_out, float *rgba_out);
+
 /* Information about the uploaded pool. */
 int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device);
 

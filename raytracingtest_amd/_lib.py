@@ -27,13 +27,13 @@ assert HIT_DTYPE.itemsize == 24
 COMPACT_DTYPE = np.dtype([("parent", "<u4"), ("meta", "<u4"), ("t", "<f4")])   # svo_hit_compact
 assert COMPACT_DTYPE.itemsize == 12
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
            "svo_destroy", "svo_last_error", "svo_abi_version", "svo_set_options", "svo_accumulate",
            "svo_kernel_time", "svo_create_multi", "svo_num_devices", "svo_get_member", "svo_render_frame",
-           "svo_assemble_frame", "svo_stage_time")
+           "svo_assemble_frame", "svo_stage_time", "svo_render_progressive")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
@@ -94,6 +94,7 @@ def lib():
         "svo_render_frame": [vp, i, i, i, vp, ctypes.POINTER(SvoFrame), vp],
         "svo_assemble_frame": [vp, i, i, i, i, ctypes.POINTER(vp), i, i, ctypes.POINTER(SvoFrame), vp],
         "svo_stage_time": [vp, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)],
+        "svo_render_progressive": [vp, i, i, i, ctypes.c_uint32, vp, vp],
         "svo_synchronize": [vp],
         "svo_destroy": [vp],
         "svo_last_error": [],

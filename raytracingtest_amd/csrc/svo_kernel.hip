@@ -971,6 +971,29 @@ hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32
     return hipGetLastError();
 }
 
+// Display RGBA8 of an RGBA32F frame (the accumulated Result): saturate, * 255,
+// round half up per colour channel, opaque alpha.  == orc_pack_rgba8.
+__global__ __launch_bounds__(256) void pack_rgba8_kernel(const float4 *__restrict__ src, uint32_t *__restrict__ dst,
+                                                         size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float4 c = src[i];
+        auto q = [](float v) {
+            v = fminf(fmaxf(v, 0.0f), 1.0f);
+            v = v * 255.0f;
+            return (uint32_t)(v + 0.5f);
+        };
+        dst[i] = q(c.x) | (q(c.y) << 8) | (q(c.z) << 16) | (255u << 24);
+    }
+}
+
+hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int num_cus, hipStream_t stream) {
+    if (n_px == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<size_t>((n_px + 255) / 256, (size_t)num_cus * 16);
+    hipLaunchKernelGGL(pack_rgba8_kernel, dim3(blocks), dim3(256), 0, stream, src, dst, n_px);
+    return hipGetLastError();
+}
+
 hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
     if (a.width <= 0 || a.height <= 0) return hipSuccess;
     const dim3 grid((unsigned)((a.width + 255) / 256), (unsigned)a.height);

@@ -87,6 +87,11 @@ struct svo_ctx {
     void *d_out_hits = nullptr;
     void *d_out_rgba = nullptr;
     size_t out_cap_px = 0;
+    // svo_render_progressive: the accumulated frame (RGBA32F, zeroed on a size
+    // change) and its RGBA8 display words
+    float4 *d_accum = nullptr;
+    uint32_t *d_accum8 = nullptr;
+    int accum_w = 0, accum_h = 0;
     int num_cus = 256;
     int xcd_remap = 2;               // env SVO_XCD_REMAP: 2 interleaved column strips (default), 0 raster
     uint32_t options = 0;            // svo_set_options
@@ -254,6 +259,23 @@ int ensure_out(svo_ctx *ctx, size_t px) {
     HIP_TRY(hipMalloc(&ctx->d_out_hits, px * sizeof(svo_hit)));
     HIP_TRY(hipMalloc(&ctx->d_out_rgba, px * 4 * sizeof(float)));
     ctx->out_cap_px = px;
+    return SVO_OK;
+}
+
+int ensure_accum(svo_ctx *ctx, int width, int height) {
+    if (ctx->d_accum && ctx->accum_w == width && ctx->accum_h == height) return SVO_OK;
+    HIP_TRY(hipDeviceSynchronize());   // an earlier asynchronous launch may still use the old frame
+    if (ctx->d_accum) hipFree(ctx->d_accum);
+    if (ctx->d_accum8) hipFree(ctx->d_accum8);
+    ctx->d_accum = nullptr;
+    ctx->d_accum8 = nullptr;
+    ctx->accum_w = ctx->accum_h = 0;
+    const size_t px = (size_t)width * (size_t)height;
+    HIP_TRY(hipMalloc(&ctx->d_accum, px * sizeof(float4)));
+    HIP_TRY(hipMalloc(&ctx->d_accum8, px * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(ctx->d_accum, 0, px * sizeof(float4)));   // a fresh render target
+    ctx->accum_w = width;
+    ctx->accum_h = height;
     return SVO_OK;
 }
 
@@ -550,6 +572,8 @@ int destroy_single(svo_ctx *ctx) {
     if (ctx->d_stage) hipFree(ctx->d_stage);
     if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
+    if (ctx->d_accum) hipFree(ctx->d_accum);
+    if (ctx->d_accum8) hipFree(ctx->d_accum8);
     if (ctx->d_shadow_cost) hipFree(ctx->d_shadow_cost);
     if (ctx->d_shadow_order) hipFree(ctx->d_shadow_order);
     for (auto &v : ctx->timing_events)
@@ -568,7 +592,7 @@ int destroy_single(svo_ctx *ctx) {
 
 extern "C" {
 
-int svo_abi_version(void) { return 2; }
+int svo_abi_version(void) { return 3; }
 
 const char *svo_last_error(void) { return g_last_error.c_str(); }
 
@@ -817,6 +841,41 @@ int svo_render(svo_ctx *ctx, int width, int height, int stack_mode, float *rgba_
         HIP_TRY(hipMemcpyAsync(hits_out, c->d_out_hits, px * sizeof(svo_hit), hipMemcpyDeviceToHost, c->stream));
     if (rgba_out)
         HIP_TRY(hipMemcpyAsync(rgba_out, c->d_out_rgba, px * 4 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SVO_OK;
+}
+
+int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, uint32_t sample,
+                           uint32_t *rgba8_out, float *rgba_out) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (!rgba8_out && !rgba_out) return fail(SVO_ERR_ARG, "no output requested");
+    if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
+    const size_t px = (size_t)width * (size_t)height;
+    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = ensure_out(c, px);
+    if (rc) return rc;
+    rc = ensure_accum(c, width, height);
+    if (rc) return rc;
+    svo_frame f{};
+    f.rgba = reinterpret_cast<float *>(c->d_out_rgba);   // this sample's Result
+    f.layout = SVO_LAYOUT_FRAME;
+    rc = is_multi(ctx) ? multi_render(ctx, width, height, stack_mode, &f, c->stream)
+                       : launch(c, width, height, stack_mode, nullptr, outputs_of(&f), c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    rc = order_streams(c, c->stream);
+    if (rc) return rc;
+    hipError_t e = svo::launch_accumulate(c->d_accum, reinterpret_cast<const float4 *>(c->d_out_rgba), px, sample,
+                                          c->num_cus, c->stream);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("accumulate launch: ") + hipGetErrorString(e));
+    if (rgba8_out) {
+        e = svo::launch_pack_rgba8(c->d_accum, c->d_accum8, px, c->num_cus, c->stream);
+        if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("pack launch: ") + hipGetErrorString(e));
+        HIP_TRY(hipMemcpyAsync(rgba8_out, c->d_accum8, px * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    }
+    if (rgba_out)
+        HIP_TRY(hipMemcpyAsync(rgba_out, c->d_accum, px * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return SVO_OK;
 }

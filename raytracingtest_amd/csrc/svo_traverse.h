@@ -107,6 +107,9 @@ hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32
 
 hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream);
 
+// Display RGBA8 words of an RGBA32F frame (svo_render_progressive).
+hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int num_cus, hipStream_t stream);
+
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, hipEvent_t primary_start = nullptr,
                          hipEvent_t primary_end = nullptr);
 

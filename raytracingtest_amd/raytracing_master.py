@@ -9,6 +9,8 @@ Same names and argument meaning as the reference:
   Render(width, height)          RaytracingMaster.cs:60-74   (Dispatch + result)
   accumulate_device(...)         RaytracingMaster.cs:70-73 + AddShader.shader (Blit with _Sample,
                                  then _currentSample++; reset to 0 when the camera moves, :44-47)
+  RenderProgressive(width, height)  OnRenderImage end to end (:55-74): one sample rendered,
+                                 accumulated on the device, display RGBA8 to the host
 Beyond the reference (one GPU, one Dispatch):
   RaytracingMaster(devices=[0, 1, ...])  one context over several GPUs of the node
                                  (svo_create_multi): SVO replica per GPU, the frame
@@ -156,6 +158,21 @@ class RaytracingMaster:
                                     None if rgba is None else rgba.ctypes.data,
                                     None if hits is None else hits.ctypes.data), "svo_render")
         return rgba, hits
+
+    def RenderProgressive(self, width, height, stack_mode=STACK_HLSL, want_rgba8=True, want_rgba=False):
+        """OnRenderImage end to end (RaytracingMaster.cs:55-74): render a sample at
+        the current camera, blend it into the plugin's device-resident accumulation
+        frame with _Sample = currentSample (AddShader), then currentSample += 1.
+        Returns (rgba8[H, W] uint32 display words or None, rgba[H, W, 4] float32
+        accumulated frame or None); only those cross PCIe."""
+        rgba8 = np.zeros((height, width), np.uint32) if want_rgba8 else None
+        rgba = np.zeros((height, width, 4), np.float32) if want_rgba else None
+        check(_lib.lib().svo_render_progressive(self._ctx, width, height, stack_mode, self.currentSample,
+                                                None if rgba8 is None else rgba8.ctypes.data,
+                                                None if rgba is None else rgba.ctypes.data),
+              "svo_render_progressive")
+        self.currentSample += 1
+        return rgba8, rgba
 
     def render_device(self, width, height, rgba_ptr=None, hits_ptr=None, stack_mode=STACK_HLSL,
                       band=None, stream=None):

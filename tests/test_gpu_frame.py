@@ -14,7 +14,7 @@
 import numpy as np
 import pytest
 
-from raytracingtest_amd import HIT_DTYPE, RaytracingMaster, band_rows
+from raytracingtest_amd import HIT_DTYPE, RaytracingMaster, SvoError, band_rows
 from raytracingtest_amd import _lib
 from raytracingtest_amd.builder import build_menger
 from raytracingtest_amd.camera import Camera, look_rotation, main_camera, main_light, overview_camera
@@ -433,3 +433,43 @@ def test_clipmap_linked_sub_svo_trunk_first(torch, oracle_mod):
         assert linked > 500 and np.all(ref["parent"][(ref["flags"] & 1) != 0] >= base)
     finally:
         m.close()
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_render_progressive_matches_oracle(torch, oracle_mod, text_svo, devices):
+    """svo_render_progressive = OnRenderImage end to end (RaytracingMaster.cs:55-74):
+    each call renders a jittered sample, blends it into the device-resident
+    accumulation frame with _Sample = currentSample (AddShader.shader:44-47) and
+    returns the accumulated frame; equal to the oracle's per-sample render +
+    orc_accumulate + orc_pack_rgba8, bit for bit.  A camera move restarts the
+    accumulation; a size change starts from a zeroed frame."""
+    from raytracingtest_amd.camera import jitter_offsets
+    W, H = 96, 70
+    cam = overview_camera()
+    rm = RaytracingMaster(capacity_nodes=1 << 16, devices=devices)
+    try:
+        rm.SetSVOBuffer(text_svo)
+        c2w, inv_proj = cam.uniforms(W, H)
+        osvo = oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments)
+        acc = np.zeros((W * H, 4), np.float32)
+        offs = jitter_offsets(5)
+        for n, off in enumerate(offs):
+            rm.UpdateShaderParameters(cam, W, H, pixel_offset=tuple(float(v) for v in off))
+            assert rm.currentSample == n
+            rgba8, rgba = rm.RenderProgressive(W, H, want_rgba=True)
+            _, smp, _ = oracle_mod.render(osvo, oracle_mod.make_camera(c2w, inv_proj, tuple(float(v) for v in off),
+                                                                      main_light()), W, H)
+            oracle_mod.accumulate(acc, np.ascontiguousarray(smp, np.float32), n)
+            assert rgba.reshape(-1, 4).tobytes() == acc.tobytes(), f"sample {n}"
+            assert np.array_equal(rgba8.reshape(-1), oracle_mod.pack_rgba8(acc))
+        # camera moved: _currentSample = 0, the new sample replaces the frame
+        rm.UpdateShaderParameters(main_camera(), W, H)
+        assert rm.currentSample == 0
+        _, rgba = rm.RenderProgressive(W, H, want_rgba8=False, want_rgba=True)
+        mc2w, minv = main_camera().uniforms(W, H)
+        _, smp, _ = oracle_mod.render(osvo, oracle_mod.make_camera(mc2w, minv, (0.5, 0.5), main_light()), W, H)
+        assert rgba.reshape(-1, 4).tobytes() == np.ascontiguousarray(smp, np.float32).tobytes()
+        with pytest.raises(SvoError):
+            rm.RenderProgressive(W, H, want_rgba8=False, want_rgba=False)
+    finally:
+        rm.close()

@@ -20,6 +20,9 @@ public static class SvoNative {
                                                              float pxOffX, float pxOffY, float[] light);
     [DllImport(Lib)] public static extern int svo_render(IntPtr ctx, int width, int height, int stackMode,
                                                          float[] rgbaOut, [Out] SvoHit[] hitsOut);
+    [DllImport(Lib)] public static extern int svo_render_progressive(IntPtr ctx, int width, int height, int stackMode,
+                                                                     uint sample, [Out] uint[] rgba8Out,
+                                                                     [Out] float[] rgbaOut);
     [DllImport(Lib)] public static extern int svo_destroy(IntPtr ctx);
     [DllImport(Lib)] public static extern IntPtr svo_last_error();
 
@@ -43,11 +46,20 @@ public class RaytracingMasterNative : MonoBehaviour {
     IntPtr _ctx;
     Camera _camera;
     Texture2D _frame;
-    float[] _rgba;
+    uint[] _rgba8;
+    uint _currentSample = 0;   // RaytracingMaster.cs:12
 
     void Awake() {
         _camera = GetComponent<Camera>();
         InitializeSVOBuffer();
+    }
+
+    // RaytracingMaster.cs:44-53: a moved camera restarts the accumulation
+    void Update() {
+        if (transform.hasChanged) {
+            _currentSample = 0;
+            transform.hasChanged = false;
+        }
     }
 
     // RaytracingMaster.cs:111-116
@@ -63,7 +75,9 @@ public class RaytracingMasterNative : MonoBehaviour {
                                                  (UIntPtr)offset), "svo_set_buffer");
     }
 
-    // RaytracingMaster.cs:32-41 + 60-74
+    // RaytracingMaster.cs:32-41 + 55-74: the sample is rendered, blended into the plugin's
+    // device-resident accumulation frame with _Sample = _currentSample (AddShader.shader:44-47),
+    // and only the accumulated display frame (RGBA8, 4 B/px) crosses PCIe.
     void OnRenderImage(RenderTexture source, RenderTexture destination) {
         Vector3 l = DirectionalLight.transform.forward;
         SvoNative.Check(SvoNative.svo_set_camera(_ctx, SvoNative.ToArray(_camera.cameraToWorldMatrix),
@@ -72,13 +86,15 @@ public class RaytracingMasterNative : MonoBehaviour {
                                                  new[] { l.x, l.y, l.z, DirectionalLight.intensity }), "svo_set_camera");
         int w = Screen.width, h = Screen.height;
         if (_frame == null || _frame.width != w || _frame.height != h) {
-            _frame = new Texture2D(w, h, TextureFormat.RGBAFloat, false, true);
-            _rgba = new float[w * h * 4];
+            _frame = new Texture2D(w, h, TextureFormat.RGBA32, false, true);
+            _rgba8 = new uint[w * h];
         }
-        SvoNative.Check(SvoNative.svo_render(_ctx, w, h, 0, _rgba, null), "svo_render");
-        _frame.SetPixelData(_rgba, 0);
+        SvoNative.Check(SvoNative.svo_render_progressive(_ctx, w, h, 0, _currentSample, _rgba8, null),
+                        "svo_render_progressive");
+        _frame.SetPixelData(_rgba8, 0);
         _frame.Apply(false);
-        Graphics.Blit(_frame, destination);
+        Graphics.Blit(_frame, destination);   // already accumulated: a plain copy, no AddMaterial
+        _currentSample++;
     }
 
     void OnDestroy() {
