@@ -607,6 +607,8 @@ int surface_leaves_gpu(int device, int type, int max_level, std::vector<uint64_t
         const size_t ncell = np2 * np2 * (size_t)zcells;
         const unsigned grid = (unsigned)std::min<size_t>((ncell + 255) / 256, 65536);
         hipLaunchKernelGGL(sign_kernel, dim3(grid), dim3(256), 0, 0, ds, type, n, size, z0, zcells, cells);
+        e = hipGetLastError();
+        if (e != hipSuccess) { cleanup(); return fail(SVOB_ERR_HIP, std::string("builder sign launch: ") + hipGetErrorString(e)); }
         for (;;) {
             e = hipMemset(dcount, 0, sizeof(unsigned long long));
             if (e != hipSuccess) break;
@@ -614,6 +616,8 @@ int surface_leaves_gpu(int device, int type, int max_level, std::vector<uint64_t
             const unsigned g2 = (unsigned)std::min<size_t>((nl + 255) / 256, 65536);
             hipLaunchKernelGGL(classify_kernel, dim3(g2), dim3(256), 0, 0, cells, n, z0, zc, dcodes, dcount,
                                (unsigned long long)cap);
+            e = hipGetLastError();
+            if (e != hipSuccess) break;
             unsigned long long cnt = 0;
             e = hipMemcpy(&cnt, dcount, sizeof(cnt), hipMemcpyDeviceToHost);
             if (e != hipSuccess) break;

@@ -994,8 +994,30 @@ hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int 
     return hipGetLastError();
 }
 
+// RGBA8 parts: pure data movement (4 B read + 4 B written per pixel), so 16 bytes
+// per lane and the row's band arithmetic once per workgroup (row = blockIdx.y).
+// Needs width % 4 == 0 (16-byte aligned rows in every part and in the frame).
+__global__ __launch_bounds__(256) void assemble_rgba8_kernel(AssembleParams a) {
+    const int y = (int)blockIdx.y;
+    const int band = y / a.band_rows;
+    const int m = band % a.n_parts;
+    if (m == a.skip_part) return;
+    const int lr = (band / a.n_parts) * a.band_rows + (y - band * a.band_rows);
+    const int q = (int)(blockIdx.x * 256 + threadIdx.x);   // 4-pixel group of the row
+    if (4 * q >= a.width) return;
+    const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(a.parts[m]) +
+                                                       (size_t)lr * (size_t)a.width);
+    uint4 *dst = reinterpret_cast<uint4 *>(a.out.rgba8 + (size_t)y * (size_t)a.width);
+    dst[q] = src[q];
+}
+
 hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
     if (a.width <= 0 || a.height <= 0) return hipSuccess;
+    if (a.part_format == PART_RGBA8 && a.width % 4 == 0) {
+        const dim3 grid((unsigned)((a.width / 4 + 255) / 256), (unsigned)a.height);
+        hipLaunchKernelGGL(assemble_rgba8_kernel, grid, dim3(256), 0, stream, a);
+        return hipGetLastError();
+    }
     const dim3 grid((unsigned)((a.width + 255) / 256), (unsigned)a.height);
     hipLaunchKernelGGL(assemble_kernel, grid, dim3(256), 0, stream, a);
     return hipGetLastError();

@@ -234,9 +234,16 @@ def test_assemble_from_rank_parts(torch, oracle_mod, world):
                          rgba=b["rgba"].data_ptr(), compact=b["compact"].data_ptr())
         b2 = _bufs(torch, w * h)
         m.assemble_frame(w, h, [c.data_ptr() for c in rgb8], _lib.PART_RGBA8, rgba8=b2["rgba8"].data_ptr())
+        # bench.py's display rank: its own bands rendered straight into the frame, the
+        # other parts assembled around them (skip_part 0)
+        b3 = _bufs(torch, w * h)
+        m.render_frame(w, h, rgba8=b3["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME, band=(8, 0, world))
+        m.assemble_frame(w, h, [None] + [c.data_ptr() for c in rgb8[1:]], _lib.PART_RGBA8,
+                         rgba8=b3["rgba8"].data_ptr(), skip_part=0)
         m.synchronize()
         _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba", "compact"))
         _check(b2, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+        _check(b3, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
         with pytest.raises(_lib.SvoError):   # RGBA8 parts cannot rebuild hit records
             m.assemble_frame(w, h, [c.data_ptr() for c in rgb8], _lib.PART_RGBA8, hits=b["hits"].data_ptr())
     finally:
