@@ -83,6 +83,9 @@ def parse():
     p.add_argument("--devices", default=None,
                    help="one-process multi-device mode: comma-separated HIP device indices of the context's members "
                         "(default 0..N-1; an index may repeat to rehearse the split on one GPU)")
+    p.add_argument("--display-share", type=float, default=None,
+                   help="N > 1: the display rank's share of a normal rank's bands (default: calibrated from its "
+                        "assemble time; 1 = round-robin)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--no-rgba", action="store_true")
     p.add_argument("--camera", choices=["flyover", "overview", "main", "terrain"], default=None)
@@ -189,19 +192,21 @@ def main():
     rm.UpdateShaderParameters(cam, W, H)
     if args.shadows:
         rm.SetShadowRays(True)
-    band = D.rank_band(rank, world) if world > 1 else None
-    rows = D.band_len(H, rank, world) if world > 1 else H
-    n_px = W * rows
-
     # a dedicated (non-null) stream: the kernel and the timing events share it
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     gather = None
+    deal_info = None
     if world > 1:
         gather = Gather(rm, W, H, rank, world, dev, args.payload, stream, args.no_rgba)
+        gather, deal_info = weigh_display_rank(gather, args, rm, dist, dev)
         hits = rgba = None
+        band = gather.band
+        n_px = gather.n_local
     else:
+        band = None
+        n_px = W * H
         hits = torch.empty(n_px * 24, dtype=torch.uint8, device=dev)
         rgba = None if args.no_rgba else torch.empty(n_px * 4, dtype=torch.float32, device=dev)
 
@@ -212,11 +217,16 @@ def main():
         else:
             gather.step(args.stack_mode)
 
+    def drain():
+        if gather is not None:
+            gather.drain()
+
     # instrumented pass (outside the timed region): per-ray fetch counts
     fetch = torch.zeros(n_px, dtype=torch.int32, device=dev)
     rm.count_fetches_device(W, H, fetch.data_ptr(), stack_mode=args.stack_mode, band=band, stream=sptr)
     for _ in range(max(1, args.warmup)):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     host_hits = (hits if gather is None else gather.local_hits()).cpu().numpy().view(_lib.HIT_DTYPE)
     n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
@@ -242,6 +252,7 @@ def main():
         step()
         if step_events:
             ev[i][1].record(stream)
+    drain()   # the last frame's assemble (each step assembles the previous frame)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -256,6 +267,7 @@ def main():
     rm.kernel_time()   # forget anything recorded before
     for i in range(args.steps):
         step()
+    drain()
     kern_ms, n_timed = rm.kernel_time()
     rm.set_kernel_timing(False)
     torch.cuda.synchronize(dev)
@@ -314,7 +326,9 @@ def main():
         digest = source_digest()
         pmc = pmc_traffic(workload, digest) if band is None else None
         traffic = pmc["hbm_bytes_per_launch"] if pmc else None
-        par = "single" if world == 1 else f"bands{world}x8rows+rccl_gather({args.payload})"
+        weighted = bool(deal_info and deal_info["cycle_bands"])
+        par = ("single" if world == 1 else
+               f"bands{world}x8rows{'-weighted' if weighted else ''}+rccl_gather({args.payload})")
         out = {
             "metric": METRIC,
             "value": round(mrays, 2),
@@ -364,6 +378,7 @@ def main():
                 "render_only_Mrays": round(rays_per_step / (kern_ms_max * 1e-3) / 1e6, 2),
                 "gather_ms_rank0": round(stages["gather_ms"], 4), "assemble_ms_rank0": round(stages["assemble_ms"], 4),
                 "payload_bytes_per_sending_rank": stages["payload_bytes"],
+                "display_rank_deal": deal_info,
                 "assembled_frame_check": frame_check,
                 "note": "value overlaps the gather of frame k with the render of frame k+1; render_only_Mrays is "
                         "the frame's rays over the slowest rank's render kernel alone; gather/assemble from a "
@@ -381,27 +396,28 @@ def main():
 class Gather:
     """One rank's render + gather + assemble pipeline (bench's N > 1 step).
 
-    Render on the caller's stream R: the display rank (0) straight into display
-    frame k (frame layout: its own bands' rows of the RGBA8 frame, and of the
-    full hit-record / Result frames for the compact payload); every other rank
-    into its band buffers and payload k.  Gather stream G waits for the render,
-    moves the payloads to rank 0 in one batch of RCCL sends / receives, and rank
-    0 rebuilds the other ranks' rows of frame k (svo_assemble_frame, skipping its
-    own part); the next render into slot k waits for that (two frames in flight)."""
+    Every rank renders frame k on its stream R: the display rank (0) straight
+    into display frame k (frame layout: its own rows of the RGBA8 frame, and of
+    the full hit-record / Result frames for the compact payload), every other
+    rank into its band buffers and payload k.  Gather stream G moves the
+    payloads to rank 0 in one batch of RCCL sends / receives while R renders
+    the next frame; rank 0 then assembles frame k's other rows on R right after
+    rendering frame k+1 (svo_assemble_frame, skipping its own part).  Render and
+    assemble on one stream cost rank 0 less than the two kernels side by side
+    (tools/rank0_cost.py).  Two payload / frame slots."""
 
-    def __init__(self, rm, W, H, rank, world, dev, payload, stream, no_rgba):
+    def __init__(self, rm, W, H, rank, world, dev, payload, stream, no_rgba, owner=None):
         import torch
         from raytracingtest_amd import _lib
         from raytracingtest_amd import distributed as D
         self.torch, self._lib, self.D = torch, _lib, D
         self.rm, self.W, self.H, self.rank, self.world, self.dev = rm, W, H, rank, world, dev
-        self.payload = payload
-        self.band = D.rank_band(rank, world)
+        self.payload, self.owner, self.no_rgba, self.R = payload, owner, no_rgba, stream
+        self.band = D.rank_band(rank, world, owner=owner)
         self.elem = 4 if payload == "rgba8" else 12
-        per = D.max_band_len(H, world) * W * self.elem // 4
-        self.R = stream
+        per = D.max_band_len(H, world, owner=owner) * W * self.elem // 4
         self.G = torch.cuda.Stream(dev)
-        n_local = D.band_len(H, rank, world) * W
+        self.n_local = D.band_len(H, rank, world, owner=owner) * W
         if rank == 0:   # display frames, double-buffered
             self.frame8 = [torch.empty(W * H, dtype=torch.int32, device=dev) for _ in range(2)]
             self.fhits = [torch.empty(W * H * 24, dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -411,33 +427,36 @@ class Gather:
                           for _ in range(2)]
             self.send = None
         else:
-            self.hits = torch.empty(n_local * 24, dtype=torch.uint8, device=dev)
-            self.rgba = None if no_rgba else torch.empty(n_local * 4, dtype=torch.float32, device=dev)
+            self.hits = torch.empty(max(self.n_local, 1) * 24, dtype=torch.uint8, device=dev)
+            self.rgba = None if no_rgba else torch.empty(max(self.n_local, 1) * 4, dtype=torch.float32, device=dev)
             self.send = [torch.zeros(per, dtype=torch.int32, device=dev) for _ in range(2)]
-        self.ev_r = [torch.cuda.Event() for _ in range(2)]
-        self.ev_g = [torch.cuda.Event() for _ in range(2)]
+        self.ev_r = [torch.cuda.Event() for _ in range(2)]   # frame rendered (payload ready)
+        self.ev_g = [torch.cuda.Event() for _ in range(2)]   # payloads moved
+        self.ev_a = [torch.cuda.Event() for _ in range(2)]   # rank 0: parts of the slot read by its assemble
         self.used = [False, False]
         self.k = 0
+        self.pending = None      # rank 0: slot rendered and gathered, not yet assembled
+        self.last = None         # slot of the last complete frame
         # bytes one sending rank moves per frame (rank 1's share; rank 0 sends nothing)
-        self.payload_bytes = D.band_len(H, 1, world) * W * self.elem
+        self.payload_bytes = D.band_len(H, 1, world, owner=owner) * W * self.elem
 
     def local_hits(self):
         """This rank's hit records (uint8 tensor, band order) of the last render."""
         if self.rank != 0:
-            return self.hits
+            return self.hits[:self.n_local * 24]
         from raytracingtest_amd import band_rows
         rows = self.torch.as_tensor(band_rows(self.H, self.band), device=self.dev)
-        return self.fhits[self.k ^ 1].view(self.H, self.W * 24)[rows].reshape(-1)
+        return self.fhits[self.last].view(self.H, self.W * 24)[rows].reshape(-1)
 
     def render(self, k, stack_mode):
-        if self.used[k]:
-            self.R.wait_event(self.ev_g[k])
         ptr = lambda t: None if t is None else t.data_ptr()
         if self.rank == 0:
             self.rm.render_frame(self.W, self.H, hits=ptr(self.fhits[k]), rgba=ptr(self.frgba[k]),
                                  rgba8=ptr(self.frame8[k]), layout=1, stack_mode=stack_mode, band=self.band,
                                  stream=self.R.cuda_stream)
         else:
+            if self.used[k]:
+                self.R.wait_event(self.ev_g[k])   # payload k sent
             sp = self.send[k].data_ptr()
             self.rm.render_frame(self.W, self.H, hits=ptr(self.hits), rgba=ptr(self.rgba),
                                  rgba8=sp if self.payload == "rgba8" else None,
@@ -446,40 +465,82 @@ class Gather:
         self.ev_r[k].record(self.R)
 
     def gather(self, k):
-        self.G.wait_event(self.ev_r[k])
+        if self.rank == 0:
+            if self.used[k]:
+                self.G.wait_event(self.ev_a[k])   # parts k read by the previous assemble
+        else:
+            self.G.wait_event(self.ev_r[k])
         with self.torch.cuda.stream(self.G):
             self.D.gather_to_root(None if self.send is None else self.send[k],
                                   self.parts[k] if self.rank == 0 else None, root=0)
+        self.ev_g[k].record(self.G)
+        self.used[k] = True
 
-    def assemble(self, k):
-        if self.rank != 0:
-            return
+    def assemble(self, k, stream):
         ptrs = [None] + [p.data_ptr() for p in self.parts[k][1:]]
+        s = stream.cuda_stream
         if self.payload == "rgba8":
             self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_RGBA8, rgba8=self.frame8[k].data_ptr(),
-                                   skip_part=0, stream=self.G.cuda_stream)
+                                   skip_part=0, stream=s, owner=self.owner)
         else:
             fr = self.frgba[k]
             self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_COMPACT, hits=self.fhits[k].data_ptr(),
                                    rgba=None if fr is None else fr.data_ptr(), rgba8=self.frame8[k].data_ptr(),
-                                   skip_part=0, stream=self.G.cuda_stream)
+                                   skip_part=0, stream=s, owner=self.owner)
+
+    def drain(self):
+        """Rank 0: assemble the frame still pending (end of a run of steps)."""
+        if self.rank == 0 and self.pending is not None:
+            k = self.pending
+            self.R.wait_event(self.ev_g[k])
+            self.assemble(k, self.R)
+            self.ev_a[k].record(self.R)
+            self.last = k
+            self.pending = None
 
     def step(self, stack_mode):
         k = self.k
         self.k ^= 1
         self.render(k, stack_mode)
         self.gather(k)
-        self.assemble(k)
-        self.ev_g[k].record(self.G)
-        self.used[k] = True
+        if self.rank == 0:
+            self.drain()          # the previous frame's rows from the other ranks, behind this render
+            self.pending = k
+        else:
+            self.last = k
+
+    def stage_times(self, stack_mode, n):
+        """Serialized render -> gather -> assemble, events on the gather stream."""
+        torch = self.torch
+        self.drain()
+        g_ms, a_ms = [], []
+        for _ in range(n):
+            torch.cuda.synchronize(self.dev)
+            self.render(0, stack_mode)
+            self.R.synchronize()
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(self.G)
+            self.gather(0)
+            e1.record(self.G)
+            if self.rank == 0:
+                self.assemble(0, self.G)
+                self.ev_a[0].record(self.G)
+            e2.record(self.G)
+            self.G.synchronize()
+            g_ms.append(e0.elapsed_time(e1))
+            a_ms.append(e1.elapsed_time(e2))
+        self.last, self.k = 0, 1
+        return {"gather_ms": float(np.median(g_ms)), "assemble_ms": float(np.median(a_ms)),
+                "payload_bytes": self.payload_bytes}
 
     def check_frame(self, stack_mode):
         """The display frame assembled from the ranks' bands vs the same frame
         rendered whole by the display GPU alone (one launch, no split): RGBA8
         words, and hit records for the compact payload, must be identical."""
         torch = self.torch
+        self.drain()
         torch.cuda.synchronize(self.dev)
-        k = self.k ^ 1   # the last frame
+        k = self.last
         whole8 = torch.empty_like(self.frame8[k])
         whole_hits = torch.empty_like(self.fhits[k]) if self.payload == "compact" else None
         self.rm.render_frame(self.W, self.H, rgba8=whole8.data_ptr(),
@@ -492,28 +553,48 @@ class Gather:
             out["hit_record_mismatches"] = int((whole_hits.view(-1, 24) != self.fhits[k].view(-1, 24)).any(1).sum().item())
         return out
 
-    def stage_times(self, stack_mode, n):
-        """Serialized render -> gather -> assemble, events on the gather stream."""
-        torch = self.torch
-        g_ms, a_ms = [], []
-        for _ in range(n):
-            torch.cuda.synchronize(self.dev)
-            self.render(0, stack_mode)
-            self.R.synchronize()
-            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            e0.record(self.G)
-            self.gather(0)
-            e1.record(self.G)
-            self.assemble(0)
-            e2.record(self.G)
-            self.ev_g[0].record(self.G)
-            self.used[0] = True
-            self.G.synchronize()
-            g_ms.append(e0.elapsed_time(e1))
-            a_ms.append(e1.elapsed_time(e2))
-        self.k = 1
-        return {"gather_ms": float(np.median(g_ms)), "assemble_ms": float(np.median(a_ms)),
-                "payload_bytes": self.payload_bytes}
+
+def weigh_display_rank(gather, args, rm, dist, dev):
+    """Balance the display rank: it also assembles the frame, so it gets a smaller
+    share of the bands (distributed.weighted_owner).  Its share = 1 - (assemble
+    time + 3 us frame-layout cost) / render-kernel time, measured here on the
+    round-robin deal (max over ranks) unless --display-share fixes it; every rank
+    uses rank 0's figure.  Returns the gather to time and a record of the deal."""
+    import torch
+    share = args.display_share
+    measured = None
+    if share is None:
+        for _ in range(3):
+            gather.step(args.stack_mode)
+        gather.drain()
+        st = gather.stage_times(args.stack_mode, 5)
+        rm.set_kernel_timing(True)
+        rm.kernel_time()
+        for _ in range(5):
+            gather.step(args.stack_mode)
+        gather.drain()
+        kern = rm.kernel_time()[0]
+        rm.set_kernel_timing(False)
+        t = torch.tensor([kern, st["assemble_ms"] if gather.rank == 0 else 0.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        kern, asm = float(t[0]), float(t[1])
+        share = max(0.0, 1.0 - (asm + 0.003) / kern)
+        measured = {"render_kernel_ms_max": round(kern, 4), "display_assemble_ms": round(asm, 4)}
+    t = torch.tensor([share], dtype=torch.float64, device=dev)
+    dist.broadcast(t, 0)
+    share = max(float(t[0]), 1.0 / 8.0)   # at least one band per round: every rank renders
+    from raytracingtest_amd import distributed as D
+    owner = D.weighted_owner(gather.world, share)
+    info = {"display_share": round(owner.count(0) / 8, 3), "calibration": measured,
+            "cycle_bands": len(owner), "rows_rank0": gather.D.band_len(gather.H, 0, gather.world, owner=owner),
+            "rows_rank1": gather.D.band_len(gather.H, 1, gather.world, owner=owner)}
+    torch.cuda.synchronize(dev)
+    if owner.count(0) == 8:   # round-robin
+        info["cycle_bands"] = 0
+        return Gather(gather.rm, gather.W, gather.H, gather.rank, gather.world, dev, gather.payload, gather.R,
+                      gather.no_rgba), info
+    return Gather(gather.rm, gather.W, gather.H, gather.rank, gather.world, dev, gather.payload, gather.R,
+                  gather.no_rgba, owner=owner), info
 
 
 def bench_multidevice(args, svo, cam, W, H, scaling, build_s):

@@ -59,12 +59,17 @@ typedef struct svo_hit_compact {
 } svo_hit_compact;
 
 /* Row split of one frame across ranks/GPUs: rows are grouped in bands of
- * `band_rows`; band b belongs to rank b % band_count.  A rank's output holds
- * only its own rows, in increasing y.  {1, 0, 1} (or NULL) = whole frame. */
+ * `band_rows`; round-robin (cycle 0) band b belongs to rank b % band_count;
+ * a weighted deal (0 < cycle <= 256) gives band b to rank owner[b % cycle]
+ * (owner: `cycle` entries, each < band_count), e.g. fewer bands to the display
+ * rank, which also assembles the frame.  A rank's output holds only its own rows,
+ * in increasing y.  {1, 0, 1} (or NULL) = whole frame. */
 typedef struct svo_band {
     int band_rows;
     int band_rank;
     int band_count;
+    int cycle;                /* 0: round-robin */
+    const uint8_t *owner;     /* cycle > 0: owner[b % cycle] = rank of band b */
 } svo_band;
 
 /* Every per-pixel output of one render (device pointers on the context's
@@ -146,8 +151,9 @@ int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const 
                      const svo_frame *frame, void *stream);
 
 /* Rebuild a split frame on this context's device from its band parts: part m
- * holds the rows of bands b with b % n_parts == m (svo_band {band_rows, m,
- * n_parts}), band layout, as svo_hit_compact records (SVO_PART_COMPACT: frame
+ * holds the rows of rank m of the deal `deal` (band_count == n_parts; band_rank
+ * ignored; round-robin: bands b with b % n_parts == m), band layout, as
+ * svo_hit_compact records (SVO_PART_COMPACT: frame
  * outputs hits / rgba / rgba8 / compact, the normal and colour rebuilt from this
  * context's SVO replica and camera) or RGBA8 words (SVO_PART_RGBA8: frame output
  * rgba8 only).  Part pointers must be readable from this device (its own memory,
@@ -156,8 +162,9 @@ int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const 
  * the one-process-per-GPU split (parts received over RCCL); multi-device
  * contexts use it internally.  Asynchronous. */
 enum { SVO_PART_COMPACT = 0, SVO_PART_RGBA8 = 1 };
-int svo_assemble_frame(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, const void *const *parts,
-                       int part_format, int skip_part, const svo_frame *frame, void *stream);
+int svo_assemble_frame(svo_ctx *ctx, int width, int height, const svo_band *deal, int n_parts,
+                       const void *const *parts, int part_format, int skip_part, const svo_frame *frame,
+                       void *stream);
 
 /* Instrumented trace: per-ray descriptor-fetch counts (device uint32 array,
  * NVIDIASVO.compute:60-62 executions), used for the algorithmic-bytes figure

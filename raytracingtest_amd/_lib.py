@@ -27,7 +27,7 @@ assert HIT_DTYPE.itemsize == 24
 COMPACT_DTYPE = np.dtype([("parent", "<u4"), ("meta", "<u4"), ("t", "<f4")])   # svo_hit_compact
 assert COMPACT_DTYPE.itemsize == 12
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
@@ -43,7 +43,21 @@ STAGE_KERNEL, STAGE_ASSEMBLE = 0, 1
 
 class SvoBand(ctypes.Structure):
     _fields_ = [("band_rows", ctypes.c_int), ("band_rank", ctypes.c_int),
-                ("band_count", ctypes.c_int)]
+                ("band_count", ctypes.c_int), ("cycle", ctypes.c_int),
+                ("owner", ctypes.POINTER(ctypes.c_uint8))]
+
+
+def make_band(band):
+    """svo_band of a Python deal: (band_rows, band_rank, band_count) round-robin, or
+    (band_rows, band_rank, band_count, owner) with owner[b % len(owner)] = rank
+    of band b.  The struct keeps its owner array alive."""
+    if len(band) == 3:
+        return SvoBand(int(band[0]), int(band[1]), int(band[2]), 0, None)
+    owner = (ctypes.c_uint8 * len(band[3]))(*[int(o) for o in band[3]])
+    b = SvoBand(int(band[0]), int(band[1]), int(band[2]), len(band[3]),
+                ctypes.cast(owner, ctypes.POINTER(ctypes.c_uint8)))
+    b._owner = owner
+    return b
 
 
 class SvoFrame(ctypes.Structure):
@@ -92,7 +106,8 @@ def lib():
         "svo_num_devices": [vp, ctypes.POINTER(i)],
         "svo_get_member": [vp, i, ctypes.POINTER(vp)],
         "svo_render_frame": [vp, i, i, i, vp, ctypes.POINTER(SvoFrame), vp],
-        "svo_assemble_frame": [vp, i, i, i, i, ctypes.POINTER(vp), i, i, ctypes.POINTER(SvoFrame), vp],
+        "svo_assemble_frame": [vp, i, i, ctypes.POINTER(SvoBand), i, ctypes.POINTER(vp), i, i,
+                               ctypes.POINTER(SvoFrame), vp],
         "svo_stage_time": [vp, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)],
         "svo_render_progressive": [vp, i, i, i, ctypes.c_uint32, vp, vp],
         "svo_synchronize": [vp],

@@ -515,8 +515,11 @@ __device__ __forceinline__ void shadow_ray(const LaunchParams &p, int x, int y, 
 }
 
 __device__ __forceinline__ int global_row(const LaunchParams &p, int lr) {
-    const int band = lr / p.band_rows;
-    return (band * p.band_count + p.band_rank) * p.band_rows + (lr - band * p.band_rows);
+    const int j = lr / p.band_rows;
+    const int in = lr - j * p.band_rows;
+    if (p.band_cycle == 0) return (j * p.band_count + p.band_rank) * p.band_rows + in;
+    const int c = j / p.band_cnt;
+    return (c * p.band_cycle + (int)p.band_pos[j - c * p.band_cnt]) * p.band_rows + in;
 }
 
 __device__ __forceinline__ size_t out_index(const LaunchParams &p, int lr, int gy, int x) {
@@ -700,17 +703,33 @@ __global__ __launch_bounds__(TILE) void shadow_tile_kernel(LaunchParams p, int t
 
 // ---------------------------------------------------------- frame assembly
 // svo_assemble_frame: one thread per pixel of the frame (one row per grid y).
-// Row y belongs to band b = y / band_rows, part m = b % n_parts, local row
-// (b / n_parts) * band_rows + y % band_rows of that part.  Parts are read where
+// Row y belongs to band b = y / band_rows and, round-robin, to part m = b % n_parts
+// at local row (b / n_parts) * band_rows + y % band_rows (part_of_row: also the
+// weighted deal).  Parts are read where
 // they lie: a peer device's memory over xGMI (peer access), or this device's.
+// Part and part-local row of frame row y (round-robin or weighted deal).
+__device__ __forceinline__ int part_of_row(const AssembleParams &a, int y, int *lr) {
+    const int band = y / a.band_rows;
+    int m, lband;
+    if (a.cycle == 0) {
+        m = band % a.n_parts;
+        lband = band / a.n_parts;
+    } else {
+        const int c = band / a.cycle, pos = band - c * a.cycle;
+        m = a.owner[pos];
+        lband = c * a.cnt[m] + a.idx[pos];
+    }
+    *lr = lband * a.band_rows + (y - band * a.band_rows);
+    return m;
+}
+
 __global__ __launch_bounds__(256) void assemble_kernel(AssembleParams a) {
     const int x = (int)(blockIdx.x * 256 + threadIdx.x);
     const int y = (int)blockIdx.y;
     if (x >= a.width) return;
-    const int band = y / a.band_rows;
-    const int m = band % a.n_parts;
+    int lr;
+    const int m = part_of_row(a, y, &lr);
     if (m == a.skip_part) return;
-    const int lr = (band / a.n_parts) * a.band_rows + (y - band * a.band_rows);
     const size_t src = (size_t)lr * (size_t)a.width + (size_t)x;
     const size_t dst = (size_t)y * (size_t)a.width + (size_t)x;
     if (a.part_format == PART_RGBA8) {
@@ -999,10 +1018,9 @@ hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int 
 // Needs width % 4 == 0 (16-byte aligned rows in every part and in the frame).
 __global__ __launch_bounds__(256) void assemble_rgba8_kernel(AssembleParams a) {
     const int y = (int)blockIdx.y;
-    const int band = y / a.band_rows;
-    const int m = band % a.n_parts;
+    int lr;
+    const int m = part_of_row(a, y, &lr);
     if (m == a.skip_part) return;
-    const int lr = (band / a.n_parts) * a.band_rows + (y - band * a.band_rows);
     const int q = (int)(blockIdx.x * 256 + threadIdx.x);   // 4-pixel group of the row
     if (4 * q >= a.width) return;
     const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(a.parts[m]) +

@@ -118,10 +118,11 @@ struct svo_ctx {
     unsigned long long shadow_launches = 0;
     size_t tile_cap = 0;
     long long order_key = -1;        // geometry d_tile_order was built for (-1: none)
-    // Work of one context is ordered across streams: the cost / order buffers,
-    // the scratch outputs and the node pool are shared by all its launches, so
-    // the first launch (or upload) on a new stream waits for everything enqueued
-    // on the previous one (an event recorded at the switch; no host sync).
+    // Renders of one context are ordered across streams: the cost / order buffers
+    // and the scratch outputs are shared by all its render launches, so the first
+    // render on a new stream waits for everything enqueued on the previous one (an
+    // event recorded at the switch; no host sync).  Assembles and accumulations
+    // touch no context state and are not ordered; uploads synchronise the device.
     hipStream_t last_stream = nullptr;
     bool last_valid = false;
     hipEvent_t switch_event = nullptr;
@@ -279,20 +280,52 @@ int ensure_accum(svo_ctx *ctx, int width, int height) {
     return SVO_OK;
 }
 
-int band_rows_local(int height, const svo_band &b) {
-    // rows y with (y / band_rows) % band_count == band_rank
+// A validated svo_band, the owner table copied (the caller's pointer is not kept).
+struct Deal {
+    int rows = 1, rank = 0, count = 1, cycle = 0;
+    uint8_t owner[svo::MAX_CYCLE] = {};
+    int owner_of(int band) const { return cycle ? owner[band % cycle] : band % count; }
+    uint64_t key() const {   // identifies the deal (tile-order cache key)
+        uint64_t h = 1469598103934665603ull;
+        for (int i = 0; i < cycle; ++i) h = (h ^ owner[i]) * 1099511628211ull;
+        return h ^ (uint64_t)cycle;
+    }
+};
+
+int band_rows_local(int height, const Deal &d) {
+    // rows y whose band y / rows belongs to this rank
     int rows = 0;
-    for (int y0 = b.band_rank * b.band_rows; y0 < height; y0 += b.band_rows * b.band_count)
-        rows += std::min(b.band_rows, height - y0);
+    if (d.cycle == 0) {
+        for (int y0 = d.rank * d.rows; y0 < height; y0 += d.rows * d.count) rows += std::min(d.rows, height - y0);
+        return rows;
+    }
+    for (int b = 0; b * d.rows < height; ++b)
+        if (d.owner[b % d.cycle] == d.rank) rows += std::min(d.rows, height - b * d.rows);
     return rows;
 }
 
-int check_band(const svo_band *band, int height, svo_band *out) {
-    svo_band b = band ? *band : svo_band{1, 0, 1};
-    if (b.band_rows <= 0 || b.band_count <= 0 || b.band_rank < 0 || b.band_rank >= b.band_count)
-        return fail(SVO_ERR_ARG, "invalid svo_band");
-    if (b.band_count == 1) b.band_rows = height > 0 ? height : 1;
-    *out = b;
+int check_band(const svo_band *band, int height, Deal *out) {
+    Deal d;
+    if (band) {
+        d.rows = band->band_rows;
+        d.rank = band->band_rank;
+        d.count = band->band_count;
+        d.cycle = band->cycle;
+    }
+    if (d.rows <= 0 || d.count <= 0 || d.rank < 0 || d.rank >= d.count) return fail(SVO_ERR_ARG, "invalid svo_band");
+    if (d.cycle < 0 || d.cycle > svo::MAX_CYCLE) return fail(SVO_ERR_ARG, "svo_band.cycle must be in [0, 256]");
+    if (d.cycle > 0) {
+        if (!band->owner) return fail(SVO_ERR_ARG, "svo_band.owner is null");
+        for (int i = 0; i < d.cycle; ++i) {
+            if (band->owner[i] >= d.count) return fail(SVO_ERR_ARG, "svo_band.owner entry out of range");
+            d.owner[i] = band->owner[i];
+        }
+    }
+    if (d.count == 1) {
+        d.rows = height > 0 ? height : 1;
+        d.cycle = 0;
+    }
+    *out = d;
     return SVO_OK;
 }
 
@@ -337,7 +370,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         return fail(SVO_ERR_ARG, "unknown stack mode");
     if (ctx->n_nodes == 0) return fail(SVO_ERR_STATE, "no node pool uploaded (svo_set_buffer)");
     if (!ctx->cam_set) return fail(SVO_ERR_STATE, "camera not set (svo_set_camera)");
-    svo_band b;
+    Deal b;
     int rc = check_band(band, height, &b);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
@@ -349,9 +382,12 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.cam = ctx->cam;
     p.width = width;
     p.height = height;
-    p.band_rows = b.band_rows;
-    p.band_rank = b.band_rank;
-    p.band_count = b.band_count;
+    p.band_rows = b.rows;
+    p.band_rank = b.rank;
+    p.band_count = b.count;
+    p.band_cycle = b.cycle;
+    for (int i = 0; i < b.cycle; ++i)
+        if (b.owner[i] == b.rank) p.band_pos[p.band_cnt++] = (uint8_t)i;
     p.local_rows = band_rows_local(height, b);
     p.slots = std::max(ctx->depth - 1, 1);
     // guard: stack-overflow test + HLSL parent round trip, needed unless the
@@ -363,7 +399,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // cost 6-12 % on the 25 M / 100 M-node C4 / C5 pools (svo_kernel.hip trace_lean)
     p.fetch_all = ctx->fetch_all >= 0 ? ctx->fetch_all : (ctx->n_nodes < ((size_t)1 << 24) ? 1 : 0);
     p.out = out;
-    if (b.band_count == 1) p.out.frame_layout = 0;   // the whole frame: both layouts coincide
+    if (b.count == 1) p.out.frame_layout = 0;   // the whole frame: both layouts coincide
     p.xcd_remap = ctx->xcd_remap;
     if (p.xcd_remap == 2 && ((width + 7) / 8) % 8 != 0) p.xcd_remap = 0;
     p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? (ctx->fused_shadows ? 2 : 1) : 0;
@@ -382,8 +418,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
     long long key = -1;
     if (ordered) {
-        key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^ ((long long)b.band_rows << 8) ^
-              (long long)b.band_rank ^ ((long long)b.band_count << 4) ^ ((long long)p.xcd_remap << 60);
+        key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^ ((long long)b.rows << 8) ^
+              (long long)b.rank ^ ((long long)b.count << 4) ^ ((long long)p.xcd_remap << 60) ^ (long long)(b.key() << 1);
+        if (key < 0) key = ~key;   // -1 means "no order"
         if (ctx->tile_cap < (size_t)n_tiles) {
             HIP_TRY(hipDeviceSynchronize());   // a pending launch may still use the old buffers
             if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
@@ -461,7 +498,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
 
 // Enqueue the assemble kernel on this context's device (svo_assemble_frame, and
 // the gather of a multi-device frame).
-int assemble(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, const void *const *parts,
+int assemble(svo_ctx *ctx, int width, int height, const Deal &deal, int n_parts, const void *const *parts,
              int part_format, int skip_part, const svo::Outputs &out, hipStream_t s) {
     svo::AssembleParams a;
     std::memset(&a, 0, sizeof a);
@@ -470,8 +507,14 @@ int assemble(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, co
     a.cam = ctx->cam;
     a.width = width;
     a.height = height;
-    a.band_rows = band_rows;
+    a.band_rows = deal.rows;
     a.n_parts = n_parts;
+    a.cycle = deal.cycle;
+    for (int i = 0; i < deal.cycle; ++i) {
+        const int m = deal.owner[i];
+        a.owner[i] = (uint8_t)m;
+        a.idx[i] = (uint8_t)a.cnt[m]++;
+    }
     a.part_format = part_format;
     a.skip_part = skip_part;
     for (int i = 0; i < n_parts; ++i) a.parts[i] = parts[i];
@@ -487,10 +530,9 @@ int assemble(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, co
     return SVO_OK;
 }
 
-int check_assemble_args(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, int part_format,
-                        int skip_part, const svo::Outputs &o) {
+int check_assemble_args(svo_ctx *ctx, int width, int height, int n_parts, int part_format, int skip_part,
+                        const svo::Outputs &o) {
     if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
-    if (band_rows <= 0) return fail(SVO_ERR_ARG, "band_rows must be positive");
     if (n_parts < 1 || n_parts > svo::MAX_PARTS) return fail(SVO_ERR_ARG, "n_parts must be in [1, 64]");
     if (skip_part < -1 || skip_part >= n_parts) return fail(SVO_ERR_ARG, "skip_part out of range");
     if (o.position || o.voxel || o.fetches) return fail(SVO_ERR_ARG, "position / voxel outputs are not assembled");
@@ -520,15 +562,18 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
     svo_ctx *m0 = ctx->members[0];
     hipStream_t s0 = stream ? stream : m0->stream;
     // the display device renders its own bands straight into the caller's frame
-    svo_band b0{ctx->band_rows, 0, n};
+    svo_band b0{ctx->band_rows, 0, n, 0, nullptr};
     int rc = launch(m0, width, height, stack_mode, &b0, out, s0);
     if (rc) return rc;
     std::vector<const void *> parts(n, nullptr);
     for (int i = 1; i < n; ++i) {
         svo_ctx *m = ctx->members[i];
         Peer &pr = ctx->peers[i];
-        svo_band bi{ctx->band_rows, i, n};
-        const size_t bytes = (size_t)band_rows_local(height, bi) * (size_t)width * elem;
+        svo_band bi{ctx->band_rows, i, n, 0, nullptr};
+        Deal di;
+        rc = check_band(&bi, height, &di);
+        if (rc) return rc;
+        const size_t bytes = (size_t)band_rows_local(height, di) * (size_t)width * elem;
         HIP_TRY(hipSetDevice(m->device));
         if (pr.cap_bytes < bytes) {
             HIP_TRY(hipSetDevice(m0->device));
@@ -556,7 +601,10 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
     for (int i = 1; i < n; ++i) HIP_TRY(hipStreamWaitEvent(s0, ctx->peers[i].rendered[k], 0));
     rc = order_streams(m0, s0);
     if (rc) return rc;
-    rc = assemble(m0, width, height, ctx->band_rows, n, parts.data(), fmt, 0, out, s0);
+    Deal deal;
+    rc = check_band(&b0, height, &deal);
+    if (rc) return rc;
+    rc = assemble(m0, width, height, deal, n, parts.data(), fmt, 0, out, s0);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(ctx->gathered[k], s0));
     ctx->gathered_used[k] = true;
@@ -592,7 +640,7 @@ int destroy_single(svo_ctx *ctx) {
 
 extern "C" {
 
-int svo_abi_version(void) { return 3; }
+int svo_abi_version(void) { return 4; }
 
 const char *svo_last_error(void) { return g_last_error.c_str(); }
 
@@ -720,8 +768,8 @@ int svo_set_buffer(svo_ctx *ctx, const int32_t *desc, size_t n_desc, const uint3
     int rc = validate_upload(ctx, lo.data(), first.data(), n_desc, dst_offset, &u);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
-    rc = order_streams(ctx, ctx->stream);   // renders on other streams may still read the pool
-    if (rc) return rc;
+    // renders, assembles and accumulations on any stream may still read the pool
+    HIP_TRY(hipDeviceSynchronize());
     if (n_desc > ctx->stage_cap) {
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         if (ctx->d_stage) hipFree(ctx->d_stage);
@@ -765,8 +813,7 @@ int svo_set_buffer_v2(svo_ctx *ctx, const uint64_t *nodes, size_t n_nodes, const
     int rc = validate_upload(ctx, lo.data(), first.data(), n_nodes, dst_offset, &u);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
-    rc = order_streams(ctx, ctx->stream);
-    if (rc) return rc;
+    HIP_TRY(hipDeviceSynchronize());   // as in svo_set_buffer
     static_assert(sizeof(uint2) == sizeof(uint64_t), "node layout");
     HIP_TRY(hipMemcpyAsync(ctx->d_nodes + dst_offset, nodes, n_nodes * sizeof(uint64_t), hipMemcpyHostToDevice,
                            ctx->stream));
@@ -801,20 +848,29 @@ int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const 
     return launch(ctx, width, height, stack_mode, band, outputs_of(frame), reinterpret_cast<hipStream_t>(stream));
 }
 
-int svo_assemble_frame(svo_ctx *ctx, int width, int height, int band_rows, int n_parts, const void *const *parts,
-                       int part_format, int skip_part, const svo_frame *frame, void *stream) {
-    if (!ctx || !parts || !frame) return fail(SVO_ERR_ARG, "null argument");
+int svo_assemble_frame(svo_ctx *ctx, int width, int height, const svo_band *deal, int n_parts,
+                       const void *const *parts, int part_format, int skip_part, const svo_frame *frame,
+                       void *stream) {
+    if (!ctx || !parts || !frame || !deal) return fail(SVO_ERR_ARG, "null argument");
     svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
     svo::Outputs o = outputs_of(frame);
-    int rc = check_assemble_args(c, width, height, band_rows, n_parts, part_format, skip_part, o);
+    int rc = check_assemble_args(c, width, height, n_parts, part_format, skip_part, o);
+    if (rc) return rc;
+    if (deal->band_count != n_parts) return fail(SVO_ERR_ARG, "deal band_count must equal n_parts");
+    svo_band db = *deal;
+    db.band_rank = 0;
+    Deal d;
+    rc = check_band(&db, height, &d);
     if (rc) return rc;
     for (int i = 0; i < n_parts; ++i)
         if (!parts[i] && i != skip_part) return fail(SVO_ERR_ARG, "null part pointer");
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
-    rc = order_streams(c, s);
-    if (rc) return rc;
-    return assemble(c, width, height, band_rows, n_parts, parts, part_format, skip_part, o, s);
+    // no ordering against the context's render streams: the assemble reads only the
+    // caller's parts and the (upload-synchronised) attachments and writes only the
+    // caller's frame, so a gather stream beside the render stream runs concurrently
+    // (ordering the two made the display rank's step 1.3x slower, tools/rank0_cost.py)
+    return assemble(c, width, height, d, n_parts, parts, part_format, skip_part, o, s);
 }
 
 int svo_render(svo_ctx *ctx, int width, int height, int stack_mode, float *rgba_out, svo_hit *hits_out) {
@@ -954,8 +1010,7 @@ int svo_accumulate(svo_ctx *ctx, void *d_accum, const void *d_sample, size_t n_p
     svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    int rc = order_streams(c, s);
-    if (rc) return rc;
+    // caller buffers only: the caller orders them against its renders (no context state)
     hipError_t e = svo::launch_accumulate(reinterpret_cast<float4 *>(d_accum), reinterpret_cast<const float4 *>(d_sample),
                                           n_px, sample, c->num_cus, s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("accumulate launch: ") + hipGetErrorString(e));

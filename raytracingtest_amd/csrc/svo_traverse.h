@@ -19,6 +19,7 @@ constexpr int S_MAX = 23;          // NVIDIASVO.compute:2
 constexpr int MAX_ITERS = 65536;   // safety net, identical in oracle/svo_oracle.c
 constexpr int TILE = 64;           // one wave64 = one 8x8 pixel tile
 constexpr int MAX_PARTS = 64;      // band parts one assemble launch reads (devices / ranks)
+constexpr int MAX_CYCLE = 256;     // bands per cycle of a weighted band deal (svo_band.cycle)
 
 struct Camera {
     float c2w[16];        // Unity Matrix4x4, column-major
@@ -57,6 +58,10 @@ struct LaunchParams {
     Camera cam;
     int width, height;
     int band_rows, band_rank, band_count, local_rows;
+    // weighted deal (band_cycle > 0): this render's j-th band is band
+    // (j / band_cnt) * band_cycle + band_pos[j % band_cnt]; 0 = round-robin
+    int band_cycle, band_cnt;
+    uint8_t band_pos[MAX_CYCLE];
     int slots;            // stack slots = depth - 1 (scales [23 - slots, 22])
     Outputs out;
     int xcd_remap;        // 2: interleaved XCD column strips, 0: raster
@@ -88,6 +93,11 @@ struct AssembleParams {
     Camera cam;
     int width, height, band_rows, n_parts, part_format, skip_part;
     const void *parts[MAX_PARTS];
+    // weighted deal (cycle > 0): band b belongs to part owner[b % cycle] and is that
+    // part's band (b / cycle) * cnt[part] + idx[b % cycle]; 0 = round-robin
+    int cycle;
+    uint8_t owner[MAX_CYCLE], idx[MAX_CYCLE];
+    int cnt[MAX_PARTS];
     Outputs out;          // frame layout
 };
 

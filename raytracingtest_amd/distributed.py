@@ -32,17 +32,31 @@ from .raytracing_master import band_rows
 DEFAULT_BAND_ROWS = 8
 
 
-def rank_band(rank, world, rows=DEFAULT_BAND_ROWS):
-    """svo_band triple (band_rows, band_rank, band_count) for this rank."""
-    return (rows, rank, world)
+def rank_band(rank, world, rows=DEFAULT_BAND_ROWS, owner=None):
+    """svo_band deal of this rank: (band_rows, band_rank, band_count) round-robin, or
+    with an owner table (weighted_owner) appended."""
+    return (rows, rank, world) if owner is None else (rows, rank, world, tuple(owner))
 
 
-def band_len(height, rank, world, rows=DEFAULT_BAND_ROWS):
-    return len(band_rows(height, (rows, rank, world)))
+def band_len(height, rank, world, rows=DEFAULT_BAND_ROWS, owner=None):
+    return len(band_rows(height, rank_band(rank, world, rows, owner)))
 
 
-def max_band_len(height, world, rows=DEFAULT_BAND_ROWS):
-    return max(band_len(height, r, world, rows) for r in range(world))
+def max_band_len(height, world, rows=DEFAULT_BAND_ROWS, owner=None):
+    return max(band_len(height, r, world, rows, owner) for r in range(world))
+
+
+def weighted_owner(world, display_share, per_round=8):
+    """Owner table of a weighted deal: `per_round` rounds in which every rank but
+    the display rank (0) takes one band and rank 0 takes one in only
+    round(display_share * per_round) of them -- rank 0 also receives and assembles
+    the frame, so it gets fewer rows.  Rounds interleave the ranks,
+    so a partial cycle at the frame's bottom stays balanced."""
+    k = int(round(min(max(display_share, 0.0), 1.0) * per_round))
+    owner = []
+    for j in range(per_round):
+        owner += [r for r in range(world) if r > 0 or j < k]
+    return owner
 
 
 def weak_frame(width, height, world):

@@ -27,7 +27,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import HIT_DTYPE, LAYOUT_BAND, LAYOUT_FRAME, STACK_EXACT, STACK_HLSL, SvoBand, SvoError, SvoFrame, check
+from ._lib import HIT_DTYPE, LAYOUT_BAND, LAYOUT_FRAME, STACK_EXACT, STACK_HLSL, SvoError, SvoFrame, check, make_band
 from .camera import column_major, main_camera, main_light
 from .svo_data import SVOData
 
@@ -178,7 +178,7 @@ class RaytracingMaster:
                       band=None, stream=None):
         """Asynchronous render into device buffers (raw device pointers, e.g. torch
         tensor.data_ptr()), optionally only this rank's row bands."""
-        b = None if band is None else ctypes.byref(SvoBand(*band))
+        b = None if band is None else ctypes.byref(make_band(band))
         check(_lib.lib().svo_render_device(self._ctx, width, height, stack_mode, b, rgba_ptr, hits_ptr, stream),
               "svo_render_device")
 
@@ -188,23 +188,27 @@ class RaytracingMaster:
         layout LAYOUT_BAND: buffers hold only `band`'s rows; LAYOUT_FRAME: full-frame
         buffers.  A multi-device context renders the whole frame (band None) onto
         devices[0]."""
-        b = None if band is None else ctypes.byref(SvoBand(*band))
+        b = None if band is None else ctypes.byref(make_band(band))
         f = _frame(hits, rgba, rgba8, compact, position, voxel, layout)
         check(_lib.lib().svo_render_frame(self._ctx, width, height, stack_mode, b, ctypes.byref(f), stream),
               "svo_render_frame")
 
     def assemble_frame(self, width, height, parts, part_format, band_rows=None, hits=None, rgba=None, rgba8=None,
-                       compact=None, skip_part=-1, stream=None):
+                       compact=None, skip_part=-1, stream=None, owner=None):
         """Rebuild a frame (full-frame device buffers) from band parts: parts[m] = the
-        device pointer of rank m's band payload (compact records or RGBA8 words)."""
+        device pointer of rank m's band payload (compact records or RGBA8 words).
+        The deal: band_rows-row bands, round-robin, or owner[b % len(owner)] = the
+        part holding band b (weighted deal)."""
         arr = (ctypes.c_void_p * len(parts))(*[p if p else None for p in parts])
         f = _frame(hits, rgba, rgba8, compact, None, None, LAYOUT_FRAME)
-        check(_lib.lib().svo_assemble_frame(self._ctx, width, height, self.band_rows if band_rows is None else band_rows,
-                                            len(parts), arr, part_format, skip_part, ctypes.byref(f), stream),
+        rows = self.band_rows if band_rows is None else band_rows
+        deal = make_band((rows, 0, len(parts)) if owner is None else (rows, 0, len(parts), owner))
+        check(_lib.lib().svo_assemble_frame(self._ctx, width, height, ctypes.byref(deal), len(parts), arr,
+                                            part_format, skip_part, ctypes.byref(f), stream),
               "svo_assemble_frame")
 
     def count_fetches_device(self, width, height, fetch_ptr, stack_mode=STACK_HLSL, band=None, stream=None):
-        b = None if band is None else ctypes.byref(SvoBand(*band))
+        b = None if band is None else ctypes.byref(make_band(band))
         check(_lib.lib().svo_count_fetches(self._ctx, width, height, stack_mode, b, fetch_ptr, stream),
               "svo_count_fetches")
 
@@ -265,10 +269,15 @@ class _MemberView(RaytracingMaster):
 
 
 def band_rows(height, band):
-    """Global row indices owned by `band` = (band_rows, band_rank, band_count), in order."""
-    rows, rank, count = band
+    """Global row indices owned by `band` = (band_rows, band_rank, band_count) (round-robin)
+    or (band_rows, band_rank, band_count, owner) (band b belongs to owner[b % len(owner)]),
+    in order."""
+    rows, rank, count = band[:3]
     ys = np.arange(height)
-    return ys[(ys // rows) % count == rank]
+    if len(band) == 3:
+        return ys[(ys // rows) % count == rank]
+    owner = np.asarray(band[3], np.int64)
+    return ys[owner[(ys // rows) % len(owner)] == rank]
 
 
 __all__ = ["RaytracingMaster", "SVOData", "SvoError", "STACK_HLSL", "STACK_EXACT", "HIT_DTYPE", "band_rows"]

@@ -40,7 +40,7 @@ def test_exports_every_declared_symbol(native):
 
 
 def test_abi_version_and_error_text(native):
-    assert native.svo_abi_version() == 3
+    assert native.svo_abi_version() == 4
     assert isinstance(native.svo_last_error(), bytes)
 
 
@@ -57,7 +57,7 @@ def test_header_layout_compiles_in_c(tmp_path):
                    '_Static_assert(sizeof(svo_hit) == 24, "hit");\n'
                    '_Static_assert(offsetof(svo_hit, t) == 8, "t");\n'
                    '_Static_assert(offsetof(svo_hit, nz) == 20, "nz");\n'
-                   '_Static_assert(sizeof(svo_band) == 12, "band");\n'
+                   '_Static_assert(sizeof(svo_band) == 16 + sizeof(void *), "band");\n'
                    '_Static_assert(sizeof(svo_hit_compact) == 12, "compact");\n'
                    '_Static_assert(offsetof(svo_frame, layout) == 48, "frame");\n'
                    '_Static_assert(SVO_PART_RGBA8 == 1 && SVO_LAYOUT_FRAME == 1 && SVO_STAGE_ASSEMBLE == 1, "enums");\n'
@@ -75,7 +75,7 @@ def test_multi_device_and_frame_entry_points_reject_bad_arguments_without_gpu(na
     assert native.svo_create_multi(devs, 0, 16, 8, ctypes.byref(out)) == -1      # no device touched
     assert native.svo_create_multi(devs, 2, 16, 0, ctypes.byref(out)) == -1      # band_rows
     assert native.svo_render_frame(None, 8, 8, 0, None, ctypes.byref(SvoFrame()), None) == -1
-    assert native.svo_assemble_frame(None, 8, 8, 8, 1, None, 0, -1, None, None) == -1
+    assert native.svo_assemble_frame(None, 8, 8, None, 1, None, 0, -1, None, None) == -1
     assert native.svo_stage_time(None, 0, None, None) == -1
     n = ctypes.c_int()
     assert native.svo_num_devices(None, ctypes.byref(n)) == -1

@@ -129,3 +129,24 @@ def test_band_helpers_cover_frame():
     parts = [np.arange(len(band_rows(20, (8, r, 2))) * 3, dtype=np.int32) + 1000 * r for r in range(2)]
     f = assemble(parts, 20, 3, np.int32)
     assert f.shape == (20, 3) and f[0, 0] == 0 and f[8, 0] == 1000
+
+
+def test_weighted_deal_covers_frame_and_balances():
+    """Weighted band deal (the display rank takes fewer bands): every row owned
+    exactly once, the display rank's share follows display_share, the other ranks
+    stay within one band of each other, also across a partial last cycle."""
+    from raytracingtest_amd import band_rows
+    from raytracingtest_amd.distributed import band_len, max_band_len, rank_band, weighted_owner
+    for world, share in ((2, 0.9), (4, 0.75), (8, 0.6), (8, 0.0), (3, 1.0)):
+        owner = weighted_owner(world, share)
+        assert len(owner) <= 256 and set(owner) <= set(range(world))
+        assert owner.count(0) == round(share * 8) and all(owner.count(r) == 8 for r in range(1, world))
+        for H in (1080, 3056, 4320, 37):
+            seen = np.concatenate([band_rows(H, rank_band(r, world, 8, owner)) for r in range(world)])
+            assert np.array_equal(np.sort(seen), np.arange(H))
+            lens = [band_len(H, r, world, 8, owner) for r in range(world)]
+            assert max(lens[1:]) - min(lens[1:]) <= 8
+            assert max_band_len(H, world, 8, owner) == max(lens)
+            if H >= 1080 and share > 0:
+                assert abs(lens[0] / lens[1] - round(share * 8) / 8) < 0.15
+    assert weighted_owner(3, 1.0) == [0, 1, 2] * 8

@@ -250,6 +250,47 @@ def test_assemble_from_rank_parts(torch, oracle_mod, world):
         m.close()
 
 
+@pytest.mark.parametrize("world,share", [(2, 0.625), (3, 0.5), (8, 0.75)])
+def test_weighted_deal_parts_match_oracle(torch, oracle_mod, world, share):
+    """bench.py's weighted deal (the display rank renders fewer bands): parts
+    rendered with the owner table in svo_band, the display rank's own rows
+    straight into the frame, the rest assembled by svo_assemble_frame with the
+    same table -- RGBA8 and compact parts, both bit-identical to one frame."""
+    from raytracingtest_amd.distributed import weighted_owner
+    svo = build_menger(7)
+    cam = overview_camera()
+    w, h = (262 if world == 3 else 264), 203   # 262: rows not 16-byte multiples (per-pixel assemble path)
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+    owner = weighted_owner(world, share)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        b = _bufs(torch, w * h)
+        m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(), rgba8=b["rgba8"].data_ptr(),
+                       layout=_lib.LAYOUT_FRAME, band=(8, 0, world, owner))
+        comp, rgb8 = [None], [None]
+        for r in range(1, world):
+            n = len(band_rows(h, (8, r, world, owner))) * w
+            comp.append(torch.zeros(max(n, 1) * 12, dtype=torch.uint8, device="cuda"))
+            rgb8.append(torch.zeros(max(n, 1), dtype=torch.int32, device="cuda"))
+            m.render_frame(w, h, compact=comp[-1].data_ptr(), rgba8=rgb8[-1].data_ptr(), band=(8, r, world, owner))
+        b2 = _bufs(torch, w * h)
+        m.render_frame(w, h, rgba8=b2["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME, band=(8, 0, world, owner))
+        m.assemble_frame(w, h, [None] + [c.data_ptr() for c in rgb8[1:]], _lib.PART_RGBA8,
+                         rgba8=b2["rgba8"].data_ptr(), skip_part=0, owner=owner)
+        m.assemble_frame(w, h, [None] + [c.data_ptr() for c in comp[1:]], _lib.PART_COMPACT,
+                         hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(), rgba8=b["rgba8"].data_ptr(),
+                         skip_part=0, owner=owner)
+        m.synchronize()
+        _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba", "rgba8"))
+        _check(b2, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+        with pytest.raises(SvoError):   # owner entry naming a rank outside the deal
+            m.render_frame(w, h, rgba8=b2["rgba8"].data_ptr(), band=(8, 0, world, [0, world]))
+    finally:
+        m.close()
+
+
 def test_two_streams_every_pixel_written(torch, oracle_mod):
     """Launches of one context alternating between two streams (advisor r1): the
     shared dispatch-order buffers are rebuilt every launch (SVO_ORDER_EVERY=1)
