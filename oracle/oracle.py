@@ -18,6 +18,7 @@ FMT_V1, FMT_V2 = 1, 2
 STACK_HLSL, STACK_EXACT = 0, 1
 SHADOW_RAYS = 0x100   # OR into stack_mode: one shadow ray per primary hit
 COUNT_ITERS = 0x200   # OR into stack_mode: the fetch output counts loop iterations instead
+COUNT_SHADOW_ITERS = 0x400   # with SHADOW_RAYS: the fetch output counts the shadow ray's iterations
 
 HIT_DTYPE = np.dtype([("parent", "<u4"), ("hit_idx", "u1"), ("hit_scale", "u1"),
                       ("flags", "<u2"), ("t", "<f4"), ("nx", "<f4"), ("ny", "<f4"),

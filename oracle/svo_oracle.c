@@ -333,6 +333,11 @@ static void shade_pixel(const orc_camera *cam, const orc_hit *hit, const float a
  * P + 0.001 * n, direction -L.  Returns 1 when the shadow ray hits a voxel. */
 int orc_shadow_ray(const orc_svo *svo, const orc_camera *cam, const float o[3], const float d[3],
                    const orc_hit *h, int mode) {
+    return orc_shadow_ray_ex(svo, cam, o, d, h, mode, NULL);
+}
+
+int orc_shadow_ray_ex(const orc_svo *svo, const orc_camera *cam, const float o[3], const float d[3],
+                      const orc_hit *h, int mode, uint32_t *iters_out) {
     const float tw = h->t * (1.0f / 64.0f);
     const float n[3] = { h->nx, h->ny, h->nz };
     float so[3], sd[3];
@@ -342,7 +347,7 @@ int orc_shadow_ray(const orc_svo *svo, const orc_camera *cam, const float o[3], 
         sd[k] = -cam->light[k];
     }
     orc_hit sh;
-    return orc_intersect(svo, so, sd, mode & 0xFF, &sh, NULL, NULL, NULL);
+    return orc_intersect(svo, so, sd, mode & 0xFF, &sh, NULL, NULL, iters_out);
 }
 
 static void trace_pixel(const orc_svo *svo, const orc_camera *cam, int width, int height,
@@ -357,8 +362,12 @@ static void trace_pixel(const orc_svo *svo, const orc_camera *cam, int width, in
     if (mode & ORC_COUNT_ITERS) f = it;   /* diagnostics: loop iterations instead of fetches */
     int shadowed = 0;
     if ((mode & ORC_SHADOW_RAYS) && (h.flags & 1)) {
-        shadowed = orc_shadow_ray(svo, cam, o, d, &h, mode);
+        uint32_t sit = 0;
+        shadowed = orc_shadow_ray_ex(svo, cam, o, d, &h, mode, &sit);
         if (shadowed) h.flags |= 8;   /* bit3: in shadow */
+        if (mode & ORC_COUNT_SHADOW_ITERS) f = sit;
+    } else if (mode & ORC_COUNT_SHADOW_ITERS) {
+        f = 0;
     }
     if (hit_out) *hit_out = h;
     if (rgba_out) {

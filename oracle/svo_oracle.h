@@ -44,6 +44,9 @@ enum { ORC_STACK_HLSL = 0, ORC_STACK_EXACT = 1 };
 #define ORC_SHADOW_RAYS 0x100
 /* OR into mode: the fetches output receives loop iterations (NVIDIASVO.compute:57) instead */
 #define ORC_COUNT_ITERS 0x200
+/* diagnostics (with ORC_SHADOW_RAYS): the fetch output counts the shadow ray's loop
+ * iterations instead (0 for pixels without a shadow ray) */
+#define ORC_COUNT_SHADOW_ITERS 0x400
 
 /* Per-pixel hit record: identical layout to svo_hit in include/svo_rt.h. */
 typedef struct orc_hit {
@@ -93,6 +96,8 @@ int  orc_intersect_ex(const orc_svo *svo, const float origin[3], const float dir
 void orc_sky(const float dir[3], float out[3]);
 
 /* Shadow ray toward -L from a primary hit; 1 if occluded (see svo_oracle.c). */
+int  orc_shadow_ray_ex(const orc_svo *svo, const orc_camera *cam, const float o[3], const float d[3],
+                       const orc_hit *h, int mode, uint32_t *iters_out);
 int  orc_shadow_ray(const orc_svo *svo, const orc_camera *cam, const float o[3], const float d[3],
                     const orc_hit *hit, int stack_mode);
 

@@ -304,3 +304,19 @@ def test_oracle_reproduces_c1_golden_frames(oracle_mod, text_svo, mode, camera_n
                                       ocam, 256, 256, mode)
     assert hits.tobytes() == z[key + "_hits"].tobytes()
     assert rgba.astype(np.float32).tobytes() == z[camera_name + "_rgba"].tobytes()
+
+
+def test_shadow_iteration_counts_diagnostic(oracle_mod, text_svo):
+    """COUNT_SHADOW_ITERS (tools/simd_efficiency.py): the per-pixel output counts the
+    shadow ray's loop iterations, 0 exactly where no shadow ray is traced; the
+    records are the same as without the diagnostic."""
+    from raytracingtest_amd.camera import main_camera, main_light
+    w = h = 64
+    c2w, inv_proj = main_camera().uniforms(w, h)
+    cam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
+    svo = oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments)
+    hits, _, sit = oracle_mod.render(svo, cam, w, h, oracle_mod.SHADOW_RAYS | oracle_mod.COUNT_SHADOW_ITERS)
+    ref, _, _ = oracle_mod.render(svo, cam, w, h, oracle_mod.SHADOW_RAYS)
+    assert hits.tobytes() == ref.tobytes()
+    hit = (hits["flags"] & 1) != 0
+    assert hit.any() and np.all(sit[~hit] == 0) and np.all(sit[hit] > 0)

@@ -46,7 +46,10 @@ def main():
                              want_rgba=False)
     _, _, fe = orc.render(osvo, ocam, W, H, 0, nthreads=min(16, os.cpu_count() or 1), want_rgba=False)
     if args.save_iters:
+        _, _, sit = orc.render(osvo, ocam, W, H, orc.SHADOW_RAYS | orc.COUNT_SHADOW_ITERS,
+                               nthreads=min(16, os.cpu_count() or 1), want_rgba=False)
         np.savez_compressed(args.save_iters, iters=it.reshape(H, W).astype(np.uint16),
+                            shadow_iters=sit.reshape(H, W).astype(np.uint16),
                             fetches=fe.reshape(H, W).astype(np.uint16),
                             hit=((hits["flags"] & 1) != 0).reshape(H, W))
     it = it.reshape(H // 8, 8, W // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64).astype(np.int64)
