@@ -77,6 +77,39 @@ int main(int argc, char **argv) {
     /* the cube face spans ~2 * atan(16/24) = 67 degrees > the 60-degree view: every ray hits */
     ok = ok && n_hit == W * H;
 
+    /* OnRenderImage end to end (svo_render_progressive): two samples at the same pixel
+     * offset accumulate to the sample itself, so the display words are the packed Result */
+    uint32_t *rgba8 = (uint32_t *)malloc(sizeof(uint32_t) * W * H);
+    for (uint32_t sample = 0; sample < 2; ++sample)
+        check(svo_render_progressive(ctx, W, H, SVO_STACK_HLSL, sample, rgba8, NULL), "svo_render_progressive");
+    int bad8 = 0;
+    for (int i = 0; i < W * H; ++i) {
+        uint32_t want = 255u << 24;
+        for (int k = 0; k < 3; ++k) {
+            float v = fminf(fmaxf(rgba[i * 4 + k], 0.0f), 1.0f) * 255.0f;
+            want |= (uint32_t)(v + 0.5f) << (8 * k);
+        }
+        bad8 += rgba8[i] != want;
+    }
+    printf("progressive: %d display words differ\n", bad8);
+    ok = ok && bad8 == 0;
+
+    /* the same frame split over a two-member multi-device context (device 0 twice:
+     * the bands of member 1 travel as a payload and are assembled on member 0) */
+    const int devs[2] = { 0, 0 };
+    svo_ctx *multi = NULL;
+    check(svo_create_multi(devs, 2, 1024, 8, &multi), "svo_create_multi");
+    check(svo_set_buffer(multi, desc, 1, att, 2, 0), "svo_set_buffer (multi)");
+    check(svo_set_camera(multi, c2w, inv_proj, 0.5f, 0.5f, light), "svo_set_camera (multi)");
+    svo_hit *hits2 = (svo_hit *)malloc(sizeof(svo_hit) * W * H);
+    check(svo_render(multi, W, H, SVO_STACK_HLSL, NULL, hits2), "svo_render (multi)");
+    const int same = memcmp(hits, hits2, sizeof(svo_hit) * W * H) == 0;
+    printf("multi-device frame %s the single-device frame\n", same ? "equals" : "DIFFERS FROM");
+    ok = ok && same;
+    check(svo_destroy(multi), "svo_destroy (multi)");
+    free(hits2);
+    free(rgba8);
+
     if (argc > 1) {   /* the Result texture as a PPM */
         FILE *fp = fopen(argv[1], "wb");
         if (fp) {

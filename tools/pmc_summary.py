@@ -29,6 +29,8 @@ def per_kernel(path, name_sub="render_tile_kernel"):
             targs = [a.strip() for a in name[name.index("<") + 1:name.index(">")].split(",")]
             if len(targs) > 1 and targs[1] == "true":   # the instrumented (fetch-counting) launch
                 continue
+            if len(targs) > 3 and targs[3] == "true":   # the fused shadow-ray launches (c3_plus_shadow_ray)
+                continue
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 

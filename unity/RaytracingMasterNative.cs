@@ -14,6 +14,8 @@ public static class SvoNative {
                            public float t, nx, ny, nz; }                          // 24 bytes == svo_hit
 
     [DllImport(Lib)] public static extern int svo_create(int device, UIntPtr capacityNodes, out IntPtr ctx);
+    [DllImport(Lib)] public static extern int svo_create_multi(int[] devices, int numDevices, UIntPtr capacityNodes,
+                                                               int bandRows, out IntPtr ctx);
     [DllImport(Lib)] public static extern int svo_set_buffer(IntPtr ctx, int[] desc, UIntPtr nDesc,
                                                              uint[] att, UIntPtr nAtt, UIntPtr dstOffset);
     [DllImport(Lib)] public static extern int svo_set_camera(IntPtr ctx, float[] c2w, float[] invProj,
@@ -42,6 +44,7 @@ public class RaytracingMasterNative : MonoBehaviour {
     public Light DirectionalLight;
     [Range(1, 8)] public int maxLevel = 5;
     public SampleFunctions.Type sampleType = SampleFunctions.Type.Custom1;
+    [Range(1, 8)] public int gpus = 1;   // > 1: the frame is split in 8-row bands over GPUs 0..gpus-1
 
     IntPtr _ctx;
     Camera _camera;
@@ -64,7 +67,14 @@ public class RaytracingMasterNative : MonoBehaviour {
 
     // RaytracingMaster.cs:111-116
     public void InitializeSVOBuffer() {
-        SvoNative.Check(SvoNative.svo_create(0, (UIntPtr)(1073741824 / 8), out _ctx), "svo_create");
+        var capacity = (UIntPtr)(1073741824 / 8);
+        if (gpus <= 1) {
+            SvoNative.Check(SvoNative.svo_create(0, capacity, out _ctx), "svo_create");
+        } else {   // one SVO replica per GPU, bands gathered to GPU 0 over xGMI; every other call is unchanged
+            var devices = new int[gpus];
+            for (int i = 0; i < gpus; i++) devices[i] = i;
+            SvoNative.Check(SvoNative.svo_create_multi(devices, gpus, capacity, 8, out _ctx), "svo_create_multi");
+        }
     }
 
     // RaytracingMaster.cs:118-135 (attachments land at 2*offset: the reference's offset bug is fixed)
