@@ -611,6 +611,35 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
     return SVO_OK;
 }
 
+// Multi-device upload: the region [offset, offset + n) was validated and uploaded on
+// the display member; copy its nodes and attachments to every other member's pool
+// device to device (xGMI / SDMA, no second host validation walk or PCIe copy) and
+// commit the same upload record there.
+int replicate_upload(svo_ctx *g, size_t offset, size_t n) {
+    svo_ctx *m0 = g->members[0];
+    if (n == 0) return SVO_OK;
+    const Upload *u0 = nullptr;
+    for (const Upload &u : m0->uploads)
+        if (u.offset == offset) u0 = &u;
+    if (!u0) return fail(SVO_ERR_STATE, "replicate_upload: no upload record on the display member");
+    const Upload u = *u0;
+    for (size_t i = 1; i < g->members.size(); ++i) {
+        svo_ctx *m = g->members[i];
+        if (offset + n > m->capacity) return fail(SVO_ERR_CAPACITY, "upload exceeds a member's node-pool capacity");
+        HIP_TRY(hipSetDevice(m->device));
+        HIP_TRY(hipDeviceSynchronize());   // renders on the member may still read its pool
+        HIP_TRY(hipSetDevice(m0->device));
+        HIP_TRY(hipMemcpyPeerAsync(m->d_nodes + offset, m->device, m0->d_nodes + offset, m0->device,
+                                   n * sizeof(uint2), m0->stream));
+        HIP_TRY(hipMemcpyPeerAsync(m->d_att + offset, m->device, m0->d_att + offset, m0->device,
+                                   n * sizeof(uint2), m0->stream));
+    }
+    HIP_TRY(hipSetDevice(m0->device));
+    HIP_TRY(hipStreamSynchronize(m0->stream));
+    for (size_t i = 1; i < g->members.size(); ++i) commit_upload(g->members[i], u);
+    return SVO_OK;
+}
+
 int destroy_single(svo_ctx *ctx) {
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
@@ -746,12 +775,10 @@ int svo_get_member(svo_ctx *ctx, int index, svo_ctx **member) {
 int svo_set_buffer(svo_ctx *ctx, const int32_t *desc, size_t n_desc, const uint32_t *att,
                    size_t n_att, size_t dst_offset) {
     if (!ctx || (!desc && n_desc) || (!att && n_att)) return fail(SVO_ERR_ARG, "null argument");
-    if (is_multi(ctx)) {   // one replica per device
-        for (svo_ctx *m : ctx->members) {
-            int rc = svo_set_buffer(m, desc, n_desc, att, n_att, dst_offset);
-            if (rc) return rc;
-        }
-        return SVO_OK;
+    if (is_multi(ctx)) {   // validated and uploaded once, then replicated device to device
+        int rc = svo_set_buffer(ctx->members[0], desc, n_desc, att, n_att, dst_offset);
+        if (rc) return rc;
+        return replicate_upload(ctx, dst_offset, n_desc);
     }
     if (dst_offset + n_desc > ctx->capacity || 2 * dst_offset + n_att > 2 * ctx->capacity)
         return fail(SVO_ERR_CAPACITY, "upload exceeds node-pool capacity");
@@ -794,11 +821,9 @@ int svo_set_buffer_v2(svo_ctx *ctx, const uint64_t *nodes, size_t n_nodes, const
                       size_t n_att, size_t dst_offset) {
     if (!ctx || (!nodes && n_nodes) || (!att && n_att)) return fail(SVO_ERR_ARG, "null argument");
     if (is_multi(ctx)) {
-        for (svo_ctx *m : ctx->members) {
-            int rc = svo_set_buffer_v2(m, nodes, n_nodes, att, n_att, dst_offset);
-            if (rc) return rc;
-        }
-        return SVO_OK;
+        int rc = svo_set_buffer_v2(ctx->members[0], nodes, n_nodes, att, n_att, dst_offset);
+        if (rc) return rc;
+        return replicate_upload(ctx, dst_offset, n_nodes);
     }
     if (dst_offset + n_nodes > ctx->capacity) return fail(SVO_ERR_CAPACITY, "upload exceeds node-pool capacity");
     if (n_att != 2 * n_nodes) return fail(SVO_ERR_ARG, "attachments must hold 2 words per node");

@@ -434,13 +434,16 @@ def test_three_linked_pools(torch, oracle_mod):
     assert np.count_nonzero(ref["flags"] & 1) > 100
 
 
-def test_clipmap_linked_sub_svo_trunk_first(torch, oracle_mod):
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_clipmap_linked_sub_svo_trunk_first(torch, oracle_mod, devices):
     """Clipmap.UpdateMasterOctree (Clipmap.cs:153-169): a trunk built with every
     leaf linked to descriptor 10000 (NaiveCreator.Create(root, x => 10000),
     NaiveCreator.cs:156-159; builder.link_leaves) is uploaded FIRST, then the
     sub-SVO at offset 10000 (SetSVOBuffer(data, 10000)).  Between the two uploads
     the links read the zero-filled pool (empty descriptors); after the second,
-    the frame equals the oracle's over the combined pool, both stack modes."""
+    the frame equals the oracle's over the combined pool, both stack modes.  With
+    a multi-device context each upload is validated once and replicated to the
+    other members device to device."""
     from raytracingtest_amd.builder import link_leaves
     from raytracingtest_amd.native_builder import build_sampler_svo
     base = 10000
@@ -463,7 +466,7 @@ def test_clipmap_linked_sub_svo_trunk_first(torch, oracle_mod):
     w, h = 320, 200
     c2w, inv_proj = cam.uniforms(w, h)
     ocam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
-    m = RaytracingMaster(device=0, capacity_nodes=len(full))
+    m = RaytracingMaster(device=0, capacity_nodes=len(full), devices=devices)
     try:
         m.SetSVOBuffer(trunk)
         m.UpdateShaderParameters(cam, w, h)
