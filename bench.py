@@ -617,6 +617,29 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
         for d in sorted(set(args.device_list)):
             torch.cuda.synchronize(d)
 
+    # the display device also assembles: the same calibrated weighted deal as the ranks
+    deal = None
+    share = args.display_share
+    for _ in range(max(1, args.warmup)):
+        step()
+    sync_all()
+    if share is None:
+        rm.set_kernel_timing(True)
+        rm.stage_time(1)
+        for i in range(n):
+            rm.member(i).kernel_time()
+        for _ in range(5):
+            step()
+        sync_all()
+        kern = max(rm.member(i).kernel_time()[0] for i in range(n))
+        asm = rm.stage_time(1)[0]
+        rm.set_kernel_timing(False)
+        share = max(0.0, 1.0 - (asm + 0.003) / kern)
+    from raytracingtest_amd import distributed as D
+    owner = D.weighted_owner(n, max(share, 1.0 / 8.0))
+    if owner.count(0) < 8:
+        rm.set_band_deal(owner)
+        deal = {"display_share": owner.count(0) / 8, "cycle_bands": len(owner)}
     for _ in range(max(1, args.warmup)):
         step()
     sync_all()
@@ -643,7 +666,7 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
         "config": {"workload": f"{args.config} {W}x{H} primary rays, {args.camera} camera, display RGBA8 frame",
                    "parallelism": f"multidevice{n}x8rows+xgmi_pull", "build_s": round(build_s, 2)},
         "multi_gpu": {"devices": args.device_list, "per_device_kernel_ms": [round(k, 4) for k in kern],
-                      "assemble_ms": round(asm_ms, 4)},
+                      "assemble_ms": round(asm_ms, 4), "display_device_deal": deal},
     }), flush=True)
 
 

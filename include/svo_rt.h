@@ -107,6 +107,10 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out);
  * dispatches one grid over the whole frame (RaytracingMaster.cs:66-68). */
 int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes, int band_rows, svo_ctx **out);
 int svo_num_devices(svo_ctx *ctx, int *num_devices);
+/* Weighted band deal for a multi-device context (svo_band.cycle / owner): band b
+ * goes to member owner[b % cycle]; e.g. fewer bands for devices[0], which also
+ * assembles the frame.  cycle 0 = round-robin (the default). */
+int svo_set_band_deal(svo_ctx *ctx, int cycle, const uint8_t *owner);
 /* The per-device context `index` of a multi-device context (the context itself
  * for index 0 of a single-device one): owned by the group, not destroyed alone. */
 int svo_get_member(svo_ctx *ctx, int index, svo_ctx **member);

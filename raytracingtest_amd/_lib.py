@@ -33,7 +33,7 @@ EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera"
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
            "svo_destroy", "svo_last_error", "svo_abi_version", "svo_set_options", "svo_accumulate",
            "svo_kernel_time", "svo_create_multi", "svo_num_devices", "svo_get_member", "svo_render_frame",
-           "svo_assemble_frame", "svo_stage_time", "svo_render_progressive")
+           "svo_assemble_frame", "svo_stage_time", "svo_render_progressive", "svo_set_band_deal")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
@@ -110,6 +110,7 @@ def lib():
                                ctypes.POINTER(SvoFrame), vp],
         "svo_stage_time": [vp, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)],
         "svo_render_progressive": [vp, i, i, i, ctypes.c_uint32, vp, vp],
+        "svo_set_band_deal": [vp, i, ctypes.POINTER(ctypes.c_uint8)],
         "svo_synchronize": [vp],
         "svo_destroy": [vp],
         "svo_last_error": [],

@@ -133,6 +133,8 @@ struct svo_ctx {
     bool gathered_used[2] = {false, false};
     int parity = 0;
     int band_rows = 8;
+    int deal_cycle = 0;                  // svo_set_band_deal: weighted deal over the members (0: round-robin)
+    uint8_t deal_owner[svo::MAX_CYCLE] = {};
 };
 
 namespace {
@@ -562,14 +564,14 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
     svo_ctx *m0 = ctx->members[0];
     hipStream_t s0 = stream ? stream : m0->stream;
     // the display device renders its own bands straight into the caller's frame
-    svo_band b0{ctx->band_rows, 0, n, 0, nullptr};
+    svo_band b0{ctx->band_rows, 0, n, ctx->deal_cycle, ctx->deal_cycle ? ctx->deal_owner : nullptr};
     int rc = launch(m0, width, height, stack_mode, &b0, out, s0);
     if (rc) return rc;
     std::vector<const void *> parts(n, nullptr);
     for (int i = 1; i < n; ++i) {
         svo_ctx *m = ctx->members[i];
         Peer &pr = ctx->peers[i];
-        svo_band bi{ctx->band_rows, i, n, 0, nullptr};
+        svo_band bi{ctx->band_rows, i, n, ctx->deal_cycle, ctx->deal_cycle ? ctx->deal_owner : nullptr};
         Deal di;
         rc = check_band(&bi, height, &di);
         if (rc) return rc;
@@ -755,6 +757,24 @@ int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes,
         if (hipEventCreateWithFlags(&g->gathered[j], hipEventDisableTiming) != hipSuccess)
             return bail(fail(SVO_ERR_HIP, "hipEventCreate"));
     *out = g;
+    return SVO_OK;
+}
+
+int svo_set_band_deal(svo_ctx *ctx, int cycle, const uint8_t *owner) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (!is_multi(ctx)) return fail(SVO_ERR_ARG, "svo_set_band_deal needs a multi-device context");
+    if (cycle < 0 || cycle > svo::MAX_CYCLE) return fail(SVO_ERR_ARG, "cycle must be in [0, 256]");
+    if (cycle > 0 && !owner) return fail(SVO_ERR_ARG, "owner is null");
+    const int n = (int)ctx->members.size();
+    for (int i = 0; i < cycle; ++i)
+        if (owner[i] >= n) return fail(SVO_ERR_ARG, "owner entry names no member");
+    // payload sizes change: let frames in flight finish with the old deal first
+    for (svo_ctx *m : ctx->members) {
+        HIP_TRY(hipSetDevice(m->device));
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    ctx->deal_cycle = cycle;
+    for (int i = 0; i < cycle; ++i) ctx->deal_owner[i] = owner[i];
     return SVO_OK;
 }
 

@@ -138,6 +138,14 @@ class RaytracingMaster:
         check(_lib.lib().svo_stage_time(self._ctx, int(stage), ctypes.byref(ms), ctypes.byref(n)), "svo_stage_time")
         return ms.value, n.value
 
+    def set_band_deal(self, owner=None):
+        """Multi-device context: deal band b to member owner[b % len(owner)]
+        (distributed.weighted_owner gives fewer bands to devices[0]); None =
+        round-robin."""
+        n = 0 if owner is None else len(owner)
+        arr = (ctypes.c_uint8 * max(n, 1))(*([int(o) for o in owner] if owner else [0]))
+        check(_lib.lib().svo_set_band_deal(self._ctx, n, arr if n else None), "svo_set_band_deal")
+
     def num_devices(self):
         n = ctypes.c_int()
         check(_lib.lib().svo_num_devices(self._ctx, ctypes.byref(n)), "svo_num_devices")

@@ -77,6 +77,7 @@ def test_multi_device_and_frame_entry_points_reject_bad_arguments_without_gpu(na
     assert native.svo_render_frame(None, 8, 8, 0, None, ctypes.byref(SvoFrame()), None) == -1
     assert native.svo_assemble_frame(None, 8, 8, None, 1, None, 0, -1, None, None) == -1
     assert native.svo_stage_time(None, 0, None, None) == -1
+    assert native.svo_set_band_deal(None, 0, None) == -1
     n = ctypes.c_int()
     assert native.svo_num_devices(None, ctypes.byref(n)) == -1
 

@@ -189,6 +189,35 @@ def test_multi_device_context_matches_oracle(torch, oracle_mod, text_svo, device
         m.close()
 
 
+def test_multi_device_weighted_deal(torch, oracle_mod):
+    """svo_set_band_deal: a three-member context whose display member takes 3 of
+    every 8 rounds' bands (it also assembles) renders the same frame as the
+    oracle, for the compact (hit records + Result) and RGBA8 payloads, and a
+    bad owner table is refused."""
+    from raytracingtest_amd.distributed import weighted_owner
+    svo = build_menger(8)
+    w, h = 300, 250
+    cam = overview_camera()
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+    m = RaytracingMaster(devices=[0, 0, 0], capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        for owner in (weighted_owner(3, 3 / 8), None, weighted_owner(3, 1 / 8)):
+            m.set_band_deal(owner)
+            rgba, hits = m.Render(w, h)
+            assert hits.tobytes() == ref_hits.tobytes()
+            assert rgba.reshape(-1, 4).tobytes() == ref_rgba.tobytes()
+            b = _bufs(torch, w * h)
+            m.render_frame(w, h, rgba8=b["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME)
+            m.synchronize()
+            _check(b, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+        with pytest.raises(SvoError):
+            m.set_band_deal([0, 1, 3])
+    finally:
+        m.close()
+
+
 def test_multi_device_shadow_rays(torch, oracle_mod):
     """The C3 '+1 shadow ray' frame through the multi-device context: the
     occlusion flag travels in the compact record and the display member
