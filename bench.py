@@ -83,6 +83,8 @@ def parse():
     p.add_argument("--devices", default=None,
                    help="one-process multi-device mode: comma-separated HIP device indices of the context's members "
                         "(default 0..N-1; an index may repeat to rehearse the split on one GPU)")
+    p.add_argument("--replica", choices=["broadcast", "build"], default="broadcast",
+                   help="N ranks: the SVO built on rank 0 and broadcast over RCCL (default), or built on every rank")
     p.add_argument("--display-share", type=float, default=None,
                    help="N > 1: the display rank's share of a normal rank's bands (default: calibrated from its "
                         "assemble time; 1 = round-robin)")
@@ -175,12 +177,18 @@ def main():
     if world > 1 and scaling == "weak":
         W, H = D.weak_frame(W, H, world)
     t0 = time.time()
-    if args.svo == "menger":   # 256^3 Menger sponge surface voxels
-        from raytracingtest_amd.builder import build_menger
-        svo = build_menger(depth=args.max_level - 1)
-    else:
-        svo = build_sampler_svo(args.sampler, args.max_level, device=dev.index)
+    svo = None
+    if mode != "ranks" or args.replica == "build" or rank == 0:
+        if args.svo == "menger":   # 256^3 Menger sponge surface voxels
+            from raytracingtest_amd.builder import build_menger
+            svo = build_menger(depth=args.max_level - 1)
+        else:
+            svo = build_sampler_svo(args.sampler, args.max_level, device=dev.index)
     build_s = time.time() - t0
+    if mode == "ranks" and args.replica == "broadcast":
+        # the SVO replicated per GPU from rank 0 over RCCL; each rank's
+        # plugin validates and uploads its copy
+        svo = D.broadcast_svo(svo, 0, device=dev)
     n_nodes = len(svo)
     cam = CAMERAS[args.camera]()
 
@@ -346,6 +354,8 @@ def main():
             "config": {"workload": workload,
                        "svo_nodes": n_nodes, "svo_format": "V%d" % svo.format, "svo_leaves": getattr(svo, "n_leaves", None),
                        "build_s": round(build_s, 2), "stack_mode": "hlsl" if args.stack_mode == 0 else "exact",
+                       "svo_replica": None if world == 1 else ("rccl_broadcast_from_rank0" if args.replica == "broadcast"
+                                                               else "built_on_every_rank"),
                        "rays_per_step": rays_per_step, "rays_per_gpu_step": n_px,
                        "hit_fraction_rank0": round(n_hit / n_px, 4),
                        "fetches_per_ray_rank0": round(F / n_px, 3), "parallelism": par},

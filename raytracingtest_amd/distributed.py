@@ -125,6 +125,46 @@ def gather_to_root(send, parts, root=0, dist=None, group=None):
         dev_buf.copy_(host)
 
 
+def broadcast_svo(svo, src=0, dist=None, device=None):
+    """Replicate a node pool from rank `src` to every rank (the
+    SVO replicated per GPU, broadcast from rank 0 over xGMI).  `svo` is the
+    SVOData on `src` (ignored elsewhere); the arrays travel as device tensors in
+    one RCCL broadcast each, and every rank gets an SVOData with identical
+    bytes (which its plugin then validates and uploads).  On gloo (CPU tests,
+    one-GPU rehearsal) host tensors are broadcast."""
+    import torch
+    from .svo_data import SVOData
+    if dist is None:
+        import torch.distributed as dist
+    rank = dist.get_rank()
+    on_dev = device is not None and dist.get_backend() != "gloo"
+    dev = device if on_dev else "cpu"
+    head = torch.zeros(4, dtype=torch.int64, device=dev)
+    if rank == src:
+        words = svo.childDescriptors if svo.format == 1 else svo.nodes
+        head[:] = torch.tensor([svo.format, len(words), len(svo.attachments), getattr(svo, "n_leaves", -1) or -1])
+    dist.broadcast(head, src)
+    fmt, n, n_att, n_leaves = (int(v) for v in head.tolist())
+    if rank == src:
+        words = svo.childDescriptors if svo.format == 1 else svo.nodes
+        w = torch.from_numpy(np.ascontiguousarray(words).view(np.int32 if fmt == 1 else np.int64)).to(dev)
+        a = torch.from_numpy(np.ascontiguousarray(svo.attachments).view(np.int32)).to(dev)
+    else:
+        w = torch.empty(n, dtype=torch.int32 if fmt == 1 else torch.int64, device=dev)
+        a = torch.empty(n_att, dtype=torch.int32, device=dev)
+    dist.broadcast(w, src)
+    dist.broadcast(a, src)
+    if rank == src:
+        return svo
+    words = w.cpu().numpy()
+    att = a.cpu().numpy().view(np.uint32)
+    out = (SVOData(childDescriptors=words.view(np.int32), attachments=att) if fmt == 1 else
+           SVOData(nodes=words.view(np.uint64), attachments=att))
+    if n_leaves >= 0:
+        out.n_leaves = n_leaves
+    return out
+
+
 def gather_bands(local, height, width, world, rank, elem_bytes, rows=DEFAULT_BAND_ROWS, dist=None):
     """Gather every rank's band buffer (uint8 tensor of band_len * width *
     elem_bytes bytes) to rank 0; returns the per-rank byte tensors trimmed to

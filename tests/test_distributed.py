@@ -150,3 +150,38 @@ def test_weighted_deal_covers_frame_and_balances():
             if H >= 1080 and share > 0:
                 assert abs(lens[0] / lens[1] - round(share * 8) / 8) < 0.15
     assert weighted_owner(3, 1.0) == [0, 1, 2] * 8
+
+
+def _bcast_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from raytracingtest_amd import SVOData
+    from raytracingtest_amd import distributed as D
+    from raytracingtest_amd.builder import build_menger
+    z = np.load(os.path.join(GOLDEN, "text_svo.npz"))
+    v1 = SVOData.from_absolute(z["abs_child_ptr"], z["valid_mask"], z["nonleaf_mask"], z["normal_code"])
+    v2 = build_menger(5)
+    for name, src in (("v1", v1), ("v2", v2)):
+        got = D.broadcast_svo(src if rank == 0 else None, 0)
+        assert got.format == src.format and len(got) == len(src)
+        words = got.childDescriptors if got.format == 1 else got.nodes
+        ref = src.childDescriptors if src.format == 1 else src.nodes
+        np.save(os.path.join(out_dir, f"{name}_{rank}.npy"),
+                np.concatenate([np.frombuffer(words.tobytes(), np.uint8), np.frombuffer(got.attachments.tobytes(), np.uint8)]))
+        assert words.tobytes() == ref.tobytes() and got.attachments.tobytes() == src.attachments.tobytes()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_svo_broadcast_replicas_identical(tmp_path):
+    """bench.py's default replica: rank 0's node pool and
+    attachments broadcast to every rank arrive byte-identical, V1 and V2."""
+    world = 3
+    mp.spawn(_bcast_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for name in ("v1", "v2"):
+        blobs = [np.load(tmp_path / f"{name}_{r}.npy").tobytes() for r in range(world)]
+        assert blobs[1] == blobs[0] and blobs[2] == blobs[0]
