@@ -315,6 +315,7 @@ def main():
                   "note": "primary pass + one shadow ray per primary hit (RaytraceCompute.compute:105-112), "
                           "whole step on the host clock between synchronizes, like value"}
     host_path = host_path_rates(rm, W, H, args) if world == 1 and args.steps > 0 else None
+    in_flight = frames_in_flight(rm, W, H, args, dev) if world == 1 and args.steps > 0 else None
     poses = None
     if world == 1 and args.extra_poses and args.svo != "menger":
         poses = extra_poses(rm, args, W, H, hits, rgba, sptr, dev)
@@ -397,6 +398,8 @@ def main():
             out["extra_poses"] = poses
         if host_path:
             out["host_path"] = host_path
+        if in_flight:
+            out["frames_in_flight"] = in_flight
         print(json.dumps(out), flush=True)
     rm.close()
     if world > 1:
@@ -678,6 +681,35 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
         "multi_gpu": {"devices": args.device_list, "per_device_kernel_ms": [round(k, 4) for k in kern],
                       "assemble_ms": round(asm_ms, 4), "display_device_deal": deal},
     }), flush=True)
+
+
+def frames_in_flight(rm, W, H, args, dev, n_streams=3):
+    """Throughput with consecutive frames on rotating streams (own output
+    buffers each; the plugin keeps per-stream dispatch-order state, so their
+    renders overlap and the next frame's waves fill one frame's ramp-down;
+    3 streams: 2 sometimes share a hardware queue, tools/overlap_experiment.py).
+    Reported beside `value`, which -- like the roofline's kernel time -- is
+    measured with one frame at a time."""
+    import torch
+    streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
+    outs = [(torch.empty(W * H * 24, dtype=torch.uint8, device=dev),
+             None if args.no_rgba else torch.empty(W * H * 4, dtype=torch.float32, device=dev))
+            for _ in range(n_streams)]
+
+    def step(i):
+        h, c = outs[i % n_streams]
+        rm.render_device(W, H, rgba_ptr=None if c is None else c.data_ptr(), hits_ptr=h.data_ptr(),
+                         stack_mode=args.stack_mode, stream=streams[i % n_streams].cuda_stream)
+
+    for i in range(2 * n_streams + 4):
+        step(i)
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t) / args.steps * 1e3
+    return {"streams": n_streams, "ms_per_frame": round(ms, 4), "Mrays_per_s": round(W * H / (ms * 1e-3) / 1e6, 2)}
 
 
 def host_path_rates(rm, W, H, args, n=5):

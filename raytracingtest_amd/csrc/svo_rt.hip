@@ -61,6 +61,27 @@ struct Upload {
 
 enum { STAGE_KERNEL = 0, STAGE_ASSEMBLE = 1, N_STAGES = 2 };
 
+// Cost-ordered dispatch state of the renders on one stream: every launch records each
+// 8x8 tile's trip count; the order kernel, enqueued right behind it, turns them into
+// the heaviest-first dispatch order of the next launch at the same geometry.  One set
+// per stream (up to MAX_SCHED streams), so renders on different streams -- frames in
+// flight -- share nothing mutable and run concurrently.
+constexpr int MAX_SCHED = 4;
+struct Sched {
+    hipStream_t stream = nullptr;
+    bool used = false;
+    unsigned long long last_use = 0;
+    hipEvent_t done = nullptr;       // recorded behind this stream's last render (eviction)
+    uint16_t *tile_cost = nullptr;
+    uint32_t *tile_order = nullptr;
+    uint16_t *shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
+    uint32_t *shadow_order = nullptr;
+    size_t cap = 0;
+    long long order_key = -1;        // geometry tile_order was built for (-1: none)
+    long long shadow_key = -1;
+    unsigned long long launches = 0, shadow_launches = 0;
+};
+
 struct Peer {                       // one per member of a multi-device context (index 0: the display device)
     void *buf[2] = {nullptr, nullptr};   // band payload, double-buffered across frames
     size_t cap_bytes = 0;
@@ -100,31 +121,20 @@ struct svo_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timing_free;               // reusable
     uint32_t *d_wave_log = nullptr;  // diagnostics: env SVO_WAVE_LOG=<file>
     size_t wave_log_cap = 0;
-    // Cost-ordered tile dispatch: every launch records each 8x8 tile's trip
-    // count; the order kernel, enqueued right behind it, turns them into the
-    // heaviest-first dispatch order of the next launch at the same geometry.
+    // cost-ordered tile dispatch (svo_rt.hip Sched): switches and per-stream state
     int tile_order = 1;              // env SVO_TILE_ORDER=0 disables
     int prio = 1;                    // env SVO_PRIO=0: no issue priority by cost class
     int shadow_order_enabled = 1;    // env SVO_SHADOW_ORDER=0: shadow tiles in plain strip order
     int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
     int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
     int order_every = 8;             // env SVO_ORDER_EVERY: rebuild the order every k-th launch
-    unsigned long long order_launches = 0;
-    uint16_t *d_tile_cost = nullptr;
-    uint32_t *d_tile_order = nullptr;
-    uint16_t *d_shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
-    uint32_t *d_shadow_order = nullptr;
-    long long shadow_order_key = -1;
-    unsigned long long shadow_launches = 0;
-    size_t tile_cap = 0;
-    long long order_key = -1;        // geometry d_tile_order was built for (-1: none)
-    // Renders of one context are ordered across streams: the cost / order buffers
-    // and the scratch outputs are shared by all its render launches, so the first
-    // render on a new stream waits for everything enqueued on the previous one (an
-    // event recorded at the switch; no host sync).  Assembles and accumulations
-    // touch no context state and are not ordered; uploads synchronise the device.
-    hipStream_t last_stream = nullptr;
-    bool last_valid = false;
+    Sched sched[MAX_SCHED];
+    unsigned long long sched_clock = 0;
+    // The one piece of state renders on different streams still share: the host-path /
+    // two-pass-shadow scratch outputs.  A render that uses them waits for the previous
+    // such render's stream (an event recorded at the switch; no host sync).
+    hipStream_t scratch_stream = nullptr;
+    bool scratch_valid = false;
     hipEvent_t switch_event = nullptr;
     // multi-device context (svo_create_multi); empty for a single-device one
     std::vector<svo_ctx *> members;
@@ -154,19 +164,58 @@ __global__ void convert_v1_kernel(const int32_t *__restrict__ desc, uint2 *__res
     nodes[base + i] = o;
 }
 
-// Make stream s wait for all work this context enqueued on another stream.
-int order_streams(svo_ctx *ctx, hipStream_t s) {
-    if (ctx->last_valid && ctx->last_stream != s) {
+// Make stream s wait for the work the previous scratch user enqueued on another stream.
+int order_scratch(svo_ctx *ctx, hipStream_t s) {
+    if (ctx->scratch_valid && ctx->scratch_stream != s) {
         if (!ctx->switch_event) HIP_TRY(hipEventCreateWithFlags(&ctx->switch_event, hipEventDisableTiming));
-        if (hipEventRecord(ctx->switch_event, ctx->last_stream) == hipSuccess) {
+        if (hipEventRecord(ctx->switch_event, ctx->scratch_stream) == hipSuccess) {
             HIP_TRY(hipStreamWaitEvent(s, ctx->switch_event, 0));
         } else {   // the previous stream is gone: wait for the whole device instead
             (void)hipGetLastError();
             HIP_TRY(hipDeviceSynchronize());
         }
     }
-    ctx->last_stream = s;
-    ctx->last_valid = true;
+    ctx->scratch_stream = s;
+    ctx->scratch_valid = true;
+    return SVO_OK;
+}
+
+void free_sched(Sched &q) {
+    if (q.tile_cost) hipFree(q.tile_cost);
+    if (q.tile_order) hipFree(q.tile_order);
+    if (q.shadow_cost) hipFree(q.shadow_cost);
+    if (q.shadow_order) hipFree(q.shadow_order);
+    q.tile_cost = nullptr;
+    q.tile_order = nullptr;
+    q.shadow_cost = nullptr;
+    q.shadow_order = nullptr;
+    q.cap = 0;
+    q.order_key = q.shadow_key = -1;
+}
+
+// The scheduling state of stream s: its own set, or a free one, or the least recently
+// used one -- taken over only after the stream that used it has finished its renders.
+int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
+    Sched *pick = nullptr;
+    for (Sched &q : ctx->sched)
+        if (q.used && q.stream == s) pick = &q;
+    if (!pick) {
+        for (Sched &q : ctx->sched)
+            if (!q.used) { pick = &q; break; }
+    }
+    if (!pick) {
+        pick = &ctx->sched[0];
+        for (Sched &q : ctx->sched)
+            if (q.last_use < pick->last_use) pick = &q;
+        if (pick->done) HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
+        pick->order_key = pick->shadow_key = -1;   // built for another stream's frames
+        pick->launches = pick->shadow_launches = 0;
+    }
+    if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
+    pick->stream = s;
+    pick->used = true;
+    pick->last_use = ++ctx->sched_clock;
+    *out = pick;
     return SVO_OK;
 }
 
@@ -408,10 +457,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     if (p.local_rows == 0) return SVO_OK;
     if (out.fetches) p.shadows = 0;
     hipStream_t s = stream ? stream : ctx->stream;
-    rc = order_streams(ctx, s);
-    if (rc) return rc;
     if (p.shadows == 1 && !p.out.hits && !p.out.compact) {   // the second shadow pass reads the primary records
         int rc2 = ensure_out(ctx, (size_t)(p.out.frame_layout ? height : p.local_rows) * (size_t)width);
+        if (rc2) return rc2;
+        rc2 = order_scratch(ctx, s);
         if (rc2) return rc2;
         p.out.hits = reinterpret_cast<svo::Hit *>(ctx->d_out_hits);
     }
@@ -419,37 +468,30 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     const bool ordered = ctx->tile_order && !p.out.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
     long long key = -1;
+    Sched *q = nullptr;
     if (ordered) {
+        rc = sched_for(ctx, s, &q);
+        if (rc) return rc;
         key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^ ((long long)b.rows << 8) ^
               (long long)b.rank ^ ((long long)b.count << 4) ^ ((long long)p.xcd_remap << 60) ^ (long long)(b.key() << 1);
         if (key < 0) key = ~key;   // -1 means "no order"
-        if (ctx->tile_cap < (size_t)n_tiles) {
-            HIP_TRY(hipDeviceSynchronize());   // a pending launch may still use the old buffers
-            if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
-            if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
-            if (ctx->d_shadow_cost) hipFree(ctx->d_shadow_cost);
-            if (ctx->d_shadow_order) hipFree(ctx->d_shadow_order);
-            ctx->d_tile_cost = nullptr;
-            ctx->d_tile_order = nullptr;
-            ctx->d_shadow_cost = nullptr;
-            ctx->d_shadow_order = nullptr;
-            ctx->tile_cap = 0;
-            ctx->order_key = -1;
-            ctx->shadow_order_key = -1;
+        if (q->cap < (size_t)n_tiles) {
+            HIP_TRY(hipStreamSynchronize(s));   // a pending launch on this stream may still use the old buffers
+            free_sched(*q);
             const size_t cap = svo::order_cost_capacity(n_tiles);
-            HIP_TRY(hipMalloc(&ctx->d_tile_cost, cap * sizeof(uint16_t)));
-            HIP_TRY(hipMemset(ctx->d_tile_cost, 0, cap * sizeof(uint16_t)));
-            HIP_TRY(hipMalloc(&ctx->d_tile_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
-            HIP_TRY(hipMalloc(&ctx->d_shadow_cost, cap * sizeof(uint16_t)));
-            HIP_TRY(hipMemset(ctx->d_shadow_cost, 0, cap * sizeof(uint16_t)));
-            HIP_TRY(hipMalloc(&ctx->d_shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
-            ctx->tile_cap = (size_t)n_tiles;
+            HIP_TRY(hipMalloc(&q->tile_cost, cap * sizeof(uint16_t)));
+            HIP_TRY(hipMemset(q->tile_cost, 0, cap * sizeof(uint16_t)));
+            HIP_TRY(hipMalloc(&q->tile_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&q->shadow_cost, cap * sizeof(uint16_t)));
+            HIP_TRY(hipMemset(q->shadow_cost, 0, cap * sizeof(uint16_t)));
+            HIP_TRY(hipMalloc(&q->shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
+            q->cap = (size_t)n_tiles;
         }
-        p.tile_order = ctx->order_key == key ? ctx->d_tile_order : nullptr;
-        p.tile_cost = ctx->d_tile_cost;
+        p.tile_order = q->order_key == key ? q->tile_order : nullptr;
+        p.tile_cost = q->tile_cost;
         if (p.shadows == 1 && ctx->shadow_order_enabled) {
-            p.shadow_cost = ctx->d_shadow_cost;
-            p.shadow_order = ctx->shadow_order_key == key ? ctx->d_shadow_order : nullptr;
+            p.shadow_cost = q->shadow_cost;
+            p.shadow_order = q->shadow_key == key ? q->shadow_order : nullptr;
         }
     }
     const char *log_path = std::getenv("SVO_WAVE_LOG");
@@ -473,19 +515,20 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     }
     hipError_t e = svo::launch_render(p, stack_mode, s, ev0, ev1);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
-    const bool refresh = p.tile_cost && (ctx->order_key != key || ctx->order_launches++ % ctx->order_every == 0);
+    const bool refresh = q && p.tile_cost && (q->order_key != key || q->launches++ % ctx->order_every == 0);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
-        e = p.xcd_remap == 2 ? svo::launch_order_strips(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, (width + 7) / 8, s)
-                             : svo::launch_order_tiles(ctx->d_tile_cost, ctx->d_tile_order, n_tiles, s);
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s)
+                             : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
-        ctx->order_key = key;
+        q->order_key = key;
     }
-    if (p.shadow_cost && (ctx->shadow_order_key != key || ctx->shadow_launches++ % ctx->order_every == 0)) {
-        e = p.xcd_remap == 2 ? svo::launch_order_strips(ctx->d_shadow_cost, ctx->d_shadow_order, n_tiles, (width + 7) / 8, s)
-                             : svo::launch_order_tiles(ctx->d_shadow_cost, ctx->d_shadow_order, n_tiles, s);
+    if (q && p.shadow_cost && (q->shadow_key != key || q->shadow_launches++ % ctx->order_every == 0)) {
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(q->shadow_cost, q->shadow_order, n_tiles, (width + 7) / 8, s)
+                             : svo::launch_order_tiles(q->shadow_cost, q->shadow_order, n_tiles, s);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("shadow order launch: ") + hipGetErrorString(e));
-        ctx->shadow_order_key = key;
+        q->shadow_key = key;
     }
+    if (q) HIP_TRY(hipEventRecord(q->done, s));
     if (p.wave_log) {   // blocking dump of the last launch's per-wave record
         HIP_TRY(hipStreamSynchronize(s));
         std::vector<uint32_t> h(n_wave * 8);
@@ -601,8 +644,6 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
     }
     HIP_TRY(hipSetDevice(m0->device));
     for (int i = 1; i < n; ++i) HIP_TRY(hipStreamWaitEvent(s0, ctx->peers[i].rendered[k], 0));
-    rc = order_streams(m0, s0);
-    if (rc) return rc;
     Deal deal;
     rc = check_band(&b0, height, &deal);
     if (rc) return rc;
@@ -645,7 +686,7 @@ int replicate_upload(svo_ctx *g, size_t offset, size_t n) {
 int destroy_single(svo_ctx *ctx) {
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    if (ctx->last_valid && ctx->last_stream && ctx->last_stream != ctx->stream) hipDeviceSynchronize();
+    hipDeviceSynchronize();   // renders on caller streams may still use the context's buffers
     if (ctx->d_nodes) hipFree(ctx->d_nodes);
     if (ctx->d_att) hipFree(ctx->d_att);
     if (ctx->d_stage) hipFree(ctx->d_stage);
@@ -653,15 +694,15 @@ int destroy_single(svo_ctx *ctx) {
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
     if (ctx->d_accum) hipFree(ctx->d_accum);
     if (ctx->d_accum8) hipFree(ctx->d_accum8);
-    if (ctx->d_shadow_cost) hipFree(ctx->d_shadow_cost);
-    if (ctx->d_shadow_order) hipFree(ctx->d_shadow_order);
+    for (Sched &q : ctx->sched) {
+        free_sched(q);
+        if (q.done) hipEventDestroy(q.done);
+    }
     for (auto &v : ctx->timing_events)
         for (auto &ev : v) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     for (auto &ev : ctx->timing_free) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     if (ctx->switch_event) hipEventDestroy(ctx->switch_event);
     if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
-    if (ctx->d_tile_cost) hipFree(ctx->d_tile_cost);
-    if (ctx->d_tile_order) hipFree(ctx->d_tile_order);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return SVO_OK;
@@ -926,6 +967,8 @@ int svo_render(svo_ctx *ctx, int width, int height, int stack_mode, float *rgba_
     HIP_TRY(hipSetDevice(c->device));
     int rc = ensure_out(c, px);
     if (rc) return rc;
+    rc = order_scratch(c, c->stream);
+    if (rc) return rc;
     svo_frame f{};
     f.hits = hits_out ? reinterpret_cast<svo_hit *>(c->d_out_hits) : nullptr;
     f.rgba = rgba_out ? reinterpret_cast<float *>(c->d_out_rgba) : nullptr;
@@ -958,6 +1001,8 @@ int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, 
     if (rc) return rc;
     rc = ensure_accum(c, width, height);
     if (rc) return rc;
+    rc = order_scratch(c, c->stream);
+    if (rc) return rc;
     svo_frame f{};
     f.rgba = reinterpret_cast<float *>(c->d_out_rgba);   // this sample's Result
     f.layout = SVO_LAYOUT_FRAME;
@@ -965,8 +1010,6 @@ int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, 
                        : launch(c, width, height, stack_mode, nullptr, outputs_of(&f), c->stream);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    rc = order_streams(c, c->stream);
-    if (rc) return rc;
     hipError_t e = svo::launch_accumulate(c->d_accum, reinterpret_cast<const float4 *>(c->d_out_rgba), px, sample,
                                           c->num_cus, c->stream);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("accumulate launch: ") + hipGetErrorString(e));
@@ -1072,8 +1115,7 @@ int svo_synchronize(svo_ctx *ctx) {
         return SVO_OK;
     }
     HIP_TRY(hipSetDevice(ctx->device));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    if (ctx->last_valid && ctx->last_stream != ctx->stream) HIP_TRY(hipStreamSynchronize(ctx->last_stream));
+    HIP_TRY(hipDeviceSynchronize());   // the context's stream and every caller stream it rendered on
     return SVO_OK;
 }
 

@@ -320,10 +320,13 @@ def test_weighted_deal_parts_match_oracle(torch, oracle_mod, world, share):
         m.close()
 
 
-def test_two_streams_every_pixel_written(torch, oracle_mod):
-    """Launches of one context alternating between two streams (advisor r1): the
-    shared dispatch-order buffers are rebuilt every launch (SVO_ORDER_EVERY=1)
-    and every frame is still complete and equal to the oracle's."""
+@pytest.mark.parametrize("n_streams", [2, 6])
+def test_two_streams_every_pixel_written(torch, oracle_mod, n_streams):
+    """Launches of one context cycling over several streams (advisor r1): each
+    stream has its own dispatch-order state (up to 4; a fifth stream takes over
+    the least recently used set after that stream's renders), the orders are
+    rebuilt every launch (SVO_ORDER_EVERY=1), the renders run concurrently, and
+    every frame is still complete and equal to the oracle's."""
     import os
     os.environ["SVO_ORDER_EVERY"] = "1"
     try:
@@ -337,11 +340,11 @@ def test_two_streams_every_pixel_written(torch, oracle_mod):
     try:
         m.SetSVOBuffer(svo)
         m.UpdateShaderParameters(cam, w, h)
-        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-        outs = [_bufs(torch, w * h) for _ in range(6)]
+        streams = [torch.cuda.Stream() for _ in range(n_streams)]
+        outs = [_bufs(torch, w * h) for _ in range(3 * n_streams)]
         for i, b in enumerate(outs):
             m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(),
-                           stream=streams[i % 2].cuda_stream)
+                           stream=streams[i % n_streams].cuda_stream)
         torch.cuda.synchronize()
         for b in outs:
             _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))

@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--streams", type=int, nargs="+", default=[1, 2, 3])
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--camera", default="flyover")
+    ap.add_argument("--separate", action="store_true",
+                    help="one context (own pool copy) per stream instead of one shared context")
     a = ap.parse_args()
     import torch
     from raytracingtest_amd import RaytracingMaster
@@ -27,9 +29,10 @@ def main():
     svo = build_sampler_svo(4, 11, device=0)
     W, H = 1920, 1080
     for S in a.streams:
-        # one context per stream (own pool replica and scheduling state): nothing
-        # shared, so the library does not order the streams against each other
-        rms = [RaytracingMaster(device=0, capacity_nodes=len(svo)) for _ in range(S)]
+        # one context: the plugin keeps per-stream dispatch-order state, so its renders on
+        # different streams overlap over one pool; --separate: a context (pool copy) per stream
+        n_ctx = S if a.separate else 1
+        rms = [RaytracingMaster(device=0, capacity_nodes=len(svo)) for _ in range(n_ctx)]
         for rm in rms:
             rm.SetSVOBuffer(svo)
             rm.UpdateShaderParameters(CAMERAS[a.camera](), W, H)
@@ -39,7 +42,7 @@ def main():
 
         def step(i):
             k = i % S
-            rms[k].render_device(W, H, rgba_ptr=rgba[k].data_ptr(), hits_ptr=hits[k].data_ptr(),
+            rms[k % n_ctx].render_device(W, H, rgba_ptr=rgba[k].data_ptr(), hits_ptr=hits[k].data_ptr(),
                              stream=streams[k].cuda_stream)
 
         for i in range(10):
