@@ -14,7 +14,7 @@ GPU, the SVO replicated per GPU (each rank builds the same bytes on its GPU),
 the frame split into 8-row bands dealt round-robin to the ranks (SURVEY.md
 8(e)), and every step ends with the north-star gather: rank 0 (the display
 GPU) renders its own bands straight into the display frame, every other rank's
-RGBA8 band payload goes to rank 0 over RCCL (one batch of sends / receives)
+3-byte RGB band payload goes to rank 0 over RCCL (one batch of sends / receives)
 and rank 0's plugin writes their rows into the frame (svo_assemble_frame).  The gather of frame k overlaps the render
 of frame k+1 (two streams, double-buffered payloads).  For C1-C3 the frame is
 the same camera at sqrt(N) times the linear resolution, so every GPU traces
@@ -77,9 +77,10 @@ def parse():
     p.add_argument("--stack-mode", type=int, default=None, help="0 = HLSL float2 stack, 1 = exact")
     p.add_argument("--frame-scaling", choices=["weak", "strong"], default=None,
                    help="N > 1: weak = frame grows with N (default for C1-C3), strong = configured frame")
-    p.add_argument("--payload", choices=["rgba8", "compact"], default="rgba8",
-                   help="N > 1: what moves to the display rank: RGBA8 display words (4 B/px) or compact "
-                        "records (12 B/px, rank 0 rebuilds hit records + Result)")
+    p.add_argument("--payload", choices=["rgb8", "rgba8", "compact"], default="rgb8",
+                   help="N > 1: what moves to the display rank: 3-byte RGB (the display word without its "
+                        "constant alpha, default), RGBA8 display words (4 B/px) or compact records (12 B/px, "
+                        "rank 0 rebuilds hit records + Result)")
     p.add_argument("--devices", default=None,
                    help="one-process multi-device mode: comma-separated HIP device indices of the context's members "
                         "(default 0..N-1; an index may repeat to rehearse the split on one GPU)")
@@ -241,9 +242,9 @@ def main():
     F = int(fetch.to(torch.int64).sum().item())
     bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if args.no_rgba else 16 * n_px)
     if gather is not None:
-        # the RGBA8 display words (rank 0, in the frame) or band payload (4 B RGBA8 / 12-B compact
-        # records) the kernel also writes
-        bytes_per_launch += (12 if args.payload == "compact" and rank != 0 else 4) * n_px
+        # the RGBA8 display words (rank 0, in the frame) or band payload (3 B RGB / 4 B RGBA8 /
+        # 12-B compact records) the kernel also writes
+        bytes_per_launch += (4 if rank == 0 else {"rgb8": 3, "rgba8": 4, "compact": 12}[args.payload]) * n_px
 
     # timed region: K steps between barrier + synchronize.  HIP events around each
     # step only with SVO_STEP_EVENTS=1 (diagnostics): their stream markers add
@@ -427,8 +428,8 @@ class Gather:
         self.rm, self.W, self.H, self.rank, self.world, self.dev = rm, W, H, rank, world, dev
         self.payload, self.owner, self.no_rgba, self.R = payload, owner, no_rgba, stream
         self.band = D.rank_band(rank, world, owner=owner)
-        self.elem = 4 if payload == "rgba8" else 12
-        per = D.max_band_len(H, world, owner=owner) * W * self.elem // 4
+        self.elem = {"rgb8": 3, "rgba8": 4, "compact": 12}[payload]
+        per = (D.max_band_len(H, world, owner=owner) * W * self.elem + 3) // 4   # int32 words
         self.G = torch.cuda.Stream(dev)
         self.n_local = D.band_len(H, rank, world, owner=owner) * W
         if rank == 0:   # display frames, double-buffered
@@ -473,6 +474,7 @@ class Gather:
             sp = self.send[k].data_ptr()
             self.rm.render_frame(self.W, self.H, hits=ptr(self.hits), rgba=ptr(self.rgba),
                                  rgba8=sp if self.payload == "rgba8" else None,
+                                 rgb8=sp if self.payload == "rgb8" else None,
                                  compact=sp if self.payload == "compact" else None,
                                  stack_mode=stack_mode, band=self.band, stream=self.R.cuda_stream)
         self.ev_r[k].record(self.R)
@@ -492,8 +494,9 @@ class Gather:
     def assemble(self, k, stream):
         ptrs = [None] + [p.data_ptr() for p in self.parts[k][1:]]
         s = stream.cuda_stream
-        if self.payload == "rgba8":
-            self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_RGBA8, rgba8=self.frame8[k].data_ptr(),
+        if self.payload in ("rgba8", "rgb8"):
+            fmt = self._lib.PART_RGBA8 if self.payload == "rgba8" else self._lib.PART_RGB8
+            self.rm.assemble_frame(self.W, self.H, ptrs, fmt, rgba8=self.frame8[k].data_ptr(),
                                    skip_part=0, stream=s, owner=self.owner)
         else:
             fr = self.frgba[k]

@@ -88,6 +88,8 @@ typedef struct svo_frame {
     uint64_t *voxel;           /* voxel key x | y << 21 | z << 42 of the hit leaf (integer voxel
                                   coordinates at the leaf scale, un-mirrored; unique for depth <= 21);
                                   misses all ones */
+    uint8_t *rgb8;             /* display RGB, 3 bytes per pixel (R, G, B): the RGBA8 word without
+                                  its constant alpha -- the smallest band payload of a split frame */
     int layout;
 } svo_frame;
 
@@ -159,13 +161,14 @@ int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const 
  * ignored; round-robin: bands b with b % n_parts == m), band layout, as
  * svo_hit_compact records (SVO_PART_COMPACT: frame
  * outputs hits / rgba / rgba8 / compact, the normal and colour rebuilt from this
- * context's SVO replica and camera) or RGBA8 words (SVO_PART_RGBA8: frame output
- * rgba8 only).  Part pointers must be readable from this device (its own memory,
+ * context's SVO replica and camera), RGBA8 words (SVO_PART_RGBA8) or 3-byte RGB
+ * (SVO_PART_RGB8; rows of 3 * width bytes) -- the last two rebuild the frame output
+ * rgba8 only.  Part pointers must be readable from this device (its own memory,
  * or a peer's with peer access).  skip_part (or -1): a part already rendered in
  * place.  `frame` must use the frame layout.  This is the display-side half of
  * the one-process-per-GPU split (parts received over RCCL); multi-device
  * contexts use it internally.  Asynchronous. */
-enum { SVO_PART_COMPACT = 0, SVO_PART_RGBA8 = 1 };
+enum { SVO_PART_COMPACT = 0, SVO_PART_RGBA8 = 1, SVO_PART_RGB8 = 2 };
 int svo_assemble_frame(svo_ctx *ctx, int width, int height, const svo_band *deal, int n_parts,
                        const void *const *parts, int part_format, int skip_part, const svo_frame *frame,
                        void *stream);

@@ -27,7 +27,7 @@ assert HIT_DTYPE.itemsize == 24
 COMPACT_DTYPE = np.dtype([("parent", "<u4"), ("meta", "<u4"), ("t", "<f4")])   # svo_hit_compact
 assert COMPACT_DTYPE.itemsize == 12
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
@@ -37,7 +37,7 @@ EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera"
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
-PART_COMPACT, PART_RGBA8 = 0, 1
+PART_COMPACT, PART_RGBA8, PART_RGB8 = 0, 1, 2
 STAGE_KERNEL, STAGE_ASSEMBLE = 0, 1
 
 
@@ -64,7 +64,7 @@ class SvoFrame(ctypes.Structure):
     """svo_frame: device pointers (ints) of every per-pixel output, each nullable."""
     _fields_ = [("hits", ctypes.c_void_p), ("rgba", ctypes.c_void_p), ("rgba8", ctypes.c_void_p),
                 ("compact", ctypes.c_void_p), ("position", ctypes.c_void_p), ("voxel", ctypes.c_void_p),
-                ("layout", ctypes.c_int)]
+                ("rgb8", ctypes.c_void_p), ("layout", ctypes.c_int)]
 
 
 class SvoError(RuntimeError):

@@ -455,7 +455,7 @@ __device__ __forceinline__ void record(const LaunchParams &p, const Ray &r, int 
     o.w[4] = (uint32_t)__float_as_int(n[1]);
     o.w[5] = (uint32_t)__float_as_int(n[2]);
     o.rgb[0] = o.rgb[1] = o.rgb[2] = 0.0f;
-    if (p.out.rgba || p.out.rgba8) {
+    if (p.out.rgba || p.out.rgba8 || p.out.rgb8) {
         float alb[3];
         decode_dxt(a.x, a.y, hit_idx, alb);
         shade_hit(p.cam, n, alb, o.rgb);
@@ -492,7 +492,16 @@ __device__ __forceinline__ void store_outputs(const Outputs &out, size_t i, cons
     }
     if (out.compact) reinterpret_cast<uint3 *>(out.compact)[i] = make_uint3(o.w[0], o.w[1], o.w[2]);
     if (out.rgba) out.rgba[i] = make_float4(o.rgb[0], o.rgb[1], o.rgb[2], 1.0f);
-    if (out.rgba8) out.rgba8[i] = pack_rgba8(o.rgb[0], o.rgb[1], o.rgb[2]);
+    if (out.rgba8 || out.rgb8) {
+        const uint32_t w = pack_rgba8(o.rgb[0], o.rgb[1], o.rgb[2]);
+        if (out.rgba8) out.rgba8[i] = w;
+        if (out.rgb8) {
+            uint8_t *d = out.rgb8 + 3 * i;
+            d[0] = (uint8_t)w;
+            d[1] = (uint8_t)(w >> 8);
+            d[2] = (uint8_t)(w >> 16);
+        }
+    }
     if (out.position) out.position[i] = make_float4(o.pos[0], o.pos[1], o.pos[2], 0.0f);
     if (out.voxel) out.voxel[i] = o.key;
 }
@@ -698,6 +707,10 @@ __global__ __launch_bounds__(TILE) void shadow_tile_kernel(LaunchParams p, int t
         if (p.out.compact) p.out.compact[3 * i + 1] = nw1;
         if (p.out.rgba) p.out.rgba[i] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
         if (p.out.rgba8) p.out.rgba8[i] = 255u << 24;
+        if (p.out.rgb8) {
+            uint8_t *d = p.out.rgb8 + 3 * i;
+            d[0] = d[1] = d[2] = 0;
+        }
     }
 }
 
@@ -734,6 +747,11 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleParams a) {
     const size_t dst = (size_t)y * (size_t)a.width + (size_t)x;
     if (a.part_format == PART_RGBA8) {
         a.out.rgba8[dst] = reinterpret_cast<const uint32_t *>(a.parts[m])[src];
+        return;
+    }
+    if (a.part_format == PART_RGB8) {
+        const uint8_t *c = reinterpret_cast<const uint8_t *>(a.parts[m]) + 3 * src;
+        a.out.rgba8[dst] = (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16) | (255u << 24);
         return;
     }
     const uint3 c = reinterpret_cast<const uint3 *>(a.parts[m])[src];
@@ -1013,9 +1031,10 @@ hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int 
     return hipGetLastError();
 }
 
-// RGBA8 parts: pure data movement (4 B read + 4 B written per pixel), so 16 bytes
-// per lane and the row's band arithmetic once per workgroup (row = blockIdx.y).
-// Needs width % 4 == 0 (16-byte aligned rows in every part and in the frame).
+// RGBA8 / RGB8 parts: pure data movement (4 or 3 B read + 4 B written per pixel), so
+// 4 pixels per lane and the row's band arithmetic once per workgroup (row =
+// blockIdx.y).  Needs width % 4 == 0 (16-byte aligned RGBA rows, 4-byte aligned RGB
+// groups in every part and in the frame).
 __global__ __launch_bounds__(256) void assemble_rgba8_kernel(AssembleParams a) {
     const int y = (int)blockIdx.y;
     int lr;
@@ -1023,15 +1042,23 @@ __global__ __launch_bounds__(256) void assemble_rgba8_kernel(AssembleParams a) {
     if (m == a.skip_part) return;
     const int q = (int)(blockIdx.x * 256 + threadIdx.x);   // 4-pixel group of the row
     if (4 * q >= a.width) return;
+    uint4 *dst = reinterpret_cast<uint4 *>(a.out.rgba8 + (size_t)y * (size_t)a.width);
+    if (a.part_format == PART_RGB8) {   // 12 bytes (4 x RGB) -> 16 (4 x RGBA, alpha 255)
+        const uint32_t *row = reinterpret_cast<const uint32_t *>(a.parts[m]) + (size_t)lr * (size_t)(3 * a.width / 4);
+        const uint32_t w0 = row[3 * q], w1 = row[3 * q + 1], w2 = row[3 * q + 2];
+        const uint32_t A = 255u << 24;
+        dst[q] = make_uint4((w0 & 0xFFFFFFu) | A, (w0 >> 24) | ((w1 & 0xFFFFu) << 8) | A,
+                            (w1 >> 16) | ((w2 & 0xFFu) << 16) | A, (w2 >> 8) | A);
+        return;
+    }
     const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(a.parts[m]) +
                                                        (size_t)lr * (size_t)a.width);
-    uint4 *dst = reinterpret_cast<uint4 *>(a.out.rgba8 + (size_t)y * (size_t)a.width);
     dst[q] = src[q];
 }
 
 hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
     if (a.width <= 0 || a.height <= 0) return hipSuccess;
-    if (a.part_format == PART_RGBA8 && a.width % 4 == 0) {
+    if ((a.part_format == PART_RGBA8 || a.part_format == PART_RGB8) && a.width % 4 == 0) {
         const dim3 grid((unsigned)((a.width / 4 + 255) / 256), (unsigned)a.height);
         hipLaunchKernelGGL(assemble_rgba8_kernel, grid, dim3(256), 0, stream, a);
         return hipGetLastError();

@@ -408,6 +408,7 @@ svo::Outputs outputs_of(const svo_frame *f) {
     o.compact = reinterpret_cast<uint32_t *>(f->compact);
     o.position = reinterpret_cast<float4 *>(f->position);
     o.voxel = reinterpret_cast<unsigned long long *>(f->voxel);
+    o.rgb8 = f->rgb8;
     o.frame_layout = f->layout == SVO_LAYOUT_FRAME ? 1 : 0;
     return o;
 }
@@ -581,8 +582,10 @@ int check_assemble_args(svo_ctx *ctx, int width, int height, int n_parts, int pa
     if (n_parts < 1 || n_parts > svo::MAX_PARTS) return fail(SVO_ERR_ARG, "n_parts must be in [1, 64]");
     if (skip_part < -1 || skip_part >= n_parts) return fail(SVO_ERR_ARG, "skip_part out of range");
     if (o.position || o.voxel || o.fetches) return fail(SVO_ERR_ARG, "position / voxel outputs are not assembled");
-    if (part_format == SVO_PART_RGBA8) {
-        if (!o.rgba8 || o.hits || o.rgba || o.compact) return fail(SVO_ERR_ARG, "RGBA8 parts rebuild only an RGBA8 frame");
+    if (o.rgb8) return fail(SVO_ERR_ARG, "the assembled frame is RGBA8 (rgb8 is a band payload)");
+    if (part_format == SVO_PART_RGBA8 || part_format == SVO_PART_RGB8) {
+        if (!o.rgba8 || o.hits || o.rgba || o.compact)
+            return fail(SVO_ERR_ARG, "RGBA8 / RGB8 parts rebuild only an RGBA8 frame");
     } else if (part_format == SVO_PART_COMPACT) {
         if ((o.hits || o.rgba || o.rgba8) && ctx->n_nodes == 0)
             return fail(SVO_ERR_STATE, "no node pool uploaded: compact parts need the SVO replica");
@@ -599,9 +602,11 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
     svo::Outputs out = outputs_of(frame);
     out.frame_layout = 1;
     if (out.position || out.voxel) return fail(SVO_ERR_ARG, "position / voxel outputs are not gathered across devices");
+    if (out.rgb8) return fail(SVO_ERR_ARG, "a multi-device frame is assembled as rgba8, not rgb8");
     if (!out.hits && !out.rgba && !out.rgba8 && !out.compact) return fail(SVO_ERR_ARG, "no output requested");
-    const int fmt = (out.hits || out.rgba || out.compact) ? SVO_PART_COMPACT : SVO_PART_RGBA8;
-    const size_t elem = fmt == SVO_PART_COMPACT ? 12 : 4;
+    // display-only frames travel as 3-byte RGB (the RGBA8 word without its constant alpha)
+    const int fmt = (out.hits || out.rgba || out.compact) ? SVO_PART_COMPACT : SVO_PART_RGB8;
+    const size_t elem = fmt == SVO_PART_COMPACT ? 12 : 3;
     const int k = ctx->parity;
     ctx->parity ^= 1;
     svo_ctx *m0 = ctx->members[0];
@@ -636,7 +641,7 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
         if (ctx->gathered_used[k]) HIP_TRY(hipStreamWaitEvent(m->stream, ctx->gathered[k], 0));   // payload k is free
         svo::Outputs oi{};
         if (fmt == SVO_PART_COMPACT) oi.compact = reinterpret_cast<uint32_t *>(pr.buf[k]);
-        else oi.rgba8 = reinterpret_cast<uint32_t *>(pr.buf[k]);
+        else oi.rgb8 = reinterpret_cast<uint8_t *>(pr.buf[k]);
         rc = launch(m, width, height, stack_mode, &bi, oi, m->stream);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(pr.rendered[k], m->stream));
@@ -712,7 +717,7 @@ int destroy_single(svo_ctx *ctx) {
 
 extern "C" {
 
-int svo_abi_version(void) { return 4; }
+int svo_abi_version(void) { return 5; }
 
 const char *svo_last_error(void) { return g_last_error.c_str(); }
 

@@ -47,6 +47,7 @@ struct Outputs {
     uint32_t *compact;         // svo_hit_compact: 3 words = the first 12 bytes of svo_hit
     float4 *position;          // bestHit.position (NVIDIASVO.compute:172-174), w = 0
     unsigned long long *voxel; // voxel key
+    uint8_t *rgb8;             // display RGB, 3 bytes per pixel (the RGBA8 word's low bytes)
     uint32_t *fetches;         // instrumented launch: descriptor fetches per ray
     int frame_layout;          // 1: index by global row (full-frame buffers)
 };
@@ -86,7 +87,7 @@ struct LaunchParams {
 // (PART_RGBA8).  Compact parts are expanded into every requested output: the
 // normal and the Result colour are rebuilt from the display device's own SVO
 // replica and camera with the render kernel's arithmetic (bit-identical).
-enum { PART_COMPACT = 0, PART_RGBA8 = 1 };
+enum { PART_COMPACT = 0, PART_RGBA8 = 1, PART_RGB8 = 2 };
 struct AssembleParams {
     const uint2 *att;
     uint32_t n_nodes;     // a parent outside the pool reads attachment words 0

@@ -35,8 +35,8 @@ from .svo_data import SVOData
 REFERENCE_CAPACITY = 1073741824 // 8
 
 
-def _frame(hits=None, rgba=None, rgba8=None, compact=None, position=None, voxel=None, layout=LAYOUT_BAND):
-    return SvoFrame(hits, rgba, rgba8, compact, position, voxel, layout)
+def _frame(hits=None, rgba=None, rgba8=None, compact=None, position=None, voxel=None, layout=LAYOUT_BAND, rgb8=None):
+    return SvoFrame(hits, rgba, rgba8, compact, position, voxel, rgb8, layout)
 
 
 class RaytracingMaster:
@@ -191,13 +191,13 @@ class RaytracingMaster:
               "svo_render_device")
 
     def render_frame(self, width, height, hits=None, rgba=None, rgba8=None, compact=None, position=None,
-                     voxel=None, layout=LAYOUT_BAND, stack_mode=STACK_HLSL, band=None, stream=None):
+                     voxel=None, layout=LAYOUT_BAND, stack_mode=STACK_HLSL, band=None, stream=None, rgb8=None):
         """Asynchronous render of every requested output (device pointers).
         layout LAYOUT_BAND: buffers hold only `band`'s rows; LAYOUT_FRAME: full-frame
         buffers.  A multi-device context renders the whole frame (band None) onto
         devices[0]."""
         b = None if band is None else ctypes.byref(make_band(band))
-        f = _frame(hits, rgba, rgba8, compact, position, voxel, layout)
+        f = _frame(hits, rgba, rgba8, compact, position, voxel, layout, rgb8)
         check(_lib.lib().svo_render_frame(self._ctx, width, height, stack_mode, b, ctypes.byref(f), stream),
               "svo_render_frame")
 

@@ -50,7 +50,8 @@ def _bufs(torch, n_px):
             "rgba8": t.full((n_px,), 0x1234567, dtype=t.int32, device="cuda"),
             "compact": t.full((n_px * 12,), 0x5A, dtype=t.uint8, device="cuda"),
             "position": t.full((n_px * 4,), -9.0, dtype=t.float32, device="cuda"),
-            "voxel": t.full((n_px,), 77, dtype=t.int64, device="cuda")}
+            "voxel": t.full((n_px,), 77, dtype=t.int64, device="cuda"),
+            "rgb8": t.full((n_px * 3,), 0xA5, dtype=t.uint8, device="cuda")}
 
 
 def _ptrs(b, keys=None):
@@ -74,13 +75,38 @@ def _check(b, oracle_mod, ref_hits, ref_rgba, ref_pos=None, ref_vox=None, keys=N
         assert c.tobytes() == ref_hits.view(np.uint8).reshape(-1, 24)[:, :12].tobytes(), "compact differs"
     if "position" in keys and ref_pos is not None:
         assert b["position"].cpu().numpy().tobytes() == ref_pos.tobytes(), "position differs"
+    if "rgb8" in keys:
+        got = b["rgb8"].cpu().numpy().reshape(-1, 3)
+        want = oracle_mod.pack_rgba8(ref_rgba).view(np.uint8).reshape(-1, 4)[:, :3]
+        assert np.array_equal(got, want), "RGB8 differs"
     if "voxel" in keys and ref_vox is not None:
         assert np.array_equal(b["voxel"].cpu().numpy().view(np.uint64), ref_vox), "voxel key differs"
 
 
+def test_each_output_alone_matches_oracle(torch, oracle_mod):
+    """Every output requested on its own (nothing computed only for another
+    output): the display words and the RGB payload carry the shaded colour even
+    without the Result, the compact record without the hit record."""
+    svo = build_menger(8)
+    w, h = 333, 201
+    cam = overview_camera()
+    ref_hits, ref_rgba, ref_pos, ref_vox = _oracle(oracle_mod, svo, cam, w, h)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        for key in ("hits", "rgba", "rgba8", "rgb8", "compact", "position", "voxel"):
+            b = _bufs(torch, w * h)
+            m.render_frame(w, h, **_ptrs(b, (key,)))
+            m.synchronize()
+            _check(b, oracle_mod, ref_hits, ref_rgba, ref_pos, ref_vox, keys=(key,))
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_every_output_matches_oracle(torch, oracle_mod, text_svo, mode):
-    """All six outputs of one launch, Text SVO (C1) and the 256^3 Menger (V2)."""
+    """All seven outputs of one launch, Text SVO (C1) and the 256^3 Menger (V2)."""
     for svo, cam, (w, h) in ((text_svo, main_camera(), (256, 256)), (text_svo, overview_camera(), (300, 200)),
                              (build_menger(8), overview_camera(), (480, 272))):
         ref_hits, ref_rgba, ref_pos, ref_vox = _oracle(oracle_mod, svo, cam, w, h, mode)
@@ -252,12 +278,14 @@ def test_assemble_from_rank_parts(torch, oracle_mod, world):
     try:
         m.SetSVOBuffer(svo)
         m.UpdateShaderParameters(cam, w, h)
-        comp, rgb8 = [], []
+        comp, rgb8, rgb3 = [], [], []
         for r in range(world):
             n = len(band_rows(h, (8, r, world))) * w
             comp.append(torch.zeros(max(n, 1) * 12, dtype=torch.uint8, device="cuda"))
             rgb8.append(torch.zeros(max(n, 1), dtype=torch.int32, device="cuda"))
-            m.render_frame(w, h, compact=comp[-1].data_ptr(), rgba8=rgb8[-1].data_ptr(), band=(8, r, world))
+            rgb3.append(torch.zeros(max(n, 1) * 3, dtype=torch.uint8, device="cuda"))
+            m.render_frame(w, h, compact=comp[-1].data_ptr(), rgba8=rgb8[-1].data_ptr(), rgb8=rgb3[-1].data_ptr(),
+                           band=(8, r, world))
         b = _bufs(torch, w * h)
         m.assemble_frame(w, h, [c.data_ptr() for c in comp], _lib.PART_COMPACT, hits=b["hits"].data_ptr(),
                          rgba=b["rgba"].data_ptr(), compact=b["compact"].data_ptr())
@@ -269,10 +297,13 @@ def test_assemble_from_rank_parts(torch, oracle_mod, world):
         m.render_frame(w, h, rgba8=b3["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME, band=(8, 0, world))
         m.assemble_frame(w, h, [None] + [c.data_ptr() for c in rgb8[1:]], _lib.PART_RGBA8,
                          rgba8=b3["rgba8"].data_ptr(), skip_part=0)
+        b4 = _bufs(torch, w * h)   # 3-byte RGB parts (the default N > 1 payload)
+        m.assemble_frame(w, h, [c.data_ptr() for c in rgb3], _lib.PART_RGB8, rgba8=b4["rgba8"].data_ptr())
         m.synchronize()
         _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba", "compact"))
         _check(b2, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
         _check(b3, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+        _check(b4, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
         with pytest.raises(_lib.SvoError):   # RGBA8 parts cannot rebuild hit records
             m.assemble_frame(w, h, [c.data_ptr() for c in rgb8], _lib.PART_RGBA8, hits=b["hits"].data_ptr())
     finally:
@@ -298,12 +329,14 @@ def test_weighted_deal_parts_match_oracle(torch, oracle_mod, world, share):
         b = _bufs(torch, w * h)
         m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(), rgba8=b["rgba8"].data_ptr(),
                        layout=_lib.LAYOUT_FRAME, band=(8, 0, world, owner))
-        comp, rgb8 = [None], [None]
+        comp, rgb8, rgb3 = [None], [None], [None]
         for r in range(1, world):
             n = len(band_rows(h, (8, r, world, owner))) * w
             comp.append(torch.zeros(max(n, 1) * 12, dtype=torch.uint8, device="cuda"))
             rgb8.append(torch.zeros(max(n, 1), dtype=torch.int32, device="cuda"))
-            m.render_frame(w, h, compact=comp[-1].data_ptr(), rgba8=rgb8[-1].data_ptr(), band=(8, r, world, owner))
+            rgb3.append(torch.zeros(max(n, 1) * 3, dtype=torch.uint8, device="cuda"))
+            m.render_frame(w, h, compact=comp[-1].data_ptr(), rgba8=rgb8[-1].data_ptr(), rgb8=rgb3[-1].data_ptr(),
+                           band=(8, r, world, owner))
         b2 = _bufs(torch, w * h)
         m.render_frame(w, h, rgba8=b2["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME, band=(8, 0, world, owner))
         m.assemble_frame(w, h, [None] + [c.data_ptr() for c in rgb8[1:]], _lib.PART_RGBA8,
@@ -311,9 +344,14 @@ def test_weighted_deal_parts_match_oracle(torch, oracle_mod, world, share):
         m.assemble_frame(w, h, [None] + [c.data_ptr() for c in comp[1:]], _lib.PART_COMPACT,
                          hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(), rgba8=b["rgba8"].data_ptr(),
                          skip_part=0, owner=owner)
+        b3 = _bufs(torch, w * h)
+        m.render_frame(w, h, rgba8=b3["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME, band=(8, 0, world, owner))
+        m.assemble_frame(w, h, [None] + [c.data_ptr() for c in rgb3[1:]], _lib.PART_RGB8,
+                         rgba8=b3["rgba8"].data_ptr(), skip_part=0, owner=owner)
         m.synchronize()
         _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba", "rgba8"))
         _check(b2, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+        _check(b3, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
         with pytest.raises(SvoError):   # owner entry naming a rank outside the deal
             m.render_frame(w, h, rgba8=b2["rgba8"].data_ptr(), band=(8, 0, world, [0, world]))
     finally:

@@ -12,7 +12,7 @@ mkdir -p gpurun_out/ranks
 export SVO_BENCH_BACKEND=gloo MASTER_ADDR=127.0.0.1
 port=29531
 for n in ${RANKS:-2}; do
-for payload in rgba8 compact; do
+for payload in rgb8 rgba8 compact; do
   port=$((port + 1))
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
     --master-port $port bench.py --gpus $n --steps 10 --warmup 2 --payload $payload > gpurun_out/ranks/out_${n}_$payload.json 2>>gpurun_out/ranks/err.log || exit $?
