@@ -43,7 +43,7 @@ def _worker(rank, world, port, mode, out_dir):
     W, H = 96, 70
     c2w, inv_proj = overview_camera().uniforms(W, H)
     osvo = orc.OracleSVO(svo.childDescriptors, svo.attachments)
-    if mode in ("bands", "rgba8", "compact"):
+    if mode in ("bands", "rgba8", "rgb8", "compact"):
         cam = orc.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
         band = D.rank_band(rank, world)
         ys = band_rows(H, band)
@@ -56,18 +56,23 @@ def _worker(rank, world, port, mode, out_dir):
                 frame = D.assemble([p.numpy() for p in parts], H, W, orc.HIT_DTYPE)
                 np.save(os.path.join(out_dir, "frame.npy"), frame)
         else:   # bench.py's Gather: equal-size int32 payload slots, sent to rank 0, which keeps its own part
-            elem = 1 if mode == "rgba8" else 3
-            per = D.max_band_len(H, world) * W * elem
-            payload = (orc.pack_rgba8(rgba).view(np.int32) if mode == "rgba8" else
-                       np.frombuffer(hits.view(np.uint8).reshape(-1, 24)[:, :12].tobytes(), np.int32))
+            elem_b = {"rgba8": 4, "rgb8": 3, "compact": 12}[mode]
+            per = (D.max_band_len(H, world) * W * elem_b + 3) // 4
+            if mode == "rgba8":
+                raw = orc.pack_rgba8(rgba).tobytes()
+            elif mode == "rgb8":   # the display word without its alpha byte
+                raw = orc.pack_rgba8(rgba).view(np.uint8).reshape(-1, 4)[:, :3].tobytes()
+            else:
+                raw = hits.view(np.uint8).reshape(-1, 24)[:, :12].tobytes()
             send = torch.zeros(per, dtype=torch.int32)
-            send[:payload.size] = torch.from_numpy(payload.copy())
+            send.numpy().view(np.uint8)[:len(raw)] = np.frombuffer(raw, np.uint8)
             parts = [None] + [torch.full((per,), -7, dtype=torch.int32) for _ in range(1, world)] if rank == 0 else None
             D.gather_to_root(None if rank == 0 else send, parts, root=0)
             if rank == 0:
                 parts[0] = send   # the display rank's own rows never leave it
-                dt = np.uint32 if mode == "rgba8" else np.dtype([("w", "<u4", 3)])
-                trimmed = [p.numpy()[:D.band_len(H, r, world) * W * elem] for r, p in enumerate(parts)]
+                dt = {"rgba8": np.dtype(np.uint32), "rgb8": np.dtype([("rgb", "u1", 3)]),
+                      "compact": np.dtype([("w", "<u4", 3)])}[mode]
+                trimmed = [p.numpy().view(np.uint8)[:D.band_len(H, r, world) * W * elem_b] for r, p in enumerate(parts)]
                 frame = D.assemble(trimmed, H, W, dt)
                 np.save(os.path.join(out_dir, "frame.npy"), frame)
     else:
@@ -82,14 +87,15 @@ def _worker(rank, world, port, mode, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,world", [("bands", 2), ("samples", 2), ("rgba8", 2), ("rgba8", 3), ("compact", 3)])
+@pytest.mark.parametrize("mode,world", [("bands", 2), ("samples", 2), ("rgba8", 2), ("rgba8", 3), ("rgb8", 3),
+                                        ("compact", 3)])
 def test_gloo_ranks(tmp_path, oracle_mod, text_svo, mode, world):
     mp.spawn(_worker, args=(world, _free_port(), mode, str(tmp_path)), nprocs=world, join=True)
     from raytracingtest_amd.camera import jitter_offsets, main_light, overview_camera
     W, H = 96, 70
     c2w, inv_proj = overview_camera().uniforms(W, H)
     osvo = oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments)
-    if mode in ("bands", "rgba8", "compact"):
+    if mode in ("bands", "rgba8", "rgb8", "compact"):
         cam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
         ref, ref_rgba, _ = oracle_mod.render(osvo, cam, W, H)
         got = np.load(tmp_path / "frame.npy")
@@ -97,6 +103,8 @@ def test_gloo_ranks(tmp_path, oracle_mod, text_svo, mode, world):
             assert got.reshape(-1).tobytes() == ref.tobytes()
         elif mode == "rgba8":
             assert np.array_equal(got.reshape(-1), oracle_mod.pack_rgba8(ref_rgba))
+        elif mode == "rgb8":
+            assert got.tobytes() == oracle_mod.pack_rgba8(ref_rgba).view(np.uint8).reshape(-1, 4)[:, :3].tobytes()
         else:
             assert got.tobytes() == ref.view(np.uint8).reshape(-1, 24)[:, :12].tobytes()
     else:
