@@ -93,8 +93,10 @@ def parse():
     p.add_argument("--no-rgba", action="store_true")
     p.add_argument("--camera", choices=["flyover", "overview", "main", "terrain"], default=None)
     p.add_argument("--shadows", action="store_true", help="C3 '+1 shadow ray' pass after the primary rays")
-    p.add_argument("--no-extra-poses", dest="extra_poses", action="store_false",
-                   help="N = 1: skip timing the frame from the other camera poses (reported beside value)")
+    p.add_argument("--no-extras", "--no-extra-poses", dest="extras", action="store_false",
+                   help="N = 1: skip the figures reported beside value (other camera poses, frames in flight, "
+                        "host path); profiling runs use it so every render_tile_kernel launch is the value's "
+                        "workload, one frame at a time")
     a = p.parse_args()
     cfg = CONFIGS[a.config]
     for k in ("width", "height", "max_level", "sampler", "camera", "stack_mode"):
@@ -315,10 +317,10 @@ def main():
                   "Mrays_per_s": round((n_px + n_hit) / (sh_ms * 1e-3) / 1e6, 2),
                   "note": "primary pass + one shadow ray per primary hit (RaytraceCompute.compute:105-112), "
                           "whole step on the host clock between synchronizes, like value"}
-    host_path = host_path_rates(rm, W, H, args) if world == 1 and args.steps > 0 else None
-    in_flight = frames_in_flight(rm, W, H, args, dev) if world == 1 and args.steps > 0 else None
+    host_path = host_path_rates(rm, W, H, args) if world == 1 and args.steps > 0 and args.extras else None
+    in_flight = frames_in_flight(rm, W, H, args, dev) if world == 1 and args.steps > 0 and args.extras else None
     poses = None
-    if world == 1 and args.extra_poses and args.svo != "menger":
+    if world == 1 and args.extras and args.svo != "menger":
         poses = extra_poses(rm, args, W, H, hits, rgba, sptr, dev)
 
     rays_per_step = W * H

@@ -7,7 +7,7 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS" \
            "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  env "$@" timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --kernel-include-regex render_tile_kernel -d $OUT/g$i -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 > /dev/null 2>> $OUT/err.log || exit $?
+  env "$@" timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --kernel-include-regex render_tile_kernel -d $OUT/g$i -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 --no-extras > /dev/null 2>> $OUT/err.log || exit $?
 done
 python3 - <<'PY'
 import csv, glob, collections
