@@ -12,7 +12,9 @@
  *    thread-local svo_last_error() gives the text.  No C++ exception crosses.
  *  - host arrays are owned by the caller and copied before the call returns
  *    (ComputeBuffer.SetData semantics); device memory is owned by the context.
- *  - one context is driven from one host thread at a time.
+ *  - one context is driven from one host thread at a time; its asynchronous
+ *    entry points take any hipStream_t, and renders on different streams run
+ *    concurrently (per-stream dispatch-order state).
  */
 #ifndef SVO_RT_H
 #define SVO_RT_H
@@ -226,7 +228,9 @@ int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, 
 /* Information about the uploaded pool. */
 int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device);
 
-/* Block until all work on the context's stream has finished. */
+/* Block until all work of the context has finished: its own stream and every
+ * caller stream it rendered, assembled or accumulated on (a device-wide
+ * synchronise of each of its devices). */
 int svo_synchronize(svo_ctx *ctx);
 
 /* Release device memory (the reference never Release()s its buffers). */
