@@ -41,13 +41,15 @@ def _stale(out, srcs):
 
 
 def source_digest(name="libsvo_rt.so"):
-    """sha1 over a library's sources, the headers and the compile flags: the key
-    under which profiling evidence (profiles/pmc_summary.json) is valid."""
+    """sha1 over what decides the render kernel's memory traffic -- the library's
+    sources (kernels and the launch configuration), the kernel headers and the
+    compile flags: the key under which profiling evidence
+    (profiles/pmc_summary.json) is valid.  The public C header (include/) is
+    left out: its declarations and comments do not change the kernel."""
     import hashlib
     h = hashlib.sha1(" ".join(COMMON + [ARCH]).encode())
     files = [os.path.join(CSRC, s) for s in TARGETS[name]]
     files += sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
-    files += sorted(os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE))
     for f in files:
         with open(f, "rb") as fh:
             h.update(os.path.basename(f).encode())
