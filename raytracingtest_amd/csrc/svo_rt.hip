@@ -80,6 +80,8 @@ struct Sched {
     long long order_key = -1;        // geometry tile_order was built for (-1: none)
     long long shadow_key = -1;
     unsigned long long launches = 0, shadow_launches = 0;
+    unsigned long long built_view = 0;   // the context's view generation the order was built under
+    int built_mode = -1;                 // shadows | stack_mode << 2 of the costs it was built from
 };
 
 struct Peer {                       // one per member of a multi-device context (index 0: the display device)
@@ -127,7 +129,9 @@ struct svo_ctx {
     int shadow_order_enabled = 1;    // env SVO_SHADOW_ORDER=0: shadow tiles in plain strip order
     int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
     int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
-    int order_every = 8;             // env SVO_ORDER_EVERY: rebuild the order every k-th launch
+    int order_every = 32;            // env SVO_ORDER_EVERY: rebuild the order every k-th launch (and after
+                                     // every camera move or change of render mode)
+    unsigned long long view_gen = 0; // bumped when svo_set_camera changes the matrices
     Sched sched[MAX_SCHED];
     unsigned long long sched_clock = 0;
     // The one piece of state renders on different streams still share: the host-path /
@@ -516,12 +520,20 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     }
     hipError_t e = svo::launch_render(p, stack_mode, s, ev0, ev1);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
-    const bool refresh = q && p.tile_cost && (q->order_key != key || q->launches++ % ctx->order_every == 0);
+    // refresh: a new geometry, every order_every-th launch, and right after the first launch
+    // following a camera move or a change of render mode (that launch still uses the old
+    // order -- a permutation of the same tiles, placement only -- and records fresh costs)
+    const int mode_now = p.shadows | (stack_mode << 2);
+    const bool refresh = q && p.tile_cost &&
+                         (q->order_key != key || q->launches++ % ctx->order_every == 0 ||
+                          q->built_view != ctx->view_gen || q->built_mode != mode_now);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
         e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s)
                              : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         q->order_key = key;
+        q->built_view = ctx->view_gen;
+        q->built_mode = mode_now;
     }
     if (q && p.shadow_cost && (q->shadow_key != key || q->shadow_launches++ % ctx->order_every == 0)) {
         e = p.xcd_remap == 2 ? svo::launch_order_strips(q->shadow_cost, q->shadow_order, n_tiles, (width + 7) / 8, s)
@@ -919,6 +931,11 @@ int svo_set_camera(svo_ctx *ctx, const float c2w[16], const float inv_proj[16], 
                    float px_off_y, const float light[4]) {
     if (!ctx || !c2w || !inv_proj || !light) return fail(SVO_ERR_ARG, "null argument");
     for (svo_ctx *m : ctx->members) svo_set_camera(m, c2w, inv_proj, px_off_x, px_off_y, light);
+    // a moved camera changes the tiles' costs: the next launch refreshes the dispatch order
+    // (a new pixel offset or light alone does not)
+    if (!ctx->cam_set || std::memcmp(ctx->cam.c2w, c2w, sizeof(ctx->cam.c2w)) != 0 ||
+        std::memcmp(ctx->cam.inv_proj, inv_proj, sizeof(ctx->cam.inv_proj)) != 0)
+        ++ctx->view_gen;
     std::memcpy(ctx->cam.c2w, c2w, sizeof(ctx->cam.c2w));
     std::memcpy(ctx->cam.inv_proj, inv_proj, sizeof(ctx->cam.inv_proj));
     ctx->cam.px_off[0] = px_off_x;
