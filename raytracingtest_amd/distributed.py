@@ -103,7 +103,8 @@ def gather_to_root(send, parts, root=0, dist=None, group=None):
     if dist is None:
         import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    staged = dist.get_backend(group) == "gloo" and (send is not None and send.is_cuda)
+    tensors = [send] if rank != root else [p for r, p in enumerate(parts) if r != root]
+    staged = dist.get_backend(group) == "gloo" and any(t is not None and t.is_cuda for t in tensors)
     ops, copies = [], []
     if rank == root:
         for r in range(world):
