@@ -13,11 +13,15 @@
  *   Assets/Shaders/RaytraceCompute.compute:93-127    Shade (hit branch)
  *
  * Parity pinning: the reference path is HLSL + C# and cannot run here (no
- * dxc/fxc, no mono/dotnet, no Unity).  The decode functions are
- * pinned by the 4,977 normal-code known answers of the reference's `Text`
- * dump; the traversal is pinned by an independent double-precision
- * brute-force first-hit search (tests/test_oracle.py).  Traversal parity
- * against the HLSL itself is therefore "parity unpinned" beyond those checks.
+ * dxc/fxc, no mono/dotnet, no Unity), and the reference holds
+ * no traversal outputs.  The decode functions are pinned by the 4,977
+ * normal-code known answers of the reference's `Text` dump and by its worked
+ * attachment example; the traversal by two independent witnesses
+ * (tests/test_oracle.py): a restatement of the reference's own C# CPU tracer
+ * (NVIDIAIterativeTracer.cs:72-290, tests/cs_tracer.py), bit-identical to the
+ * EXACT stack mode on every reachable hit of both full C1 frames, and a
+ * double-precision brute-force first-hit search over the same frames.  The
+ * HLSL compiler's own FMA / rsqrt choices stay unpinned (strict IEEE here).
  */
 #ifndef SVO_ORACLE_H
 #define SVO_ORACLE_H
