@@ -47,7 +47,10 @@ def source_digest(name="libsvo_rt.so"):
     (profiles/pmc_summary.json) is valid.  The public C header (include/) is
     left out: its declarations and comments do not change the kernel."""
     import hashlib
-    h = hashlib.sha1(" ".join(COMMON + [ARCH]).encode())
+    # flags without the include paths: the digest must not depend on where the tree lies
+    # (the GPU box runs it from a scratch copy)
+    flags = [f for f in COMMON if not f.startswith("-I")]
+    h = hashlib.sha1(" ".join(flags + [ARCH]).encode())
     files = [os.path.join(CSRC, s) for s in TARGETS[name]]
     files += sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
     for f in files:

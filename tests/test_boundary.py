@@ -118,3 +118,19 @@ def test_unknown_option_bits_rejected_without_gpu(native):
     assert (SVO_OPT_SHADOW_RAYS, SVO_OPT_KERNEL_TIMING) == (1, 2)
     text = open(HEADER).read()
     assert "SVO_OPT_SHADOW_RAYS = 1" in text and "SVO_OPT_KERNEL_TIMING = 2" in text
+
+
+def test_profile_key_does_not_depend_on_the_tree_location(tmp_path):
+    """bench.py reads roofline.traffic from profiles/pmc_summary.json only when its
+    source digest matches the running tree; the GPU box runs a scratch copy at
+    another path, so the digest must not hash absolute paths."""
+    import shutil
+    import subprocess
+    import sys
+    dst = tmp_path / "copy"
+    for d in ("raytracingtest_amd", "include"):
+        shutil.copytree(os.path.join(ROOT, d), dst / d, ignore=shutil.ignore_patterns("*.so", "__pycache__"))
+    code = "import sys; sys.path.insert(0, sys.argv[1]); from raytracingtest_amd.build import source_digest; print(source_digest())"
+    here = subprocess.run([sys.executable, "-c", code, ROOT], capture_output=True, text=True, check=True).stdout
+    there = subprocess.run([sys.executable, "-c", code, str(dst)], capture_output=True, text=True, check=True).stdout
+    assert here.strip() and here == there
