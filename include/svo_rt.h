@@ -91,7 +91,10 @@ typedef struct svo_frame {
                                   coordinates at the leaf scale, un-mirrored; unique for depth <= 21);
                                   misses all ones */
     uint8_t *rgb8;             /* display RGB, 3 bytes per pixel (R, G, B): the RGBA8 word without
-                                  its constant alpha -- the smallest band payload of a split frame */
+                                  its constant alpha -- the dense band payload of a split frame */
+    uint64_t *hitmask;         /* one word per 8x8 tile of the render's rows (band-local tiles, row-major,
+                                  ceil(W/8) per tile row): bit (y%8)*8 + x%8 set = that pixel hit a
+                                  voxel (the wave's ballot) -- the head of a sparse band payload */
     int layout;
 } svo_frame;
 
@@ -164,16 +167,27 @@ int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const 
  * svo_hit_compact records (SVO_PART_COMPACT: frame
  * outputs hits / rgba / rgba8 / compact, the normal and colour rebuilt from this
  * context's SVO replica and camera), RGBA8 words (SVO_PART_RGBA8) or 3-byte RGB
- * (SVO_PART_RGB8; rows of 3 * width bytes) -- the last two rebuild the frame output
- * rgba8 only.  Part pointers must be readable from this device (its own memory,
+ * (SVO_PART_RGB8; rows of 3 * width bytes) or sparse hit RGB (SVO_PART_SPARSE_RGB8:
+ * svo_pack_hits' layout; miss pixels get the sky computed here) -- the last three
+ * rebuild the frame output rgba8 only.  Part pointers must be readable from this device (its own memory,
  * or a peer's with peer access).  skip_part (or -1): a part already rendered in
  * place.  `frame` must use the frame layout.  This is the display-side half of
  * the one-process-per-GPU split (parts received over RCCL); multi-device
  * contexts use it internally.  Asynchronous. */
-enum { SVO_PART_COMPACT = 0, SVO_PART_RGBA8 = 1, SVO_PART_RGB8 = 2 };
+enum { SVO_PART_COMPACT = 0, SVO_PART_RGBA8 = 1, SVO_PART_RGB8 = 2, SVO_PART_SPARSE_RGB8 = 3 };
 int svo_assemble_frame(svo_ctx *ctx, int width, int height, const svo_band *deal, int n_parts,
                        const void *const *parts, int part_format, int skip_part, const svo_frame *frame,
                        void *stream);
+
+/* Sparse band payload (wave ballot + prefix sum): `d_part` starts with the band's
+ * hit masks (svo_frame.hitmask, n_tiles = ceil(W/8) * ceil(rows/8) words, written by
+ * the render); this packs the 3-byte RGB of every hit pixel of `d_rgb8` (the band's
+ * dense svo_frame.rgb8) behind them, tile by tile in lane order.  d_offsets (n_tiles +
+ * 1 uint32, device) receives the hits before each tile and, last, the band's hit
+ * count: the part is n_tiles * 8 + count * 3 bytes.  Misses cost nothing -- the
+ * display device computes their sky.  Asynchronous. */
+int svo_pack_hits(svo_ctx *ctx, int width, int height, const svo_band *band, const void *d_rgb8, void *d_part,
+                  uint32_t *d_offsets, void *stream);
 
 /* Instrumented trace: per-ray descriptor-fetch counts (device uint32 array,
  * NVIDIASVO.compute:60-62 executions), used for the algorithmic-bytes figure

@@ -27,17 +27,18 @@ assert HIT_DTYPE.itemsize == 24
 COMPACT_DTYPE = np.dtype([("parent", "<u4"), ("meta", "<u4"), ("t", "<f4")])   # svo_hit_compact
 assert COMPACT_DTYPE.itemsize == 12
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
            "svo_destroy", "svo_last_error", "svo_abi_version", "svo_set_options", "svo_accumulate",
            "svo_kernel_time", "svo_create_multi", "svo_num_devices", "svo_get_member", "svo_render_frame",
-           "svo_assemble_frame", "svo_stage_time", "svo_render_progressive", "svo_set_band_deal")
+           "svo_assemble_frame", "svo_stage_time", "svo_render_progressive", "svo_set_band_deal",
+           "svo_pack_hits")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
-PART_COMPACT, PART_RGBA8, PART_RGB8 = 0, 1, 2
+PART_COMPACT, PART_RGBA8, PART_RGB8, PART_SPARSE_RGB8 = 0, 1, 2, 3
 STAGE_KERNEL, STAGE_ASSEMBLE = 0, 1
 
 
@@ -64,7 +65,7 @@ class SvoFrame(ctypes.Structure):
     """svo_frame: device pointers (ints) of every per-pixel output, each nullable."""
     _fields_ = [("hits", ctypes.c_void_p), ("rgba", ctypes.c_void_p), ("rgba8", ctypes.c_void_p),
                 ("compact", ctypes.c_void_p), ("position", ctypes.c_void_p), ("voxel", ctypes.c_void_p),
-                ("rgb8", ctypes.c_void_p), ("layout", ctypes.c_int)]
+                ("rgb8", ctypes.c_void_p), ("hitmask", ctypes.c_void_p), ("layout", ctypes.c_int)]
 
 
 class SvoError(RuntimeError):
@@ -111,6 +112,7 @@ def lib():
         "svo_stage_time": [vp, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)],
         "svo_render_progressive": [vp, i, i, i, ctypes.c_uint32, vp, vp],
         "svo_set_band_deal": [vp, i, ctypes.POINTER(ctypes.c_uint8)],
+        "svo_pack_hits": [vp, i, i, ctypes.POINTER(SvoBand), vp, vp, vp, vp],
         "svo_synchronize": [vp],
         "svo_destroy": [vp],
         "svo_last_error": [],

@@ -628,6 +628,10 @@ __global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int t
             trips = __shfl(trips, __ffsll((long long)hits) - 1);   // primary + shadow trips of the wave
         }
     }
+    if (p.out.hitmask) {   // the tile's hit lanes, for the sparse band payload
+        const uint64_t hm = __ballot(r.scale < S_MAX);
+        if (lane == 0) p.out.hitmask[t] = hm;
+    }
     if (p.tile_cost && (!SH || lane == 0)) p.tile_cost[t] = (uint16_t)min(trips, 65535);
     if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
         uint32_t *w = p.wave_log + 8 * (size_t)blockIdx.x;
@@ -752,6 +756,26 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleParams a) {
     if (a.part_format == PART_RGB8) {
         const uint8_t *c = reinterpret_cast<const uint8_t *>(a.parts[m]) + 3 * src;
         a.out.rgba8[dst] = (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16) | (255u << 24);
+        return;
+    }
+    if (a.part_format == PART_SPARSE_RGB8) {   // hit: its colour from the part; miss: the sky here
+        const int tiles_x = (a.width + 7) / 8;
+        const int t = (lr >> 3) * tiles_x + (x >> 3);
+        const int bit = ((lr & 7) << 3) | (x & 7);
+        const unsigned long long *masks = reinterpret_cast<const unsigned long long *>(a.parts[m]);
+        const unsigned long long mk = masks[t];
+        uint32_t w;
+        if ((mk >> bit) & 1ull) {
+            const uint32_t k = a.tile_offset[m][t] + (uint32_t)__popcll(mk & ((1ull << bit) - 1ull));
+            const uint8_t *c = reinterpret_cast<const uint8_t *>(masks + a.n_tiles[m]) + 3 * (size_t)k;
+            w = (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16) | (255u << 24);
+        } else {
+            float org[3], dir[3], rgb[3];
+            camera_ray(a.cam, a.width, a.height, x, y, org, dir);
+            sky(dir[1], rgb);
+            w = pack_rgba8(rgb[0], rgb[1], rgb[2]);
+        }
+        a.out.rgba8[dst] = w;
         return;
     }
     const uint3 c = reinterpret_cast<const uint3 *>(a.parts[m])[src];
@@ -1054,6 +1078,73 @@ __global__ __launch_bounds__(256) void assemble_rgba8_kernel(AssembleParams a) {
     const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(a.parts[m]) +
                                                        (size_t)lr * (size_t)a.width);
     dst[q] = src[q];
+}
+
+// ------------------------------------------------------ sparse hit payload
+// Exclusive scan of the tiles' hit counts: one 1024-thread workgroup walks the masks in
+// chunks of 1024 (wave prefix by shuffles, then across the 16 waves in LDS).
+constexpr int SCAN_THREADS = 1024;
+__global__ __launch_bounds__(SCAN_THREADS) void tile_scan_kernel(const unsigned long long *__restrict__ masks, int n,
+                                                                 uint32_t *__restrict__ offsets) {
+    __shared__ uint32_t wave_sum[SCAN_THREADS / 64];
+    __shared__ uint32_t carry;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += SCAN_THREADS) {
+        const int i = base + tid;
+        const uint32_t c = i < n ? (uint32_t)__popcll(masks[i]) : 0u;
+        uint32_t incl = c;   // inclusive prefix within the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, d);
+            if (lane >= d) incl += v;
+        }
+        if (lane == 63) wave_sum[wave] = incl;
+        __syncthreads();
+        uint32_t before = carry;
+        for (int w = 0; w < wave; ++w) before += wave_sum[w];
+        if (i < n) offsets[i] = before + incl - c;
+        __syncthreads();
+        if (tid == SCAN_THREADS - 1) carry = before + incl;   // the last thread's inclusive total
+        __syncthreads();
+    }
+    if (tid == 0) offsets[n] = carry;
+}
+
+hipError_t launch_tile_scan(const unsigned long long *masks, int n, uint32_t *offsets, hipStream_t stream) {
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, masks, n, offsets);
+    return hipGetLastError();
+}
+
+// One thread per pixel of the band: a hit pixel copies its 3 bytes to slot
+// offsets[t] + (hit lanes before it in its tile) behind the masks.
+__global__ __launch_bounds__(256) void pack_hits_kernel(const uint8_t *__restrict__ rgb8, int width, int local_rows,
+                                                        const uint32_t *__restrict__ offsets, unsigned long long *part) {
+    const int x = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int lr = (int)blockIdx.y;
+    if (x >= width || lr >= local_rows) return;
+    const int tiles_x = (width + 7) / 8;
+    const int t = (lr >> 3) * tiles_x + (x >> 3);
+    const int bit = ((lr & 7) << 3) | (x & 7);
+    const unsigned long long mk = part[t];
+    if (!((mk >> bit) & 1ull)) return;
+    const int n_tiles = tiles_x * ((local_rows + 7) / 8);
+    const uint32_t k = offsets[t] + (uint32_t)__popcll(mk & ((1ull << bit) - 1ull));
+    const uint8_t *s = rgb8 + 3 * ((size_t)lr * (size_t)width + (size_t)x);
+    uint8_t *d = reinterpret_cast<uint8_t *>(part + n_tiles) + 3 * (size_t)k;
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+}
+
+hipError_t launch_pack_hits(const uint8_t *rgb8, int width, int local_rows, const uint32_t *offsets, void *part,
+                            hipStream_t stream) {
+    if (width <= 0 || local_rows <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((width + 255) / 256), (unsigned)local_rows);
+    hipLaunchKernelGGL(pack_hits_kernel, grid, dim3(256), 0, stream, rgb8, width, local_rows, offsets,
+                       reinterpret_cast<unsigned long long *>(part));
+    return hipGetLastError();
 }
 
 hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {

@@ -48,6 +48,8 @@ struct Outputs {
     float4 *position;          // bestHit.position (NVIDIASVO.compute:172-174), w = 0
     unsigned long long *voxel; // voxel key
     uint8_t *rgb8;             // display RGB, 3 bytes per pixel (the RGBA8 word's low bytes)
+    unsigned long long *hitmask;   // per 8x8 tile of the render's rows (band-local tile index
+                                   // (lr / 8) * tiles_x + x / 8): the wave's ballot of its hit lanes
     uint32_t *fetches;         // instrumented launch: descriptor fetches per ray
     int frame_layout;          // 1: index by global row (full-frame buffers)
 };
@@ -87,7 +89,7 @@ struct LaunchParams {
 // (PART_RGBA8).  Compact parts are expanded into every requested output: the
 // normal and the Result colour are rebuilt from the display device's own SVO
 // replica and camera with the render kernel's arithmetic (bit-identical).
-enum { PART_COMPACT = 0, PART_RGBA8 = 1, PART_RGB8 = 2 };
+enum { PART_COMPACT = 0, PART_RGBA8 = 1, PART_RGB8 = 2, PART_SPARSE_RGB8 = 3 };
 struct AssembleParams {
     const uint2 *att;
     uint32_t n_nodes;     // a parent outside the pool reads attachment words 0
@@ -99,6 +101,10 @@ struct AssembleParams {
     int cycle;
     uint8_t owner[MAX_CYCLE], idx[MAX_CYCLE];
     int cnt[MAX_PARTS];
+    // PART_SPARSE_RGB8: part m = [n_tiles[m] hit masks (u64)][3-byte RGB of the hit pixels, tile
+    // by tile, lanes in order]; tile_offset[m][t] = hits before tile t (svo_rt.hip scans them)
+    uint32_t n_tiles[MAX_PARTS];
+    const uint32_t *tile_offset[MAX_PARTS];
     Outputs out;          // frame layout
 };
 
@@ -117,6 +123,14 @@ hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32
                              hipStream_t stream);
 
 hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream);
+
+// Exclusive prefix sum of the hit masks' popcounts (n tiles; one workgroup): offsets[t],
+// and the total in offsets[n].
+hipError_t launch_tile_scan(const unsigned long long *masks, int n, uint32_t *offsets, hipStream_t stream);
+// Sparse hit payload of a band: copy the 3-byte RGB of every hit pixel (per the masks at the
+// head of `part`) behind the masks, tile by tile (offsets from launch_tile_scan).
+hipError_t launch_pack_hits(const uint8_t *rgb8, int width, int local_rows, const uint32_t *offsets, void *part,
+                            hipStream_t stream);
 
 // Display RGBA8 words of an RGBA32F frame (svo_render_progressive).
 hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int num_cus, hipStream_t stream);

@@ -35,8 +35,9 @@ from .svo_data import SVOData
 REFERENCE_CAPACITY = 1073741824 // 8
 
 
-def _frame(hits=None, rgba=None, rgba8=None, compact=None, position=None, voxel=None, layout=LAYOUT_BAND, rgb8=None):
-    return SvoFrame(hits, rgba, rgba8, compact, position, voxel, rgb8, layout)
+def _frame(hits=None, rgba=None, rgba8=None, compact=None, position=None, voxel=None, layout=LAYOUT_BAND, rgb8=None,
+           hitmask=None):
+    return SvoFrame(hits, rgba, rgba8, compact, position, voxel, rgb8, hitmask, layout)
 
 
 class RaytracingMaster:
@@ -191,13 +192,14 @@ class RaytracingMaster:
               "svo_render_device")
 
     def render_frame(self, width, height, hits=None, rgba=None, rgba8=None, compact=None, position=None,
-                     voxel=None, layout=LAYOUT_BAND, stack_mode=STACK_HLSL, band=None, stream=None, rgb8=None):
+                     voxel=None, layout=LAYOUT_BAND, stack_mode=STACK_HLSL, band=None, stream=None, rgb8=None,
+                     hitmask=None):
         """Asynchronous render of every requested output (device pointers).
         layout LAYOUT_BAND: buffers hold only `band`'s rows; LAYOUT_FRAME: full-frame
         buffers.  A multi-device context renders the whole frame (band None) onto
         devices[0]."""
         b = None if band is None else ctypes.byref(make_band(band))
-        f = _frame(hits, rgba, rgba8, compact, position, voxel, layout, rgb8)
+        f = _frame(hits, rgba, rgba8, compact, position, voxel, layout, rgb8, hitmask)
         check(_lib.lib().svo_render_frame(self._ctx, width, height, stack_mode, b, ctypes.byref(f), stream),
               "svo_render_frame")
 
@@ -214,6 +216,14 @@ class RaytracingMaster:
         check(_lib.lib().svo_assemble_frame(self._ctx, width, height, ctypes.byref(deal), len(parts), arr,
                                             part_format, skip_part, ctypes.byref(f), stream),
               "svo_assemble_frame")
+
+    def pack_hits(self, width, height, band, rgb8, part, offsets, stream=None):
+        """Sparse band payload: `part` (device pointer) starts with the band's hit
+        masks (render_frame(hitmask=part)); pack the RGB of its hit pixels from the
+        band's dense `rgb8` behind them.  offsets (n_tiles + 1 uint32, device)
+        receives the per-tile hit offsets and, last, the band's hit count."""
+        b = ctypes.byref(make_band(band if band is not None else (self.band_rows, 0, 1)))
+        check(_lib.lib().svo_pack_hits(self._ctx, width, height, b, rgb8, part, offsets, stream), "svo_pack_hits")
 
     def count_fetches_device(self, width, height, fetch_ptr, stack_mode=STACK_HLSL, band=None, stream=None):
         b = None if band is None else ctypes.byref(make_band(band))

@@ -40,7 +40,7 @@ def test_exports_every_declared_symbol(native):
 
 
 def test_abi_version_and_error_text(native):
-    assert native.svo_abi_version() == 5
+    assert native.svo_abi_version() == 6
     assert isinstance(native.svo_last_error(), bytes)
 
 
@@ -59,7 +59,7 @@ def test_header_layout_compiles_in_c(tmp_path):
                    '_Static_assert(offsetof(svo_hit, nz) == 20, "nz");\n'
                    '_Static_assert(sizeof(svo_band) == 16 + sizeof(void *), "band");\n'
                    '_Static_assert(sizeof(svo_hit_compact) == 12, "compact");\n'
-                   '_Static_assert(offsetof(svo_frame, layout) == 56, "frame");\n'
+                   '_Static_assert(offsetof(svo_frame, layout) == 64, "frame");\n'
                    '_Static_assert(SVO_PART_RGBA8 == 1 && SVO_PART_RGB8 == 2 && SVO_LAYOUT_FRAME == 1 && SVO_STAGE_ASSEMBLE == 1, "enums");\n'
                    'int main(void){return 0;}\n')
     subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),

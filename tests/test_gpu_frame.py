@@ -358,6 +358,109 @@ def test_weighted_deal_parts_match_oracle(torch, oracle_mod, world, share):
         m.close()
 
 
+def _sparse_part(torch, m, w, h, band):
+    """A rank's sparse payload: render the dense RGB + the tile hit masks (at the
+    part's head), then svo_pack_hits.  Returns (part, offsets, n_tiles)."""
+    rows = len(band_rows(h, band))
+    n_tiles = ((w + 7) // 8) * ((rows + 7) // 8)
+    dense = torch.full((max(rows * w, 1) * 3,), 0xA5, dtype=torch.uint8, device="cuda")
+    part = torch.full((n_tiles * 8 + rows * w * 3 + 8,), 0x5A, dtype=torch.uint8, device="cuda")
+    offs = torch.full((n_tiles + 1,), -1, dtype=torch.int32, device="cuda")
+    m.render_frame(w, h, rgb8=dense.data_ptr(), hitmask=part.data_ptr(), band=band)
+    m.pack_hits(w, h, band, dense.data_ptr(), part.data_ptr(), offs.data_ptr())
+    return part, offs, n_tiles
+
+
+@pytest.mark.parametrize("world,share", [(1, None), (2, None), (3, 0.5), (8, 0.75)])
+def test_sparse_parts_match_oracle(torch, oracle_mod, world, share):
+    """The sparse band payload (tile hit masks + the RGB of hit pixels only):
+    each rank's hit count equals the oracle's hits in its rows, the packed
+    colours are the hits' RGBA8 bytes in tile/lane order, and the display rank
+    rebuilds the frame (misses: sky computed there) bit-identical to one frame
+    -- round-robin and weighted deals, frame widths that are not tile multiples."""
+    from raytracingtest_amd.distributed import weighted_owner
+    svo = build_menger(7)
+    cam = overview_camera()
+    w, h = (262, 203) if world == 3 else (264, 200)
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+    ref_hit = ((ref_hits["flags"] & 1) != 0).reshape(h, w)
+    ref_rgb = oracle_mod.pack_rgba8(ref_rgba).view(np.uint8).reshape(h, w, 4)[:, :, :3]
+    owner = None if share is None else weighted_owner(world, share)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        parts = []
+        for r in range(world):
+            band = (8, r, world) if owner is None else (8, r, world, owner)
+            part, offs, n_tiles = _sparse_part(torch, m, w, h, band)
+            parts.append(part)
+            m.synchronize()
+            ys = band_rows(h, band)
+            count = int(offs[-1].item())
+            assert count == int(ref_hit[ys].sum())
+            # the packed colours: tiles in order, lanes (row-major 8x8) within a tile
+            tx = (w + 7) // 8
+            want = []
+            for t in range(n_tiles):
+                by, bx = divmod(t, tx)
+                for lane in range(64):
+                    ly, lx = by * 8 + lane // 8, bx * 8 + lane % 8
+                    if ly < len(ys) and lx < w and ref_hit[ys[ly], lx]:
+                        want.append(ref_rgb[ys[ly], lx])
+            got = part[n_tiles * 8:n_tiles * 8 + 3 * count].cpu().numpy().reshape(-1, 3)
+            assert np.array_equal(got, np.array(want, np.uint8).reshape(-1, 3))
+        b = _bufs(torch, w * h)
+        m.assemble_frame(w, h, [p.data_ptr() for p in parts], _lib.PART_SPARSE_RGB8, rgba8=b["rgba8"].data_ptr(),
+                         owner=owner)
+        b2 = _bufs(torch, w * h)   # the display rank's own rows rendered in place
+        band0 = (8, 0, world) if owner is None else (8, 0, world, owner)
+        m.render_frame(w, h, rgba8=b2["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME, band=band0)
+        m.assemble_frame(w, h, [None] + [p.data_ptr() for p in parts[1:]], _lib.PART_SPARSE_RGB8,
+                         rgba8=b2["rgba8"].data_ptr(), skip_part=0, owner=owner)
+        m.synchronize()
+        _check(b, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+        _check(b2, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+        with pytest.raises(SvoError):   # sparse parts rebuild only display words
+            m.assemble_frame(w, h, [p.data_ptr() for p in parts], _lib.PART_SPARSE_RGB8, hits=b["hits"].data_ptr())
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("pose", ["all_miss", "all_hit"])
+def test_sparse_parts_extremes(torch, oracle_mod, pose):
+    """Sparse payload edge cases: a frame with no hit (the part is the masks
+    alone, count 0) and a frame hit everywhere (the part is as large as the
+    dense RGB plus the masks); both rebuild the oracle's frame."""
+    from raytracingtest_amd.builder import build_menger as menger
+    svo = menger(6, levels=0)   # a solid cube
+    if pose == "all_miss":
+        cam = overview_camera(target=(0.0, 60.0, -80.0))
+    else:
+        cam = overview_camera()
+        cam.fov = 5.0
+    w, h = 200, 120
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+    n_hit = int(np.count_nonzero(ref_hits["flags"] & 1))
+    assert n_hit == (0 if pose == "all_miss" else w * h)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        parts = []
+        for r in range(2):
+            part, offs, _ = _sparse_part(torch, m, w, h, (8, r, 2))
+            parts.append(part)
+            m.synchronize()
+            assert int(offs[-1].item()) == (0 if pose == "all_miss" else len(band_rows(h, (8, r, 2))) * w)
+        b = _bufs(torch, w * h)
+        m.assemble_frame(w, h, [p.data_ptr() for p in parts], _lib.PART_SPARSE_RGB8, rgba8=b["rgba8"].data_ptr())
+        m.synchronize()
+        _check(b, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("n_streams", [2, 6])
 def test_two_streams_every_pixel_written(torch, oracle_mod, n_streams):
     """Launches of one context cycling over several streams (advisor r1): each
