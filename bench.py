@@ -77,10 +77,12 @@ def parse():
     p.add_argument("--stack-mode", type=int, default=None, help="0 = HLSL float2 stack, 1 = exact")
     p.add_argument("--frame-scaling", choices=["weak", "strong"], default=None,
                    help="N > 1: weak = frame grows with N (default for C1-C3), strong = configured frame")
-    p.add_argument("--payload", choices=["rgb8", "rgba8", "compact"], default="rgb8",
+    p.add_argument("--payload", choices=["auto", "rgb8", "rgba8", "compact", "sparse"], default="auto",
                    help="N > 1: what moves to the display rank: 3-byte RGB (the display word without its "
-                        "constant alpha, default), RGBA8 display words (4 B/px) or compact records (12 B/px, "
-                        "rank 0 rebuilds hit records + Result)")
+                        "constant alpha), sparse (tile hit masks + the RGB of hit pixels only; rank 0 computes "
+                        "the sky), RGBA8 display words (4 B/px) or compact records (12 B/px, rank 0 rebuilds hit "
+                        "records + Result); auto (default): rgb8 or sparse, whichever ran the pipelined step "
+                        "faster in a calibration run (both reported)")
     p.add_argument("--devices", default=None,
                    help="one-process multi-device mode: comma-separated HIP device indices of the context's members "
                         "(default 0..N-1; an index may repeat to rehearse the split on one GPU)")
@@ -210,8 +212,8 @@ def main():
     gather = None
     deal_info = None
     if world > 1:
-        gather = Gather(rm, W, H, rank, world, dev, args.payload, stream, args.no_rgba)
-        gather, deal_info = weigh_display_rank(gather, args, rm, dist, dev)
+        gather, deal_info, payload_choice = choose_payload(args, rm, W, H, rank, world, dev, stream, dist)
+        args.payload = gather.payload
         hits = rgba = None
         band = gather.band
         n_px = gather.n_local
@@ -246,7 +248,7 @@ def main():
     if gather is not None:
         # the RGBA8 display words (rank 0, in the frame) or band payload (3 B RGB / 4 B RGBA8 /
         # 12-B compact records) the kernel also writes
-        bytes_per_launch += (4 if rank == 0 else {"rgb8": 3, "rgba8": 4, "compact": 12}[args.payload]) * n_px
+        bytes_per_launch += (4 if rank == 0 else {"rgb8": 3, "rgba8": 4, "compact": 12, "sparse": 3}[args.payload]) * n_px
 
     # timed region: K steps between barrier + synchronize.  HIP events around each
     # step only with SVO_STEP_EVENTS=1 (diagnostics): their stream markers add
@@ -393,6 +395,7 @@ def main():
                 "gather_ms_rank0": round(stages["gather_ms"], 4), "assemble_ms_rank0": round(stages["assemble_ms"], 4),
                 "payload_bytes_per_sending_rank": stages["payload_bytes"],
                 "display_rank_deal": deal_info,
+                "payload_choice": payload_choice,
                 "assembled_frame_check": frame_check,
                 "note": "value overlaps the gather of frame k with the render of frame k+1; render_only_Mrays is "
                         "the frame's rays over the slowest rank's render kernel alone; gather/assemble from a "
@@ -430,8 +433,13 @@ class Gather:
         self.rm, self.W, self.H, self.rank, self.world, self.dev = rm, W, H, rank, world, dev
         self.payload, self.owner, self.no_rgba, self.R = payload, owner, no_rgba, stream
         self.band = D.rank_band(rank, world, owner=owner)
-        self.elem = {"rgb8": 3, "rgba8": 4, "compact": 12}[payload]
-        per = (D.max_band_len(H, world, owner=owner) * W * self.elem + 3) // 4   # int32 words
+        self.elem = {"rgb8": 3, "rgba8": 4, "compact": 12, "sparse": 3}[payload]
+        rows_max = D.max_band_len(H, world, owner=owner)
+        if payload == "sparse":   # head + every pixel a hit + the pack's scratch tail
+            part_bytes = _lib.sparse_part_bytes(((W + 7) // 8) * ((rows_max + 7) // 8), rows_max * W)
+        else:
+            part_bytes = rows_max * W * self.elem
+        per = (part_bytes + 3) // 4   # int32 words
         self.G = torch.cuda.Stream(dev)
         self.n_local = D.band_len(H, rank, world, owner=owner) * W
         if rank == 0:   # display frames, double-buffered
@@ -496,8 +504,9 @@ class Gather:
     def assemble(self, k, stream):
         ptrs = [None] + [p.data_ptr() for p in self.parts[k][1:]]
         s = stream.cuda_stream
-        if self.payload in ("rgba8", "rgb8"):
-            fmt = self._lib.PART_RGBA8 if self.payload == "rgba8" else self._lib.PART_RGB8
+        if self.payload in ("rgba8", "rgb8", "sparse"):
+            fmt = {"rgba8": self._lib.PART_RGBA8, "rgb8": self._lib.PART_RGB8,
+                   "sparse": self._lib.PART_SPARSE_RGB8}[self.payload]
             self.rm.assemble_frame(self.W, self.H, ptrs, fmt, rgba8=self.frame8[k].data_ptr(),
                                    skip_part=0, stream=s, owner=self.owner)
         else:
@@ -572,6 +581,176 @@ class Gather:
         return out
 
 
+class SparseGather(Gather):
+    """Gather with the sparse band payload: a sending rank renders
+    its dense RGB into a scratch band and the tile hit masks into the head of
+    payload k, svo_pack_hits packs the hits' RGB behind the masks, and only
+    masks + hits cross xGMI.  The size varies per frame, so the transfer runs one
+    step late: step s sends frame s's hit count to rank 0 (4 bytes per rank, on
+    the gather stream) and then frame s-1's payload at its exact size, after the
+    host has read frame s-1's counts -- by then frame s's render is already
+    queued on every GPU, so the host wait does not idle them.  Rank 0 assembles
+    frame s-1 behind the render of frame s (misses: sky computed there)."""
+
+    def __init__(self, rm, W, H, rank, world, dev, payload, stream, no_rgba, owner=None):
+        super().__init__(rm, W, H, rank, world, dev, payload, stream, no_rgba, owner)
+        torch, D = self.torch, self.D
+        self.tiles = [((W + 7) // 8) * ((D.band_len(H, m, world, owner=owner) + 7) // 8) for m in range(world)]
+        if rank == 0:
+            self.cbuf = [torch.zeros(world, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.cnt_host = [torch.zeros(world, dtype=torch.int32).pin_memory() for _ in range(2)]
+            self.ev_c = [torch.cuda.Event() for _ in range(2)]
+        else:
+            self.dense = torch.empty(max(self.n_local, 1) * 3, dtype=torch.uint8, device=dev)
+            self.cnt_host = [torch.zeros(1, dtype=torch.int32).pin_memory() for _ in range(2)]
+        self.sent = 0            # payload bytes of the last frame this rank sent (rank 0: rank 1's)
+
+    def render(self, k, stack_mode):
+        if self.rank == 0:
+            return super().render(k, stack_mode)
+        if self.used[k]:
+            self.R.wait_event(self.ev_g[k])   # payload k sent
+        s = self.R.cuda_stream
+        ptr = lambda t: None if t is None else t.data_ptr()
+        nt = self.tiles[self.rank]
+        self.rm.render_frame(self.W, self.H, hits=ptr(self.hits), rgba=ptr(self.rgba), rgb8=self.dense.data_ptr(),
+                             hitmask=self.send[k].data_ptr(), stack_mode=stack_mode, band=self.band, stream=s)
+        self.rm.pack_hits(self.W, self.H, self.band, self.dense.data_ptr(), self.send[k].data_ptr(), stream=s)
+        with self.torch.cuda.stream(self.R):
+            self.cnt_host[k].copy_(self.send[k][3 * nt:3 * nt + 1], non_blocking=True)   # the count, byte 12 n
+        self.ev_r[k].record(self.R)
+
+    def _part_bytes(self, m, count):
+        return self._lib.sparse_head_bytes(self.tiles[m]) + 3 * int(count)
+
+    def gather_counts(self, k):
+        """Frame k's hit counts to rank 0 (device to device, then to pinned host)."""
+        if self.rank == 0:
+            with self.torch.cuda.stream(self.G):
+                self.D.gather_to_root(None, [self.cbuf[k][m:m + 1] for m in range(self.world)], root=0)
+                self.cnt_host[k].copy_(self.cbuf[k], non_blocking=True)
+            self.ev_c[k].record(self.G)
+        else:
+            nt = self.tiles[self.rank]
+            self.G.wait_event(self.ev_r[k])
+            with self.torch.cuda.stream(self.G):
+                self.D.gather_to_root(self.send[k][3 * nt:3 * nt + 1], None, root=0)
+
+    def gather(self, k):
+        """Frame k's payloads at their exact sizes (its counts gathered a step earlier)."""
+        if self.rank == 0:
+            self.ev_c[k].synchronize()
+            counts = self.cnt_host[k].tolist()
+            if self.used[k]:
+                self.G.wait_event(self.ev_a[k])   # parts k read by the previous assemble
+            parts = [None] + [self.parts[k][m].view(self.torch.uint8)[:self._part_bytes(m, counts[m])]
+                              for m in range(1, self.world)]
+            with self.torch.cuda.stream(self.G):
+                self.D.gather_to_root(None, parts, root=0)
+            self.sent = self._part_bytes(1, counts[1])
+        else:
+            self.ev_r[k].synchronize()
+            n = self._part_bytes(self.rank, self.cnt_host[k].item())
+            with self.torch.cuda.stream(self.G):
+                self.D.gather_to_root(self.send[k].view(self.torch.uint8)[:n], None, root=0)
+            self.sent = n
+        self.ev_g[k].record(self.G)
+        self.used[k] = True
+
+    def drain(self):
+        """Send and (rank 0) assemble the frame still pending."""
+        if self.pending is None:
+            return
+        k = self.pending
+        self.pending = None
+        self.gather(k)
+        if self.rank == 0:
+            self.R.wait_event(self.ev_g[k])
+            self.assemble(k, self.R)
+            self.ev_a[k].record(self.R)
+        self.last = k
+
+    def step(self, stack_mode):
+        k = self.k
+        self.k ^= 1
+        self.render(k, stack_mode)
+        self.gather_counts(k)
+        self.drain()             # frame k-1: its payloads, and on rank 0 its assemble behind render k
+        self.pending = k
+
+    def stage_times(self, stack_mode, n):
+        """Serialized render -> counts -> payload -> assemble, events on the gather stream."""
+        torch = self.torch
+        self.drain()
+        g_ms, a_ms, sent = [], [], []
+        for _ in range(n):
+            torch.cuda.synchronize(self.dev)
+            self.render(0, stack_mode)
+            self.R.synchronize()
+            e0, e1, e2, e3, e4 = (torch.cuda.Event(enable_timing=True) for _ in range(5))
+            e0.record(self.G)
+            self.gather_counts(0)
+            e1.record(self.G)
+            self.G.synchronize()
+            e2.record(self.G)
+            self.gather(0)
+            e3.record(self.G)
+            if self.rank == 0:
+                self.assemble(0, self.G)
+                self.ev_a[0].record(self.G)
+            e4.record(self.G)
+            self.G.synchronize()
+            g_ms.append(e0.elapsed_time(e1) + e2.elapsed_time(e3))
+            a_ms.append(e3.elapsed_time(e4))
+            sent.append(self.sent)
+        self.last, self.k, self.pending = 0, 1, None
+        self.payload_bytes = int(np.median(sent))
+        return {"gather_ms": float(np.median(g_ms)), "assemble_ms": float(np.median(a_ms)),
+                "payload_bytes": self.payload_bytes}
+
+
+def choose_payload(args, rm, W, H, rank, world, dev, stream, dist, steps=20):
+    """The N > 1 gather of the run: the payload --payload names, or with `auto`
+    the faster of rgb8 and sparse.  Each candidate gets its own weighted deal
+    (weigh_display_rank) and then runs `steps` pipelined steps between barriers;
+    the slowest rank's time decides (all ranks take the same choice).  Sparse
+    moves ~0.45x the bytes at a C3 pose but costs every sending rank a pack
+    (~11 us) and rank 0 the sky of every miss: it wins when xGMI,
+    not the render, bounds the step."""
+    import torch
+    cands = ["rgb8", "sparse"] if args.payload == "auto" else [args.payload]
+    timed = {}
+    best = None
+    for p in cands:
+        cls = SparseGather if p == "sparse" else Gather
+        g = cls(rm, W, H, rank, world, dev, p, stream, args.no_rgba)
+        g, info = weigh_display_rank(g, args, rm, dist, dev)
+        ms = None
+        if len(cands) > 1:
+            for _ in range(3):
+                g.step(args.stack_mode)
+            g.drain()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                g.step(args.stack_mode)
+            g.drain()
+            torch.cuda.synchronize(dev)
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms = float(t[0]) / steps * 1e3
+            timed[p] = {"ms_per_step": round(ms, 4), "display_share": info["display_share"]}
+        if best is None or (ms is not None and ms < best[0]):
+            best = (ms, g, info)
+        else:
+            del g
+    choice = None
+    if timed:
+        choice = {"mode": "auto", "calibration_steps": steps, "candidates": timed, "chosen": best[1].payload}
+    return best[1], best[2], choice
+
+
 def weigh_display_rank(gather, args, rm, dist, dev):
     """Balance the display rank: it also assembles the frame, so it gets a smaller
     share of the bands (distributed.weighted_owner).  Its share = 1 - (assemble
@@ -609,10 +788,10 @@ def weigh_display_rank(gather, args, rm, dist, dev):
     torch.cuda.synchronize(dev)
     if owner.count(0) == 8:   # round-robin
         info["cycle_bands"] = 0
-        return Gather(gather.rm, gather.W, gather.H, gather.rank, gather.world, dev, gather.payload, gather.R,
-                      gather.no_rgba), info
-    return Gather(gather.rm, gather.W, gather.H, gather.rank, gather.world, dev, gather.payload, gather.R,
-                  gather.no_rgba, owner=owner), info
+        return type(gather)(gather.rm, gather.W, gather.H, gather.rank, gather.world, dev, gather.payload, gather.R,
+                            gather.no_rgba), info
+    return type(gather)(gather.rm, gather.W, gather.H, gather.rank, gather.world, dev, gather.payload, gather.R,
+                        gather.no_rgba, owner=owner), info
 
 
 def bench_multidevice(args, svo, cam, W, H, scaling, build_s):

@@ -168,7 +168,8 @@ int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const 
  * outputs hits / rgba / rgba8 / compact, the normal and colour rebuilt from this
  * context's SVO replica and camera), RGBA8 words (SVO_PART_RGBA8) or 3-byte RGB
  * (SVO_PART_RGB8; rows of 3 * width bytes) or sparse hit RGB (SVO_PART_SPARSE_RGB8:
- * svo_pack_hits' layout; miss pixels get the sky computed here) -- the last three
+ * svo_pack_hits' layout, read as is -- no scan here; miss pixels get the sky computed
+ * here) -- the last three
  * rebuild the frame output rgba8 only.  Part pointers must be readable from this device (its own memory,
  * or a peer's with peer access).  skip_part (or -1): a part already rendered in
  * place.  `frame` must use the frame layout.  This is the display-side half of
@@ -179,15 +180,23 @@ int svo_assemble_frame(svo_ctx *ctx, int width, int height, const svo_band *deal
                        const void *const *parts, int part_format, int skip_part, const svo_frame *frame,
                        void *stream);
 
-/* Sparse band payload (wave ballot + prefix sum): `d_part` starts with the band's
- * hit masks (svo_frame.hitmask, n_tiles = ceil(W/8) * ceil(rows/8) words, written by
- * the render); this packs the 3-byte RGB of every hit pixel of `d_rgb8` (the band's
- * dense svo_frame.rgb8) behind them, tile by tile in lane order.  d_offsets (n_tiles +
- * 1 uint32, device) receives the hits before each tile and, last, the band's hit
- * count: the part is n_tiles * 8 + count * 3 bytes.  Misses cost nothing -- the
- * display device computes their sky.  Asynchronous. */
+/* Sparse band payload (wave ballot + prefix sum).  Part layout, n_tiles = ceil(W/8) *
+ * ceil(rows/8) of the band:
+ *   bytes [0, 8 n)             uint64 hit mask per tile (svo_frame.hitmask, written by the render)
+ *   bytes [8 n, 12 n + 4)      uint32 hits before each tile, then the band's hit count
+ *   bytes [12 n + 4, + 3 count) the 3-byte RGB of every hit pixel, tile by tile in lane order
+ * `d_part` holds the masks on entry; this writes the offsets (an exclusive scan of the
+ * masks' popcounts) and packs the hits' RGB from `d_rgb8` (the band's dense
+ * svo_frame.rgb8).  Allocate SVO_SPARSE_PART_BYTES(n_tiles, band pixels) (its tail
+ * beyond the RGB is the scan's scratch, never sent); the part to send is
+ * SVO_SPARSE_HEAD_BYTES(n_tiles) + 3 * count bytes, count = the uint32 at byte 12 n.
+ * Misses cost nothing -- the display device computes their sky.  Asynchronous. */
+#define SVO_SPARSE_HEAD_BYTES(n_tiles) (12u * (size_t)(n_tiles) + 4u)
+#define SVO_SPARSE_PART_BYTES(n_tiles, n_px)                                                          \
+    (((SVO_SPARSE_HEAD_BYTES(n_tiles) + 3u * (size_t)(n_px) + 3u) & ~(size_t)3) + 4u * (size_t)(n_tiles) + \
+     4u * (((size_t)(n_tiles) + 1023u) / 1024u))
 int svo_pack_hits(svo_ctx *ctx, int width, int height, const svo_band *band, const void *d_rgb8, void *d_part,
-                  uint32_t *d_offsets, void *stream);
+                  void *stream);
 
 /* Instrumented trace: per-ray descriptor-fetch counts (device uint32 array,
  * NVIDIASVO.compute:60-62 executions), used for the algorithmic-bytes figure

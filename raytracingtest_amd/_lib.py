@@ -39,6 +39,18 @@ SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
 PART_COMPACT, PART_RGBA8, PART_RGB8, PART_SPARSE_RGB8 = 0, 1, 2, 3
+
+
+def sparse_head_bytes(n_tiles):
+    """SVO_SPARSE_HEAD_BYTES: tile masks + tile offsets + count of a sparse part;
+    the band's hit count is the uint32 at byte 12 * n_tiles."""
+    return 12 * n_tiles + 4
+
+
+def sparse_part_bytes(n_tiles, n_px):
+    """SVO_SPARSE_PART_BYTES: capacity of a sparse part (every pixel a hit, plus
+    the scan's scratch tail)."""
+    return ((sparse_head_bytes(n_tiles) + 3 * n_px + 3) & ~3) + 4 * n_tiles + 4 * ((n_tiles + 1023) // 1024)
 STAGE_KERNEL, STAGE_ASSEMBLE = 0, 1
 
 
@@ -112,7 +124,7 @@ def lib():
         "svo_stage_time": [vp, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)],
         "svo_render_progressive": [vp, i, i, i, ctypes.c_uint32, vp, vp],
         "svo_set_band_deal": [vp, i, ctypes.POINTER(ctypes.c_uint8)],
-        "svo_pack_hits": [vp, i, i, ctypes.POINTER(SvoBand), vp, vp, vp, vp],
+        "svo_pack_hits": [vp, i, i, ctypes.POINTER(SvoBand), vp, vp, vp],
         "svo_synchronize": [vp],
         "svo_destroy": [vp],
         "svo_last_error": [],

@@ -740,6 +740,26 @@ __device__ __forceinline__ int part_of_row(const AssembleParams &a, int y, int *
     return m;
 }
 
+// One pixel of a sparse part (svo_rt.h layout): a hit's colour from the part, a miss's
+// sky computed here from the camera (the render kernel's miss branch).
+__device__ __forceinline__ uint32_t sparse_pixel(const AssembleParams &a, int m, int lr, int x, int y) {
+    const int tiles_x = (a.width + 7) / 8;
+    const int t = (lr >> 3) * tiles_x + (x >> 3);
+    const int bit = ((lr & 7) << 3) | (x & 7);
+    const unsigned long long *masks = reinterpret_cast<const unsigned long long *>(a.parts[m]);
+    const unsigned long long mk = masks[t];
+    if ((mk >> bit) & 1ull) {
+        const uint32_t *offsets = reinterpret_cast<const uint32_t *>(masks + a.n_tiles[m]);
+        const uint32_t k = offsets[t] + (uint32_t)__popcll(mk & ((1ull << bit) - 1ull));
+        const uint8_t *c = reinterpret_cast<const uint8_t *>(offsets + a.n_tiles[m] + 1) + 3 * (size_t)k;
+        return (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16) | (255u << 24);
+    }
+    float org[3], dir[3], rgb[3];
+    camera_ray(a.cam, a.width, a.height, x, y, org, dir);
+    sky(dir[1], rgb);
+    return pack_rgba8(rgb[0], rgb[1], rgb[2]);
+}
+
 __global__ __launch_bounds__(256) void assemble_kernel(AssembleParams a) {
     const int x = (int)(blockIdx.x * 256 + threadIdx.x);
     const int y = (int)blockIdx.y;
@@ -758,24 +778,8 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleParams a) {
         a.out.rgba8[dst] = (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16) | (255u << 24);
         return;
     }
-    if (a.part_format == PART_SPARSE_RGB8) {   // hit: its colour from the part; miss: the sky here
-        const int tiles_x = (a.width + 7) / 8;
-        const int t = (lr >> 3) * tiles_x + (x >> 3);
-        const int bit = ((lr & 7) << 3) | (x & 7);
-        const unsigned long long *masks = reinterpret_cast<const unsigned long long *>(a.parts[m]);
-        const unsigned long long mk = masks[t];
-        uint32_t w;
-        if ((mk >> bit) & 1ull) {
-            const uint32_t k = a.tile_offset[m][t] + (uint32_t)__popcll(mk & ((1ull << bit) - 1ull));
-            const uint8_t *c = reinterpret_cast<const uint8_t *>(masks + a.n_tiles[m]) + 3 * (size_t)k;
-            w = (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16) | (255u << 24);
-        } else {
-            float org[3], dir[3], rgb[3];
-            camera_ray(a.cam, a.width, a.height, x, y, org, dir);
-            sky(dir[1], rgb);
-            w = pack_rgba8(rgb[0], rgb[1], rgb[2]);
-        }
-        a.out.rgba8[dst] = w;
+    if (a.part_format == PART_SPARSE_RGB8) {
+        a.out.rgba8[dst] = sparse_pixel(a, m, lr, x, y);
         return;
     }
     const uint3 c = reinterpret_cast<const uint3 *>(a.parts[m])[src];
@@ -1075,81 +1079,128 @@ __global__ __launch_bounds__(256) void assemble_rgba8_kernel(AssembleParams a) {
                             (w1 >> 16) | ((w2 & 0xFFu) << 16) | A, (w2 >> 8) | A);
         return;
     }
+    if (a.part_format == PART_SPARSE_RGB8) {   // 4 pixels of one tile row: one mask, one offset
+        const int x = 4 * q;
+        dst[q] = make_uint4(sparse_pixel(a, m, lr, x, y), sparse_pixel(a, m, lr, x + 1, y),
+                            sparse_pixel(a, m, lr, x + 2, y), sparse_pixel(a, m, lr, x + 3, y));
+        return;
+    }
     const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(a.parts[m]) +
                                                        (size_t)lr * (size_t)a.width);
     dst[q] = src[q];
 }
 
 // ------------------------------------------------------ sparse hit payload
-// Exclusive scan of the tiles' hit counts: one 1024-thread workgroup walks the masks in
-// chunks of 1024 (wave prefix by shuffles, then across the 16 waves in LDS).
+// Two launches over the band's n tiles (svo_rt.h layout).
+// (1) tile_scan_local: one workgroup per chunk of SCAN_THREADS tiles scans the masks'
+//     popcounts (wave prefix by shuffles, then across the 16 waves in LDS) into the
+//     part's scratch tail: L[t] = hits before t within its chunk, S[c] = chunk c's total.
+// (2) pack_hits: one thread per pixel; a 256-pixel row segment spans 32 tiles, so at
+//     most two chunks: the workgroup sums S over the chunks before its first one and
+//     every pixel gets offset(t) = L[t] + its chunk's prefix.  A tile's first pixel
+//     writes offset(t) into the part's head (the last tile also the count), a hit pixel
+//     its 3 bytes to slot offset(t) + the tile's hit lanes before it.
 constexpr int SCAN_THREADS = 1024;
-__global__ __launch_bounds__(SCAN_THREADS) void tile_scan_kernel(const unsigned long long *__restrict__ masks, int n,
-                                                                 uint32_t *__restrict__ offsets) {
+constexpr int PACK_THREADS = 256;
+
+struct SparseLayout {   // byte offsets of a part (svo_rt.h SVO_SPARSE_*)
+    size_t offsets, rgb, scratch;
+};
+__host__ __device__ inline SparseLayout sparse_layout(int n, int n_px) {
+    SparseLayout l;
+    l.offsets = 8 * (size_t)n;
+    l.rgb = 12 * (size_t)n + 4;
+    l.scratch = (l.rgb + 3 * (size_t)n_px + 3) & ~(size_t)3;
+    return l;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void tile_scan_local_kernel(const unsigned long long *__restrict__ masks,
+                                                                       int n, uint32_t *__restrict__ local,
+                                                                       uint32_t *__restrict__ sums,
+                                                                       uint32_t *__restrict__ count) {
     __shared__ uint32_t wave_sum[SCAN_THREADS / 64];
-    __shared__ uint32_t carry;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) carry = 0;
-    __syncthreads();
-    for (int base = 0; base < n; base += SCAN_THREADS) {
-        const int i = base + tid;
-        const uint32_t c = i < n ? (uint32_t)__popcll(masks[i]) : 0u;
-        uint32_t incl = c;   // inclusive prefix within the wave
+    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int i = (int)blockIdx.x * SCAN_THREADS + tid;
+    const uint32_t c = i < n ? (uint32_t)__popcll(masks[i]) : 0u;
+    uint32_t incl = c;   // inclusive prefix within the wave
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t v = (uint32_t)__shfl_up((int)incl, d);
-            if (lane >= d) incl += v;
-        }
-        if (lane == 63) wave_sum[wave] = incl;
-        __syncthreads();
-        uint32_t before = carry;
-        for (int w = 0; w < wave; ++w) before += wave_sum[w];
-        if (i < n) offsets[i] = before + incl - c;
-        __syncthreads();
-        if (tid == SCAN_THREADS - 1) carry = before + incl;   // the last thread's inclusive total
-        __syncthreads();
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= d) incl += v;
     }
-    if (tid == 0) offsets[n] = carry;
+    if (lane == 63) wave_sum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (int w = 0; w < SCAN_THREADS / 64; ++w) {
+        const uint32_t v = wave_sum[w];
+        if (w < wave) before += v;
+        total += v;
+    }
+    if (i < n) local[i] = before + incl - c;
+    if (tid == 0) sums[blockIdx.x] = total;
+    if (n == 0 && tid == 0) *count = 0u;   // an empty band: no pack workgroup writes it
 }
 
-hipError_t launch_tile_scan(const unsigned long long *masks, int n, uint32_t *offsets, hipStream_t stream) {
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, masks, n, offsets);
-    return hipGetLastError();
-}
-
-// One thread per pixel of the band: a hit pixel copies its 3 bytes to slot
-// offsets[t] + (hit lanes before it in its tile) behind the masks.
-__global__ __launch_bounds__(256) void pack_hits_kernel(const uint8_t *__restrict__ rgb8, int width, int local_rows,
-                                                        const uint32_t *__restrict__ offsets, unsigned long long *part) {
-    const int x = (int)(blockIdx.x * 256 + threadIdx.x);
-    const int lr = (int)blockIdx.y;
-    if (x >= width || lr >= local_rows) return;
+__global__ __launch_bounds__(PACK_THREADS) void pack_hits_kernel(const uint8_t *__restrict__ rgb8, int width,
+                                                                 int local_rows, uint8_t *__restrict__ part) {
+    __shared__ uint32_t wsum[PACK_THREADS / 64];
     const int tiles_x = (width + 7) / 8;
+    const int n = tiles_x * ((local_rows + 7) / 8);
+    const SparseLayout L = sparse_layout(n, width * local_rows);
+    const unsigned long long *masks = reinterpret_cast<const unsigned long long *>(part);
+    uint32_t *offsets = reinterpret_cast<uint32_t *>(part + L.offsets);
+    const uint32_t *local = reinterpret_cast<const uint32_t *>(part + L.scratch);
+    const uint32_t *sums = local + n;
+    const int lr = (int)blockIdx.y;
+    const int x0 = (int)blockIdx.x * PACK_THREADS;
+    const int c0 = ((lr >> 3) * tiles_x + (x0 >> 3)) / SCAN_THREADS;   // the segment's first chunk
+    uint32_t v = 0;
+    for (int c = (int)threadIdx.x; c < c0; c += PACK_THREADS) v += sums[c];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const uint32_t prefix0 = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    const int x = x0 + (int)threadIdx.x;
+    if (x >= width) return;
     const int t = (lr >> 3) * tiles_x + (x >> 3);
     const int bit = ((lr & 7) << 3) | (x & 7);
-    const unsigned long long mk = part[t];
+    const unsigned long long mk = masks[t];
+    const uint32_t off = local[t] + prefix0 + (t / SCAN_THREADS > c0 ? sums[c0] : 0u);
+    if (bit == 0) {
+        offsets[t] = off;
+        if (t == n - 1) offsets[n] = off + (uint32_t)__popcll(mk);   // the band's hit count
+    }
     if (!((mk >> bit) & 1ull)) return;
-    const int n_tiles = tiles_x * ((local_rows + 7) / 8);
-    const uint32_t k = offsets[t] + (uint32_t)__popcll(mk & ((1ull << bit) - 1ull));
-    const uint8_t *s = rgb8 + 3 * ((size_t)lr * (size_t)width + (size_t)x);
-    uint8_t *d = reinterpret_cast<uint8_t *>(part + n_tiles) + 3 * (size_t)k;
-    d[0] = s[0];
-    d[1] = s[1];
-    d[2] = s[2];
+    const uint32_t k = off + (uint32_t)__popcll(mk & ((1ull << bit) - 1ull));
+    const uint8_t *src = rgb8 + 3 * ((size_t)lr * (size_t)width + (size_t)x);
+    uint8_t *dst = part + L.rgb + 3 * (size_t)k;
+    dst[0] = src[0];
+    dst[1] = src[1];
+    dst[2] = src[2];
 }
 
-hipError_t launch_pack_hits(const uint8_t *rgb8, int width, int local_rows, const uint32_t *offsets, void *part,
-                            hipStream_t stream) {
-    if (width <= 0 || local_rows <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((width + 255) / 256), (unsigned)local_rows);
-    hipLaunchKernelGGL(pack_hits_kernel, grid, dim3(256), 0, stream, rgb8, width, local_rows, offsets,
-                       reinterpret_cast<unsigned long long *>(part));
+hipError_t launch_pack_hits(const uint8_t *rgb8, int width, int local_rows, void *part, hipStream_t stream) {
+    if (width <= 0 || local_rows < 0) return hipSuccess;
+    const int n = ((width + 7) / 8) * ((local_rows + 7) / 8);
+    const int chunks = (n + SCAN_THREADS - 1) / SCAN_THREADS;
+    uint8_t *p = reinterpret_cast<uint8_t *>(part);
+    const SparseLayout L = sparse_layout(n, width * local_rows);
+    uint32_t *local = reinterpret_cast<uint32_t *>(p + L.scratch);
+    hipLaunchKernelGGL(tile_scan_local_kernel, dim3(chunks > 0 ? chunks : 1), dim3(SCAN_THREADS), 0, stream,
+                       reinterpret_cast<const unsigned long long *>(p), n, local, local + n,
+                       reinterpret_cast<uint32_t *>(p + L.offsets) + n);
+    if (local_rows > 0) {
+        const dim3 grid((unsigned)((width + PACK_THREADS - 1) / PACK_THREADS), (unsigned)local_rows);
+        hipLaunchKernelGGL(pack_hits_kernel, grid, dim3(PACK_THREADS), 0, stream, rgb8, width, local_rows, p);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
     if (a.width <= 0 || a.height <= 0) return hipSuccess;
-    if ((a.part_format == PART_RGBA8 || a.part_format == PART_RGB8) && a.width % 4 == 0) {
+    if ((a.part_format == PART_RGBA8 || a.part_format == PART_RGB8 || a.part_format == PART_SPARSE_RGB8) &&
+        a.width % 4 == 0) {
         const dim3 grid((unsigned)((a.width / 4 + 255) / 256), (unsigned)a.height);
         hipLaunchKernelGGL(assemble_rgba8_kernel, grid, dim3(256), 0, stream, a);
         return hipGetLastError();

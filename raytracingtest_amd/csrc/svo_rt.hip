@@ -140,12 +140,6 @@ struct svo_ctx {
     hipStream_t scratch_stream = nullptr;
     bool scratch_valid = false;
     hipEvent_t switch_event = nullptr;
-    // sparse-part assembles: the parts' tile offsets (scanned here), ordered like the scratch
-    uint32_t *d_sparse_off = nullptr;
-    size_t sparse_off_cap = 0;
-    hipStream_t sparse_stream = nullptr;
-    bool sparse_valid = false;
-    hipEvent_t sparse_event = nullptr;
     // multi-device context (svo_create_multi); empty for a single-device one
     std::vector<svo_ctx *> members;
     std::vector<Peer> peers;
@@ -328,8 +322,6 @@ int ensure_accum(svo_ctx *ctx, int width, int height) {
     if (ctx->d_accum && ctx->accum_w == width && ctx->accum_h == height) return SVO_OK;
     HIP_TRY(hipDeviceSynchronize());   // an earlier asynchronous launch may still use the old frame
     if (ctx->d_accum) hipFree(ctx->d_accum);
-    if (ctx->d_sparse_off) hipFree(ctx->d_sparse_off);
-    if (ctx->sparse_event) hipEventDestroy(ctx->sparse_event);
     if (ctx->d_accum8) hipFree(ctx->d_accum8);
     ctx->d_accum = nullptr;
     ctx->d_accum8 = nullptr;
@@ -591,39 +583,12 @@ int assemble(svo_ctx *ctx, int width, int height, const Deal &deal, int n_parts,
     int rc = take_events(ctx, STAGE_ASSEMBLE, &ev0, &ev1);
     if (rc) return rc;
     if (ev0) HIP_TRY(hipEventRecord(ev0, s));
-    if (part_format == SVO_PART_SPARSE_RGB8) {   // every part's tile offsets (prefix sums of its masks)
+    if (part_format == SVO_PART_SPARSE_RGB8) {   // the parts' tile counts (their offsets travel in them)
         const int tiles_x = (width + 7) / 8;
-        size_t need = 0;
         for (int m = 0; m < n_parts; ++m) {
             Deal dm = deal;
             dm.rank = m;
             a.n_tiles[m] = (uint32_t)(tiles_x * ((band_rows_local(height, dm) + 7) / 8));
-            need += a.n_tiles[m] + 1;
-        }
-        if (ctx->sparse_off_cap < need) {
-            HIP_TRY(hipDeviceSynchronize());   // an earlier assemble may still read the old offsets
-            if (ctx->d_sparse_off) hipFree(ctx->d_sparse_off);
-            ctx->d_sparse_off = nullptr;
-            ctx->sparse_off_cap = 0;
-            HIP_TRY(hipMalloc(&ctx->d_sparse_off, need * sizeof(uint32_t)));
-            ctx->sparse_off_cap = need;
-        }
-        if (ctx->sparse_valid && ctx->sparse_stream != s) {   // the offsets buffer is shared: order its users
-            if (!ctx->sparse_event) HIP_TRY(hipEventCreateWithFlags(&ctx->sparse_event, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(ctx->sparse_event, ctx->sparse_stream));
-            HIP_TRY(hipStreamWaitEvent(s, ctx->sparse_event, 0));
-        }
-        ctx->sparse_stream = s;
-        ctx->sparse_valid = true;
-        size_t at = 0;
-        for (int m = 0; m < n_parts; ++m) {
-            a.tile_offset[m] = ctx->d_sparse_off + at;
-            if (m != skip_part && a.n_tiles[m] > 0) {
-                hipError_t e = svo::launch_tile_scan(reinterpret_cast<const unsigned long long *>(parts[m]),
-                                                     (int)a.n_tiles[m], ctx->d_sparse_off + at, s);
-                if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile scan launch: ") + hipGetErrorString(e));
-            }
-            at += a.n_tiles[m] + 1;
         }
     }
     hipError_t e = svo::launch_assemble(a, s);
@@ -756,8 +721,6 @@ int destroy_single(svo_ctx *ctx) {
     if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
     if (ctx->d_accum) hipFree(ctx->d_accum);
-    if (ctx->d_sparse_off) hipFree(ctx->d_sparse_off);
-    if (ctx->sparse_event) hipEventDestroy(ctx->sparse_event);
     if (ctx->d_accum8) hipFree(ctx->d_accum8);
     for (Sched &q : ctx->sched) {
         free_sched(q);
@@ -1108,19 +1071,17 @@ int svo_render_device(svo_ctx *ctx, int width, int height, int stack_mode, const
 }
 
 int svo_pack_hits(svo_ctx *ctx, int width, int height, const svo_band *band, const void *d_rgb8, void *d_part,
-                  uint32_t *d_offsets, void *stream) {
-    if (!ctx || !d_rgb8 || !d_part || !d_offsets) return fail(SVO_ERR_ARG, "null argument");
+                  void *stream) {
+    if (!ctx || !d_rgb8 || !d_part) return fail(SVO_ERR_ARG, "null argument");
     if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
     svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
     Deal d;
     int rc = check_band(band, height, &d);
     if (rc) return rc;
     const int rows = band_rows_local(height, d);
-    const int n_tiles = ((width + 7) / 8) * ((rows + 7) / 8);
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
-    hipError_t e = svo::launch_tile_scan(reinterpret_cast<const unsigned long long *>(d_part), n_tiles, d_offsets, s);
-    if (e == hipSuccess) e = svo::launch_pack_hits(reinterpret_cast<const uint8_t *>(d_rgb8), width, rows, d_offsets, d_part, s);
+    hipError_t e = svo::launch_pack_hits(reinterpret_cast<const uint8_t *>(d_rgb8), width, rows, d_part, s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("pack hits launch: ") + hipGetErrorString(e));
     return SVO_OK;
 }

@@ -101,10 +101,9 @@ struct AssembleParams {
     int cycle;
     uint8_t owner[MAX_CYCLE], idx[MAX_CYCLE];
     int cnt[MAX_PARTS];
-    // PART_SPARSE_RGB8: part m = [n_tiles[m] hit masks (u64)][3-byte RGB of the hit pixels, tile
-    // by tile, lanes in order]; tile_offset[m][t] = hits before tile t (svo_rt.hip scans them)
+    // PART_SPARSE_RGB8: part m = [n_tiles[m] hit masks (u64)][n_tiles[m] + 1 tile offsets (u32)]
+    // [3-byte RGB of the hit pixels, tile by tile, lanes in order] (svo_rt.h, svo_pack_hits)
     uint32_t n_tiles[MAX_PARTS];
-    const uint32_t *tile_offset[MAX_PARTS];
     Outputs out;          // frame layout
 };
 
@@ -124,13 +123,10 @@ hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32
 
 hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream);
 
-// Exclusive prefix sum of the hit masks' popcounts (n tiles; one workgroup): offsets[t],
-// and the total in offsets[n].
-hipError_t launch_tile_scan(const unsigned long long *masks, int n, uint32_t *offsets, hipStream_t stream);
-// Sparse hit payload of a band: copy the 3-byte RGB of every hit pixel (per the masks at the
-// head of `part`) behind the masks, tile by tile (offsets from launch_tile_scan).
-hipError_t launch_pack_hits(const uint8_t *rgb8, int width, int local_rows, const uint32_t *offsets, void *part,
-                            hipStream_t stream);
+// Sparse hit payload of a band (svo_rt.h layout): `part` holds the n tile masks; write the
+// tile offsets (exclusive scan of the masks' popcounts, count last) and pack the 3-byte RGB
+// of every hit pixel of the band's dense `rgb8` behind them.  Three launches.
+hipError_t launch_pack_hits(const uint8_t *rgb8, int width, int local_rows, void *part, hipStream_t stream);
 
 // Display RGBA8 words of an RGBA32F frame (svo_render_progressive).
 hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int num_cus, hipStream_t stream);

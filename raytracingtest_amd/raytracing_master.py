@@ -217,13 +217,14 @@ class RaytracingMaster:
                                             part_format, skip_part, ctypes.byref(f), stream),
               "svo_assemble_frame")
 
-    def pack_hits(self, width, height, band, rgb8, part, offsets, stream=None):
-        """Sparse band payload: `part` (device pointer) starts with the band's hit
-        masks (render_frame(hitmask=part)); pack the RGB of its hit pixels from the
-        band's dense `rgb8` behind them.  offsets (n_tiles + 1 uint32, device)
-        receives the per-tile hit offsets and, last, the band's hit count."""
+    def pack_hits(self, width, height, band, rgb8, part, stream=None):
+        """Sparse band payload (svo_rt.h layout): `part` (device pointer, capacity
+        _lib.sparse_part_bytes) starts with the band's hit masks
+        (render_frame(hitmask=part)); write the tile offsets and the hit count
+        behind them and pack the RGB of the hit pixels from the band's dense
+        `rgb8` after that."""
         b = ctypes.byref(make_band(band if band is not None else (self.band_rows, 0, 1)))
-        check(_lib.lib().svo_pack_hits(self._ctx, width, height, b, rgb8, part, offsets, stream), "svo_pack_hits")
+        check(_lib.lib().svo_pack_hits(self._ctx, width, height, b, rgb8, part, stream), "svo_pack_hits")
 
     def count_fetches_device(self, width, height, fetch_ptr, stack_mode=STACK_HLSL, band=None, stream=None):
         b = None if band is None else ctypes.byref(make_band(band))

@@ -360,15 +360,14 @@ def test_weighted_deal_parts_match_oracle(torch, oracle_mod, world, share):
 
 def _sparse_part(torch, m, w, h, band):
     """A rank's sparse payload: render the dense RGB + the tile hit masks (at the
-    part's head), then svo_pack_hits.  Returns (part, offsets, n_tiles)."""
+    part's head), then svo_pack_hits.  Returns (part, offsets incl. the count, n_tiles)."""
     rows = len(band_rows(h, band))
     n_tiles = ((w + 7) // 8) * ((rows + 7) // 8)
     dense = torch.full((max(rows * w, 1) * 3,), 0xA5, dtype=torch.uint8, device="cuda")
-    part = torch.full((n_tiles * 8 + rows * w * 3 + 8,), 0x5A, dtype=torch.uint8, device="cuda")
-    offs = torch.full((n_tiles + 1,), -1, dtype=torch.int32, device="cuda")
+    part = torch.full((_lib.sparse_part_bytes(n_tiles, rows * w),), 0x5A, dtype=torch.uint8, device="cuda")
     m.render_frame(w, h, rgb8=dense.data_ptr(), hitmask=part.data_ptr(), band=band)
-    m.pack_hits(w, h, band, dense.data_ptr(), part.data_ptr(), offs.data_ptr())
-    return part, offs, n_tiles
+    m.pack_hits(w, h, band, dense.data_ptr(), part.data_ptr())
+    return part, part[8 * n_tiles:12 * n_tiles + 4].view(torch.int32), n_tiles
 
 
 @pytest.mark.parametrize("world,share", [(1, None), (2, None), (3, 0.5), (8, 0.75)])
@@ -381,7 +380,7 @@ def test_sparse_parts_match_oracle(torch, oracle_mod, world, share):
     from raytracingtest_amd.distributed import weighted_owner
     svo = build_menger(7)
     cam = overview_camera()
-    w, h = (262, 203) if world == 3 else (264, 200)
+    w, h = {1: (1000, 600), 3: (262, 203)}.get(world, (264, 200))   # 1000x600: 9,375 tiles, a 10-chunk scan
     ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
     ref_hit = ((ref_hits["flags"] & 1) != 0).reshape(h, w)
     ref_rgb = oracle_mod.pack_rgba8(ref_rgba).view(np.uint8).reshape(h, w, 4)[:, :, :3]
@@ -397,7 +396,7 @@ def test_sparse_parts_match_oracle(torch, oracle_mod, world, share):
             parts.append(part)
             m.synchronize()
             ys = band_rows(h, band)
-            count = int(offs[-1].item())
+            count = int(offs[n_tiles].item())
             assert count == int(ref_hit[ys].sum())
             # the packed colours: tiles in order, lanes (row-major 8x8) within a tile
             tx = (w + 7) // 8
@@ -408,7 +407,8 @@ def test_sparse_parts_match_oracle(torch, oracle_mod, world, share):
                     ly, lx = by * 8 + lane // 8, bx * 8 + lane % 8
                     if ly < len(ys) and lx < w and ref_hit[ys[ly], lx]:
                         want.append(ref_rgb[ys[ly], lx])
-            got = part[n_tiles * 8:n_tiles * 8 + 3 * count].cpu().numpy().reshape(-1, 3)
+            head = _lib.sparse_head_bytes(n_tiles)
+            got = part[head:head + 3 * count].cpu().numpy().reshape(-1, 3)
             assert np.array_equal(got, np.array(want, np.uint8).reshape(-1, 3))
         b = _bufs(torch, w * h)
         m.assemble_frame(w, h, [p.data_ptr() for p in parts], _lib.PART_SPARSE_RGB8, rgba8=b["rgba8"].data_ptr(),
@@ -423,6 +423,46 @@ def test_sparse_parts_match_oracle(torch, oracle_mod, world, share):
         _check(b2, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
         with pytest.raises(SvoError):   # sparse parts rebuild only display words
             m.assemble_frame(w, h, [p.data_ptr() for p in parts], _lib.PART_SPARSE_RGB8, hits=b["hits"].data_ptr())
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("w,rows", [(7680, 1080), (64, 8), (13, 3), (1000, 7)])
+def test_pack_hits_random_masks(torch, w, rows):
+    """svo_pack_hits on random masks and colours (no render): the offsets are the
+    exclusive prefix sum of the tiles' popcounts over a multi-chunk scan (7680 x
+    1080: 129,600 tiles), the count is the total, and the packed bytes are the hit
+    pixels' RGB in tile / lane order; pixels outside the band's width or rows
+    never count."""
+    rng = np.random.default_rng(w * 31 + rows)
+    tx, ty = (w + 7) // 8, (rows + 7) // 8
+    n_tiles = tx * ty
+    lane_ok = np.zeros((ty, tx, 64), bool)
+    for lane in range(64):
+        ly, lx = np.arange(ty)[:, None] * 8 + lane // 8, np.arange(tx)[None, :] * 8 + lane % 8
+        lane_ok[:, :, lane] = (ly < rows) & (lx < w)
+    density = rng.uniform(0.0, 1.0, (ty, tx, 1))
+    bits = (rng.uniform(0.0, 1.0, (ty, tx, 64)) < density) & lane_ok
+    masks = (bits.astype(np.uint64) << np.arange(64, dtype=np.uint64)).sum(axis=2, dtype=np.uint64).reshape(-1)
+    rgb = rng.integers(0, 256, (rows, w, 3), dtype=np.uint8)
+    m = RaytracingMaster(device=0, capacity_nodes=16)
+    try:
+        part = torch.full((_lib.sparse_part_bytes(n_tiles, rows * w),), 0xEE, dtype=torch.uint8, device="cuda")
+        part[:n_tiles * 8] = torch.from_numpy(masks.view(np.uint8)).cuda()
+        dense = torch.from_numpy(rgb.reshape(-1)).cuda()
+        m.pack_hits(w, rows, (8, 0, 1), dense.data_ptr(), part.data_ptr())
+        m.synchronize()
+        offs = part[8 * n_tiles:12 * n_tiles + 4].view(torch.int32)
+        cnt = bits.reshape(n_tiles, 64).sum(axis=1)
+        want_off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+        got_off = offs[:n_tiles + 1].cpu().numpy().astype(np.int64)
+        assert np.array_equal(got_off, want_off)
+        t, lane = np.nonzero(bits.reshape(n_tiles, 64))
+        ys = (t // tx) * 8 + lane // 8
+        xs = (t % tx) * 8 + lane % 8
+        head = _lib.sparse_head_bytes(n_tiles)
+        got = part[head:head + 3 * int(want_off[-1])].cpu().numpy().reshape(-1, 3)
+        assert np.array_equal(got, rgb[ys, xs])
     finally:
         m.close()
 
@@ -449,10 +489,10 @@ def test_sparse_parts_extremes(torch, oracle_mod, pose):
         m.UpdateShaderParameters(cam, w, h)
         parts = []
         for r in range(2):
-            part, offs, _ = _sparse_part(torch, m, w, h, (8, r, 2))
+            part, offs, nt = _sparse_part(torch, m, w, h, (8, r, 2))
             parts.append(part)
             m.synchronize()
-            assert int(offs[-1].item()) == (0 if pose == "all_miss" else len(band_rows(h, (8, r, 2))) * w)
+            assert int(offs[nt].item()) == (0 if pose == "all_miss" else len(band_rows(h, (8, r, 2))) * w)
         b = _bufs(torch, w * h)
         m.assemble_frame(w, h, [p.data_ptr() for p in parts], _lib.PART_SPARSE_RGB8, rgba8=b["rgba8"].data_ptr())
         m.synchronize()
