@@ -647,192 +647,6 @@ __global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int t
     store_outputs(p.out, out_index(p, lr, gy, x), o);
 }
 
-// ------------------------------------------------------------- refill experiment
-// atomic-free lane refill.  Wave w owns a static
-// list of K 8x8 tiles (64 K rays) and starts with the first 64; at the end of a trip,
-// once at least T lanes are idle (or all are) and rays remain, the lanes whose rays
-// finished write their outputs and take the list's next rays (ballot + mbcnt rank, no
-// atomics).  The trip is trace_lean's (same arithmetic, bit-exact) with the octant
-// per lane.  Lists: K neighbouring tiles in raster order, or (refill_paired, with the
-// global heaviest-first tile_order) the ranks w, w + G, w + 2G, ... of that order, so
-// a wave pairs one heavy tile with lighter ones.  Primary rays only; the wave trip cap
-// counts the wave's trips, not one ray's.  Env SVO_REFILL=K,T[,paired]: measured, not
-// the default.
-template <int MODE, bool FA>
-__global__ __launch_bounds__(TILE) void render_refill_kernel(LaunchParams p, int tiles_x, int n_tiles) {
-    extern __shared__ uint2 stk_base[];
-    const int lane = (int)threadIdx.x;
-    const int K = p.refill_k, T = p.refill_t;
-    const int G = (int)gridDim.x, w = (int)blockIdx.x;
-    const bool paired = p.refill_paired && p.tile_order;
-    const int n_list = 64 * K;
-    uint2 *stk = stk_base + lane;
-    constexpr int STRIDE = TILE;
-    const int slots = p.slots;
-    const int scale_lo = S_MAX - slots;
-    const uint32_t stk_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
-    constexpr uint32_t SLOT = (uint32_t)(STRIDE * sizeof(uint2));
-    constexpr int SLOT_SH = 23 - 9;
-    const uint32_t push_base = stk_addr - (uint32_t)(104 + scale_lo) * SLOT;
-    const uint2 *stk_pop = stk - (127 + scale_lo) * STRIDE;
-    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots);
-
-    FRay r;
-    int oct = 16, sh = 0;
-    int x = 0, lr = 0, gy = 0;   // the lane's pixel
-    // Ray q of the wave's list into this lane (a valid ray state even when q is no
-    // pixel of the band: then the lane stays idle).  Returns whether it is a pixel.
-    auto take = [&](int q) -> bool {
-        const int j = q >> 6;
-        int t;
-        if (paired) {
-            const int rk = w + j * G;
-            t = rk < n_tiles ? (int)p.tile_order[rk] : -1;
-        } else {
-            t = w * K + j < n_tiles ? w * K + j : -1;
-        }
-        bool ok = t >= 0;
-        x = ok ? (t % tiles_x) * 8 + (q & 7) : 0;
-        lr = ok ? (t / tiles_x) * 8 + ((q >> 3) & 7) : 0;
-        ok = ok && x < p.width && lr < p.local_rows;
-        if (!ok) x = lr = 0;
-        gy = global_row(p, lr);
-        float org[3], dir[3];
-        camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
-        Ray ray;
-        setup_ray(org, dir, ray);
-        to_fray(ray, r);
-        // per-lane values (the LLVM uniformity bug trace_lean works round: constants
-        // assigned under a lane mask would otherwise be kept in SGPRs)
-        asm volatile("" : "+v"(r.parent), "+v"(r.cd16), "+v"(r.first), "+v"(r.flags));
-        for (int s = 0; s <= slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
-        oct = r.octant_mask | 16;
-        sh = r.idx ^ oct;
-        return ok;
-    };
-    lmask ovf = 0;
-    auto finish = [&]() {
-        r.idx = sh ^ oct;
-        if (LM_ON(ovf)) r.flags |= 4u;
-        Ray ray;
-        from_fray(r, ray);
-        Record o;
-        record(p, ray, x, gy, o);
-        store_outputs(p.out, out_index(p, lr, gy, x), o);
-    };
-    int ptr = 64;   // wave-uniform: the list's next ray
-    lmask act = LM_OF(take(lane));
-    lmask live = act;   // lanes holding a ray whose outputs are still to write
-    lmask cached = 0;
-    int it = 0;
-    asm volatile("" : "+v"(r.parent), "+v"(r.cd16), "+v"(r.first));
-    lmask go;
-    do {
-        asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
-        const lmask need = FA ? ~(lmask)0 : act & ~cached;
-        if (FA || LM_ON(need)) {
-            const uint2 nd = *(const uint2 *)((const char *)p.nodes + (uint32_t)(r.parent << 3));
-            r.cd16 = nd.x;
-            r.first = nd.y;
-        }
-        cached |= need;
-        const float tx = r.px * r.cx - r.bx;
-        const float ty = r.py * r.cy - r.by;
-        const float tz = r.pz * r.cz - r.bz;
-        const float tc_max = fminf(fminf(tx, ty), tz);
-        const float tv_max = vmin(r.t_max, tc_max);
-        const float half = r.sexp * 0.5f;
-        const lmask cx = LM_OF(center(half, r.cx, tx) > r.t_min);
-        const lmask cy = LM_OF(center(half, r.cy, ty) > r.t_min);
-        const lmask cz = LM_OF(center(half, r.cz, tz) > r.t_min);
-        const lmask lx = LM_OF(tx <= tc_max), ly = LM_OF(ty <= tc_max), lz = LM_OF(tz <= tc_max);
-        const lmask in_span = LM_OF(r.t_min <= tv_max), below_h = LM_OF(tc_max < r.h);
-        const uint32_t cm = r.cd16 << sh;
-        const lmask descend = act & LM_OF((int32_t)cm < 0) & in_span;
-        const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
-        const lmask hit = descend & leaf;
-        const lmask store = descend & ~leaf & below_h;
-        const lmask push = descend & ~leaf;
-        const lmask adv = act & ~descend;
-        if (LM_ON(store)) {
-            const uint32_t a = push_base + (__float_as_uint(r.sexp) >> SLOT_SH);
-            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(r.t_max) : "memory");
-        }
-        const lmask sx = adv & lx;
-        const lmask sy = adv & ly;
-        const lmask sz = adv & lz;
-        const float se = r.sexp;
-        const float delta = LM_ON(push) ? half : -se;
-        const float ox = r.px, oy = r.py, oz = r.pz;
-        const lmask mvx = (push & cx) | sx, mvy = (push & cy) | sy, mvz = (push & cz) | sz;
-        const float qx = r.px + (LM_ON(mvx) ? delta : 0.0f);
-        const float qy = r.py + (LM_ON(mvy) ? delta : 0.0f);
-        const float qz = r.pz + (LM_ON(mvz) ? delta : 0.0f);
-        const int mv = lanes_to_idx(mvx, mvy, mvz);
-        const lmask pop = adv & LM_OF((mv & ~(sh ^ oct)) != 0);
-        const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
-        sh = (LM_ON(push) ? oct : sh) ^ mv;
-        if (LM_ON(push)) {
-            r.parent = child;
-            r.h = tc_max;
-            r.t_max = tv_max;
-            r.sexp = half;
-        }
-        r.t_min = LM_ON(adv) ? tc_max : r.t_min;
-        cached &= ~(push | pop);
-        r.px = qx; r.py = qy; r.pz = qz;
-        lmask out = 0;
-        if (pop != 0) {
-            const uint32_t diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) |
-                                  (__float_as_uint(oy) ^ __float_as_uint(qy)) |
-                                  (__float_as_uint(oz) ^ __float_as_uint(qz));
-            const uint32_t fd = __float_as_uint((float)diff);
-            const uint32_t ef = __builtin_amdgcn_ubfe(fd, 23, 8);
-            const int scale = (int)ef - 127;
-            const uint2 e = stk_pop[min(ef, e_max) * STRIDE];
-            uint32_t pa = e.x, tm = e.y;
-            if (MODE == 0) tm = (uint32_t)cvt_i32((float)(int32_t)tm);
-            const uint32_t keep = 0xFFFFFFFFu << scale;
-            const uint32_t bx_ = __builtin_amdgcn_ubfe(__float_as_uint(qx), scale, 1);
-            const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
-            const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
-            const bool pl = LM_ON(pop);
-            r.sexp = pl ? __uint_as_float((ef << 23) - (23u << 23)) : r.sexp;
-            r.parent = pl ? pa : r.parent;
-            r.t_max = pl ? __uint_as_float(tm) : r.t_max;
-            const uint32_t k = pl ? keep : 0xFFFFFFFFu;
-            r.px = __uint_as_float(__float_as_uint(r.px) & k);
-            r.py = __uint_as_float(__float_as_uint(r.py) & k);
-            r.pz = __uint_as_float(__float_as_uint(r.pz) & k);
-            r.h = pl ? 0.0f : r.h;
-            sh = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) ^ oct : sh;
-            out = pop & LM_OF(scale >= S_MAX);
-        }
-        act &= ~(hit | out);
-        const lmask idle = ~act;
-        if (ptr < n_list && (__popcll(idle) >= T || act == 0)) {   // refill the idle lanes
-            const lmask fin = live & idle;
-            if (LM_ON(fin)) finish();
-            live &= ~fin;
-            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-            const int q = ptr + rank;
-            const lmask give = idle & LM_OF(q < n_list);
-            bool ok = false;
-            if (LM_ON(give)) ok = take(q);
-            const lmask got = give & LM_OF(ok);
-            ptr += __popcll(give);
-            act |= got;
-            live |= got;
-            cached &= ~give;
-            ovf &= ~give;
-        }
-        go = it < MAX_ITERS ? (act | (ptr < n_list ? ~(lmask)0 : (lmask)0)) : (lmask)0;
-    } while (go != 0);
-    if (LM_ON(act)) r.flags |= 2u;   // still tracing at the wave's trip cap
-    if (LM_ON(live)) finish();
-}
-
 // ------------------------------------------------------------- shadow pass
 // Two-pass form (env SVO_FUSED_SHADOWS=0): one shadow ray per primary hit, read
 // back from the primary pass's records (svo_hit or compact); an occluded pixel
@@ -1008,14 +822,6 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
     const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
     const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2);   // + the spare slot
     const dim3 grid((unsigned)(bx * by)), block(TILE);
-    if (!COUNT && p.refill_k > 0 && p.shadows != 2 && !p.guard && !p.wave_log && !p.out.hitmask) {
-        const int waves = (bx * by + p.refill_k - 1) / p.refill_k;   // refill experiment (env SVO_REFILL)
-        if (p.fetch_all)
-            hipLaunchKernelGGL((render_refill_kernel<MODE, true>), dim3((unsigned)waves), block, lds, stream, p, bx, bx * by);
-        else
-            hipLaunchKernelGGL((render_refill_kernel<MODE, false>), dim3((unsigned)waves), block, lds, stream, p, bx, bx * by);
-        return hipGetLastError();
-    }
     if (COUNT)
         hipLaunchKernelGGL((render_tile_kernel<MODE, true>), grid, block, lds, stream, p, bx);
     else if (p.shadows == 2) {   // shadow pass fused into the primary launch

@@ -500,14 +500,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             p.shadow_order = q->shadow_key == key ? q->shadow_order : nullptr;
         }
     }
-    if (const char *rf = std::getenv("SVO_REFILL")) {   // refill experiment: K,T[,paired]
-        int k = 0, t = 0, pr = 0;
-        if (std::sscanf(rf, "%d,%d,%d", &k, &t, &pr) >= 2 && k >= 1 && k <= 64 && t >= 1 && t <= 64) {
-            p.refill_k = k;
-            p.refill_t = t;
-            p.refill_paired = pr != 0 && p.xcd_remap == 0;
-        }
-    }
     const char *log_path = std::getenv("SVO_WAVE_LOG");
     const size_t n_wave = (size_t)n_tiles;
     if (log_path && !p.out.fetches) {

@@ -81,8 +81,6 @@ struct LaunchParams {
     // The same cost-ordered dispatch for the two-pass shadow form (its own costs and order).
     const uint32_t *shadow_order;
     uint16_t *shadow_cost;
-    // refill experiment (env SVO_REFILL=K,T[,paired]; svo_kernel.hip render_refill_kernel): 0 = off
-    int refill_k, refill_t, refill_paired;
 };
 
 // Re-interleave the band parts of a split frame on the display device

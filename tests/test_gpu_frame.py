@@ -501,34 +501,6 @@ def test_sparse_parts_extremes(torch, oracle_mod, pose):
         m.close()
 
 
-@pytest.mark.parametrize("refill", ["2,16", "4,32", "3,8,1", "8,64"])
-def test_refill_experiment_matches_oracle(torch, oracle_mod, monkeypatch, refill):
-    """The atomic-free lane-refill kernel (env SVO_REFILL=K,T[,paired]; VERDICT r1
-    item 9, measured in DESIGN.md 5.1, not the default) writes the same hit
-    records, Result and display words as the oracle: neighbouring-tile lists and
-    cost-paired lists (those need the raster tile order: SVO_XCD_REMAP=0)."""
-    monkeypatch.setenv("SVO_REFILL", refill)
-    if refill.count(",") == 2:
-        monkeypatch.setenv("SVO_XCD_REMAP", "0")
-    svo = build_menger(8)
-    for cam, (w, h) in ((overview_camera(), (333, 201)),
-                        (Camera(position=(30.0, 12.0, -25.0), rotation=look_rotation((-30.0, -12.0, 25.0))),
-                         (256, 192))):
-        ref_hits, ref_rgba, ref_pos, ref_vox = _oracle(oracle_mod, svo, cam, w, h)
-        m = RaytracingMaster(device=0, capacity_nodes=len(svo))
-        try:
-            m.SetSVOBuffer(svo)
-            m.UpdateShaderParameters(cam, w, h)
-            for _ in range(3):   # the paired lists use the order the first launches build
-                b = _bufs(torch, w * h)
-                m.render_frame(w, h, **_ptrs(b, ("hits", "rgba", "rgba8", "position", "voxel")))
-                m.synchronize()
-                _check(b, oracle_mod, ref_hits, ref_rgba, ref_pos, ref_vox,
-                       keys=("hits", "rgba", "rgba8", "position", "voxel"))
-        finally:
-            m.close()
-
-
 @pytest.mark.parametrize("n_streams", [2, 6])
 def test_two_streams_every_pixel_written(torch, oracle_mod, n_streams):
     """Launches of one context cycling over several streams (advisor r1): each
