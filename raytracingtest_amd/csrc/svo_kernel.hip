@@ -718,6 +718,60 @@ __global__ __launch_bounds__(TILE) void shadow_tile_kernel(LaunchParams p, int t
     }
 }
 
+// Compacted form (env SVO_SHADOW_COMPACT=1): the primary pass's
+// hit masks are scanned and its hit pixels packed into a dense list in tile order
+// (pack_hits_kernel<INDEX>, the sparse payload's ballot + prefix sum), and one wave
+// traces 64 consecutive list entries.  The grid covers every pixel; waves past the
+// device-side hit count return at once.
+template <int MODE, bool FA = false>
+__global__ __launch_bounds__(TILE) void shadow_list_kernel(LaunchParams p, const uint32_t *__restrict__ list,
+                                                           const uint32_t *__restrict__ count) {
+    extern __shared__ uint2 stk_base[];
+    const int lane = (int)threadIdx.x;
+    const uint32_t k = blockIdx.x * TILE + (uint32_t)lane;
+    const uint32_t n = *count;
+    if (blockIdx.x * TILE >= n || k >= n) return;
+    const uint32_t px = list[k];
+    const int x = (int)(px % (uint32_t)p.width), lr = (int)(px / (uint32_t)p.width);
+    const int gy = global_row(p, lr);
+    const size_t i = out_index(p, lr, gy, x);
+    uint32_t w1, w2;
+    float nrm[3];
+    if (p.out.hits) {
+        const uint2 *rec = reinterpret_cast<const uint2 *>(p.out.hits + i);
+        const uint2 a = rec[0], b = rec[1], c = rec[2];
+        w1 = a.y; w2 = b.x;
+        nrm[0] = __uint_as_float(b.y); nrm[1] = __uint_as_float(c.x); nrm[2] = __uint_as_float(c.y);
+    } else {
+        const uint3 c = reinterpret_cast<const uint3 *>(p.out.compact)[i];
+        w1 = c.y; w2 = c.z;
+        const uint2 a = p.att[c.x];
+        decode_normal(a.y >> 16, nrm);
+        normalize3(nrm);
+    }
+    float so[3], sd[3];
+    shadow_ray(p, x, gy, w2, __float_as_uint(nrm[0]), __float_as_uint(nrm[1]), __float_as_uint(nrm[2]), so, sd);
+    Ray r;
+    setup_ray(so, sd, r);
+    uint2 *stk = stk_base + lane;
+    FRay f;
+    to_fray(r, f);
+    if (p.guard) trace_lean<MODE, true>(p, f, stk);
+    else trace_lean<MODE, false, false, FA>(p, f, stk);
+    from_fray(f, r);
+    if (r.scale < S_MAX) {   // occluded
+        const uint32_t nw1 = w1 | (8u << 16);
+        if (p.out.hits) reinterpret_cast<uint32_t *>(p.out.hits + i)[1] = nw1;
+        if (p.out.compact) p.out.compact[3 * i + 1] = nw1;
+        if (p.out.rgba) p.out.rgba[i] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+        if (p.out.rgba8) p.out.rgba8[i] = 255u << 24;
+        if (p.out.rgb8) {
+            uint8_t *d = p.out.rgb8 + 3 * i;
+            d[0] = d[1] = d[2] = 0;
+        }
+    }
+}
+
 // ---------------------------------------------------------- frame assembly
 // svo_assemble_frame: one thread per pixel of the frame (one row per grid y).
 // Row y belongs to band b = y / band_rows and, round-robin, to part m = b % n_parts
@@ -1106,11 +1160,12 @@ constexpr int PACK_THREADS = 256;
 struct SparseLayout {   // byte offsets of a part (svo_rt.h SVO_SPARSE_*)
     size_t offsets, rgb, scratch;
 };
-__host__ __device__ inline SparseLayout sparse_layout(int n, int n_px) {
+// elem: bytes per packed hit (3: RGB payload, 4: pixel index of the compacted shadow pass)
+__host__ __device__ inline SparseLayout sparse_layout(int n, int n_px, int elem = 3) {
     SparseLayout l;
     l.offsets = 8 * (size_t)n;
     l.rgb = 12 * (size_t)n + 4;
-    l.scratch = (l.rgb + 3 * (size_t)n_px + 3) & ~(size_t)3;
+    l.scratch = (l.rgb + (size_t)elem * (size_t)n_px + 3) & ~(size_t)3;
     return l;
 }
 
@@ -1141,12 +1196,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void tile_scan_local_kernel(const uns
     if (n == 0 && tid == 0) *count = 0u;   // an empty band: no pack workgroup writes it
 }
 
+// INDEX: pack the hit pixels' band-local indices (lr * width + x, 4 bytes) instead of
+// their RGB -- the compacted shadow pass's hit list.
+template <bool INDEX>
 __global__ __launch_bounds__(PACK_THREADS) void pack_hits_kernel(const uint8_t *__restrict__ rgb8, int width,
                                                                  int local_rows, uint8_t *__restrict__ part) {
     __shared__ uint32_t wsum[PACK_THREADS / 64];
     const int tiles_x = (width + 7) / 8;
     const int n = tiles_x * ((local_rows + 7) / 8);
-    const SparseLayout L = sparse_layout(n, width * local_rows);
+    const SparseLayout L = sparse_layout(n, width * local_rows, INDEX ? 4 : 3);
     const unsigned long long *masks = reinterpret_cast<const unsigned long long *>(part);
     uint32_t *offsets = reinterpret_cast<uint32_t *>(part + L.offsets);
     const uint32_t *local = reinterpret_cast<const uint32_t *>(part + L.scratch);
@@ -1173,6 +1231,10 @@ __global__ __launch_bounds__(PACK_THREADS) void pack_hits_kernel(const uint8_t *
     }
     if (!((mk >> bit) & 1ull)) return;
     const uint32_t k = off + (uint32_t)__popcll(mk & ((1ull << bit) - 1ull));
+    if (INDEX) {
+        reinterpret_cast<uint32_t *>(part + L.rgb)[k] = (uint32_t)lr * (uint32_t)width + (uint32_t)x;
+        return;
+    }
     const uint8_t *src = rgb8 + 3 * ((size_t)lr * (size_t)width + (size_t)x);
     uint8_t *dst = part + L.rgb + 3 * (size_t)k;
     dst[0] = src[0];
@@ -1180,21 +1242,31 @@ __global__ __launch_bounds__(PACK_THREADS) void pack_hits_kernel(const uint8_t *
     dst[2] = src[2];
 }
 
-hipError_t launch_pack_hits(const uint8_t *rgb8, int width, int local_rows, void *part, hipStream_t stream) {
+template <bool INDEX>
+static hipError_t launch_pack(const uint8_t *rgb8, int width, int local_rows, void *part, hipStream_t stream) {
     if (width <= 0 || local_rows < 0) return hipSuccess;
     const int n = ((width + 7) / 8) * ((local_rows + 7) / 8);
     const int chunks = (n + SCAN_THREADS - 1) / SCAN_THREADS;
     uint8_t *p = reinterpret_cast<uint8_t *>(part);
-    const SparseLayout L = sparse_layout(n, width * local_rows);
+    const SparseLayout L = sparse_layout(n, width * local_rows, INDEX ? 4 : 3);
     uint32_t *local = reinterpret_cast<uint32_t *>(p + L.scratch);
     hipLaunchKernelGGL(tile_scan_local_kernel, dim3(chunks > 0 ? chunks : 1), dim3(SCAN_THREADS), 0, stream,
                        reinterpret_cast<const unsigned long long *>(p), n, local, local + n,
                        reinterpret_cast<uint32_t *>(p + L.offsets) + n);
     if (local_rows > 0) {
         const dim3 grid((unsigned)((width + PACK_THREADS - 1) / PACK_THREADS), (unsigned)local_rows);
-        hipLaunchKernelGGL(pack_hits_kernel, grid, dim3(PACK_THREADS), 0, stream, rgb8, width, local_rows, p);
+        hipLaunchKernelGGL(pack_hits_kernel<INDEX>, grid, dim3(PACK_THREADS), 0, stream, rgb8, width, local_rows, p);
     }
     return hipGetLastError();
+}
+
+hipError_t launch_pack_hits(const uint8_t *rgb8, int width, int local_rows, void *part, hipStream_t stream) {
+    return launch_pack<false>(rgb8, width, local_rows, part, stream);
+}
+
+size_t shadow_list_bytes(int width, int local_rows) {
+    const int n = ((width + 7) / 8) * ((local_rows + 7) / 8);
+    return sparse_layout(n, width * local_rows, 4).scratch + 4 * (size_t)n + 4 * (size_t)((n + SCAN_THREADS - 1) / SCAN_THREADS);
 }
 
 hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
@@ -1235,6 +1307,27 @@ hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stre
     if (primary_end && (e = hipEventRecord(primary_end, stream)) != hipSuccess) return e;
     if (!count && p.shadows == 1 && (p.out.hits || p.out.compact))
         return stack_mode == 0 ? launch_shadows<0>(p, stream) : launch_shadows<1>(p, stream);
+    if (!count && p.shadows == 3 && (p.out.hits || p.out.compact) && p.out.hitmask) {
+        // compacted shadow pass: the hit list in the scratch whose head the primary filled
+        if ((e = launch_pack<true>(nullptr, p.width, p.local_rows, p.out.hitmask, stream)) != hipSuccess) return e;
+        const int n = ((p.width + 7) / 8) * ((p.local_rows + 7) / 8);
+        const SparseLayout L = sparse_layout(n, p.width * p.local_rows, 4);
+        const uint8_t *base = reinterpret_cast<const uint8_t *>(p.out.hitmask);
+        const uint32_t *list = reinterpret_cast<const uint32_t *>(base + L.rgb);
+        const uint32_t *cnt = reinterpret_cast<const uint32_t *>(base + L.offsets) + n;
+        const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2);
+        const dim3 grid((unsigned)(((size_t)p.width * (size_t)p.local_rows + TILE - 1) / TILE));
+        LaunchParams q = p;
+        q.out.hitmask = nullptr;
+        if (stack_mode == 0) {
+            if (p.fetch_all && !p.guard) hipLaunchKernelGGL((shadow_list_kernel<0, true>), grid, dim3(TILE), lds, stream, q, list, cnt);
+            else hipLaunchKernelGGL((shadow_list_kernel<0>), grid, dim3(TILE), lds, stream, q, list, cnt);
+        } else {
+            if (p.fetch_all && !p.guard) hipLaunchKernelGGL((shadow_list_kernel<1, true>), grid, dim3(TILE), lds, stream, q, list, cnt);
+            else hipLaunchKernelGGL((shadow_list_kernel<1>), grid, dim3(TILE), lds, stream, q, list, cnt);
+        }
+        return hipGetLastError();
+    }
     return hipSuccess;
 }
 

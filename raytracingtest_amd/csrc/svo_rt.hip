@@ -108,6 +108,8 @@ struct svo_ctx {
     bool depth_exact = false;        // see recompute_depth
     // host-path output scratch
     void *d_out_hits = nullptr;
+    void *d_shadow_list = nullptr;   // compacted shadow pass: hit masks, offsets, hit list (svo_kernel.hip)
+    size_t shadow_list_cap = 0;
     void *d_out_rgba = nullptr;
     size_t out_cap_px = 0;
     // svo_render_progressive: the accumulated frame (RGBA32F, zeroed on a size
@@ -129,6 +131,7 @@ struct svo_ctx {
     int shadow_order_enabled = 1;    // env SVO_SHADOW_ORDER=0: shadow tiles in plain strip order
     int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
     int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
+    int shadow_compact = 0;          // env SVO_SHADOW_COMPACT=1: that launch over the compacted hit list
     int order_every = 32;            // env SVO_ORDER_EVERY: rebuild the order every k-th launch (and after
                                      // every camera move or change of render mode)
     unsigned long long view_gen = 0; // bumped when svo_set_camera changes the matrices
@@ -459,16 +462,31 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     if (b.count == 1) p.out.frame_layout = 0;   // the whole frame: both layouts coincide
     p.xcd_remap = ctx->xcd_remap;
     if (p.xcd_remap == 2 && ((width + 7) / 8) % 8 != 0) p.xcd_remap = 0;
-    p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? (ctx->fused_shadows ? 2 : 1) : 0;
+    p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? (ctx->shadow_compact ? 3 : ctx->fused_shadows ? 2 : 1) : 0;
+    if (p.shadows == 3 && out.hitmask) p.shadows = 1;   // the caller's masks are not a list scratch
     if (p.local_rows == 0) return SVO_OK;
     if (out.fetches) p.shadows = 0;
     hipStream_t s = stream ? stream : ctx->stream;
-    if (p.shadows == 1 && !p.out.hits && !p.out.compact) {   // the second shadow pass reads the primary records
+    if ((p.shadows == 1 || p.shadows == 3) && !p.out.hits && !p.out.compact) {   // the second pass reads the records
         int rc2 = ensure_out(ctx, (size_t)(p.out.frame_layout ? height : p.local_rows) * (size_t)width);
         if (rc2) return rc2;
         rc2 = order_scratch(ctx, s);
         if (rc2) return rc2;
         p.out.hits = reinterpret_cast<svo::Hit *>(ctx->d_out_hits);
+    }
+    if (p.shadows == 3) {   // the compacted pass's masks + hit list (shared scratch, ordered like d_out_hits)
+        const size_t need = svo::shadow_list_bytes(width, p.local_rows);
+        if (ctx->shadow_list_cap < need) {
+            HIP_TRY(hipDeviceSynchronize());   // an earlier launch may still read the old list
+            if (ctx->d_shadow_list) hipFree(ctx->d_shadow_list);
+            ctx->d_shadow_list = nullptr;
+            ctx->shadow_list_cap = 0;
+            HIP_TRY(hipMalloc(&ctx->d_shadow_list, need));
+            ctx->shadow_list_cap = need;
+        }
+        rc = order_scratch(ctx, s);
+        if (rc) return rc;
+        p.out.hitmask = reinterpret_cast<unsigned long long *>(ctx->d_shadow_list);
     }
     p.prio = ctx->prio;
     const bool ordered = ctx->tile_order && !p.out.fetches;
@@ -718,6 +736,7 @@ int destroy_single(svo_ctx *ctx) {
     if (ctx->d_nodes) hipFree(ctx->d_nodes);
     if (ctx->d_att) hipFree(ctx->d_att);
     if (ctx->d_stage) hipFree(ctx->d_stage);
+    if (ctx->d_shadow_list) hipFree(ctx->d_shadow_list);
     if (ctx->d_out_hits) hipFree(ctx->d_out_hits);
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
     if (ctx->d_accum) hipFree(ctx->d_accum);
@@ -772,6 +791,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_SHADOW_ORDER")) ctx->shadow_order_enabled = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_FETCH_ALL")) ctx->fetch_all = std::atoi(k) != 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_FUSED_SHADOWS")) ctx->fused_shadows = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_SHADOW_COMPACT")) ctx->shadow_compact = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
     if (e != hipSuccess) {
         destroy_single(ctx);

@@ -68,7 +68,8 @@ struct LaunchParams {
     int slots;            // stack slots = depth - 1 (scales [23 - slots, 22])
     Outputs out;
     int xcd_remap;        // 2: interleaved XCD column strips, 0: raster
-    int shadows;          // one shadow ray per primary hit: 1 = second pass (needs hits), 2 = fused into the primary launch
+    int shadows;          // one shadow ray per primary hit: 1 = second pass (needs hits), 2 = fused into the primary
+                          // launch, 3 = second pass over the compacted hit list (needs hits + out.hitmask scratch)
     uint32_t *wave_log;   // diagnostics (env SVO_WAVE_LOG): per wave {t0, t1, HW_ID, XCC_ID | trips << 8,
                           //   loop cycles, fetch-wait cycles, fetch trips, pop trips} (instrumented loop)
     // Cost-ordered dispatch: block b traces 8x8 tile tile_order[b] (null = b)
@@ -127,6 +128,9 @@ hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream);
 // tile offsets (exclusive scan of the masks' popcounts, count last) and pack the 3-byte RGB
 // of every hit pixel of the band's dense `rgb8` behind them.  Three launches.
 hipError_t launch_pack_hits(const uint8_t *rgb8, int width, int local_rows, void *part, hipStream_t stream);
+// Scratch bytes of the compacted shadow pass (shadows == 3): hit masks, tile offsets, count,
+// the hit pixels' band-local indices and the scan's scratch; LaunchParams.out.hitmask points at it.
+size_t shadow_list_bytes(int width, int local_rows);
 
 // Display RGBA8 words of an RGBA32F frame (svo_render_progressive).
 hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int num_cus, hipStream_t stream);

@@ -244,13 +244,16 @@ def test_multi_device_weighted_deal(torch, oracle_mod):
         m.close()
 
 
-def test_multi_device_shadow_rays(torch, oracle_mod):
+@pytest.mark.parametrize("compact", [False, True])
+def test_multi_device_shadow_rays(torch, oracle_mod, monkeypatch, compact):
     """The C3 '+1 shadow ray' frame through the multi-device context: the
     occlusion flag travels in the compact record and the display member
     rebuilds the black Result."""
     svo = build_menger(8)
     w, h = 400, 240
     cam = overview_camera()
+    if compact:   # every member's shadow pass over its bands' compacted hit list
+        monkeypatch.setenv("SVO_SHADOW_COMPACT", "1")
     ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h, shadows=True)
     m = RaytracingMaster(devices=[0, 0, 0], capacity_nodes=len(svo))
     try:

@@ -194,7 +194,8 @@ def test_errors_are_loud(rm):
 
 @pytest.mark.parametrize("env", [
     {"SVO_XCD_REMAP": "0"}, {"SVO_TILE_ORDER": "0"}, {"SVO_PRIO": "0"}, {"SVO_FETCH_ALL": "0"},
-    {"SVO_FETCH_ALL": "1"}, {"SVO_ORDER_EVERY": "1"}, {"SVO_SHADOW_ORDER": "0", "SVO_FUSED_SHADOWS": "0"}])
+    {"SVO_FETCH_ALL": "1"}, {"SVO_ORDER_EVERY": "1"}, {"SVO_SHADOW_ORDER": "0", "SVO_FUSED_SHADOWS": "0"},
+    {"SVO_SHADOW_COMPACT": "1"}])
 def test_runtime_switches_identical(oracle_mod, monkeypatch, env):
     """Every surviving placement / loop-form switch (svo_rt.hip svo_create; the
     loop forms and block shapes measured slower in round 1 were removed) gives
@@ -242,12 +243,16 @@ def test_shadow_rays_parity(rm, oracle_mod, mode):
     _compare(hits, rgba, ref_hits, ref_rgba)
 
 
-@pytest.mark.parametrize("fused", ["0", "1"])
-def test_shadow_pass_forms_identical(oracle_mod, monkeypatch, fused):
-    """The shadow rays as a second cost-ordered launch (SVO_FUSED_SHADOWS=0) and
-    fused into the primary launch (default) give the oracle's frame, over repeated
-    launches (the dispatch order is rebuilt from recorded costs) and with RGBA only."""
-    monkeypatch.setenv("SVO_FUSED_SHADOWS", fused)
+@pytest.mark.parametrize("form", ["two_pass", "fused", "compact"])
+def test_shadow_pass_forms_identical(oracle_mod, monkeypatch, form):
+    """The shadow rays as a second cost-ordered launch over the tiles
+    (SVO_FUSED_SHADOWS=0), fused into the primary launch (default), and as a second
+    launch over the compacted hit list (SVO_SHADOW_COMPACT=1: ballot masks, prefix
+    sum, dense waves of 64 hits) give the oracle's frame, over repeated launches
+    (the dispatch order is rebuilt from recorded costs) and with RGBA only."""
+    monkeypatch.setenv("SVO_FUSED_SHADOWS", "0" if form == "two_pass" else "1")
+    if form == "compact":
+        monkeypatch.setenv("SVO_SHADOW_COMPACT", "1")
     svo = build_menger(8)
     cam = overview_camera()
     w, h = 480, 272
