@@ -1,8 +1,9 @@
 """World-size-2/3 gloo tests of the multi-GPU path on CPU.
 
 The per-rank renderer is the CPU oracle (test infrastructure) standing in for
-the HIP kernel; the band layout, the payload formats (RGBA8 words, 12-byte
-compact records = svo_hit prefix) and the one gather to rank 0
+the HIP kernel; the band layout, the payload formats (RGBA8 words, 3-byte RGB,
+12-byte compact records = svo_hit prefix, the sparse hit payload with its
+count-first exchange) and the one gather to rank 0
 (distributed.gather_to_root, the batch of sends / receives bench.py's
 Gather makes on RCCL) run as in
 bench.py; the re-interleave is the host restatement of the assemble kernel's
@@ -24,6 +25,44 @@ def _free_port():
     port = s.getsockname()[1]
     s.close()
     return port
+
+
+def _sparse_part(hit, rgb):
+    """Host restatement of the sparse band payload (svo_rt.h layout, svo_pack_hits):
+    [u64 hit mask per 8x8 tile][u32 hits before each tile, then the count][3-B RGB
+    of every hit pixel, tile by tile, lanes in row-major order]."""
+    R, W = hit.shape
+    tx, ty = -(-W // 8), -(-R // 8)
+    h = np.zeros((ty * 8, tx * 8), bool)
+    h[:R, :W] = hit
+    c = np.zeros((ty * 8, tx * 8, 3), np.uint8)
+    c[:R, :W] = rgb
+    lanes = h.reshape(ty, 8, tx, 8).transpose(0, 2, 1, 3).reshape(-1, 64)
+    cols = c.reshape(ty, 8, tx, 8, 3).transpose(0, 2, 1, 3, 4).reshape(-1, 64, 3)
+    masks = (lanes.astype(np.uint64) << np.arange(64, dtype=np.uint64)).sum(axis=1, dtype=np.uint64)
+    cnt = lanes.sum(axis=1)
+    offs = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint32)
+    return masks.tobytes() + offs.tobytes() + cols[lanes].tobytes()
+
+
+def _sparse_unpack(raw, R, W, sky):
+    """The display side (the sparse assemble): hits from the part, misses from `sky`."""
+    tx, ty = -(-W // 8), -(-R // 8)
+    n = tx * ty
+    masks = np.frombuffer(raw[:8 * n], np.uint64)
+    offs = np.frombuffer(raw[8 * n:12 * n + 4], np.uint32)
+    rgb = np.frombuffer(raw[12 * n + 4:], np.uint8).reshape(-1, 3)
+    assert len(rgb) == offs[-1]
+    out = sky.copy()
+    for y in range(R):
+        for x in range(W):
+            t = (y // 8) * tx + x // 8
+            bit = (y % 8) * 8 + x % 8
+            m = int(masks[t])
+            if (m >> bit) & 1:
+                k = int(offs[t]) + bin(m & ((1 << bit) - 1)).count("1")
+                out[y, x] = int(rgb[k, 0]) | int(rgb[k, 1]) << 8 | int(rgb[k, 2]) << 16 | 255 << 24
+    return out
 
 
 def _worker(rank, world, port, mode, out_dir):
@@ -75,6 +114,31 @@ def _worker(rank, world, port, mode, out_dir):
                 trimmed = [p.numpy().view(np.uint8)[:D.band_len(H, r, world) * W * elem_b] for r, p in enumerate(parts)]
                 frame = D.assemble(trimmed, H, W, dt)
                 np.save(os.path.join(out_dir, "frame.npy"), frame)
+    elif mode == "sparse":   # bench.py's SparseGather protocol: counts first, then exact-size parts
+        cam = orc.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
+        band = D.rank_band(rank, world)
+        ys = band_rows(H, band)
+        pix = (ys[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
+        hits, rgba, _ = orc.render_pixels(osvo, cam, W, H, pix, nthreads=2)
+        part = _sparse_part((hits["flags"] & 1).reshape(len(ys), W) != 0,
+                            orc.pack_rgba8(rgba).view(np.uint8).reshape(len(ys), W, 4)[:, :, :3])
+        cnt = torch.tensor([len(part)], dtype=torch.int32)
+        sizes = [torch.zeros(1, dtype=torch.int32) for _ in range(world)] if rank == 0 else None
+        D.gather_to_root(None if rank == 0 else cnt, sizes, root=0)
+        if rank == 0:
+            bufs = [None] + [torch.full((int(sizes[r].item()),), 0xEE, dtype=torch.uint8) for r in range(1, world)]
+            D.gather_to_root(None, bufs, root=0)
+            _, ref_rgba, _ = orc.render(osvo, cam, W, H, nthreads=2)   # the display rank's sky for misses
+            frame = orc.pack_rgba8(ref_rgba).copy().reshape(H, W)
+            frame[:] = 0
+            for r in range(world):
+                ys_r = band_rows(H, D.rank_band(r, world))
+                raw = part if r == 0 else bufs[r].numpy().tobytes()
+                sky = orc.pack_rgba8(ref_rgba).reshape(H, W)[ys_r]
+                frame[ys_r] = _sparse_unpack(raw, len(ys_r), W, sky)
+            np.save(os.path.join(out_dir, "frame.npy"), frame)
+        else:
+            D.gather_to_root(torch.from_numpy(np.frombuffer(part, np.uint8).copy()), None, root=0)
     else:
         off = (0.5, 0.5) if rank == 0 else tuple(float(v) for v in jitter_offsets(world)[rank])
         cam = orc.make_camera(c2w, inv_proj, off, main_light())
@@ -88,18 +152,20 @@ def _worker(rank, world, port, mode, out_dir):
 
 
 @pytest.mark.parametrize("mode,world", [("bands", 2), ("samples", 2), ("rgba8", 2), ("rgba8", 3), ("rgb8", 3),
-                                        ("compact", 3)])
+                                        ("compact", 3), ("sparse", 3)])
 def test_gloo_ranks(tmp_path, oracle_mod, text_svo, mode, world):
     mp.spawn(_worker, args=(world, _free_port(), mode, str(tmp_path)), nprocs=world, join=True)
     from raytracingtest_amd.camera import jitter_offsets, main_light, overview_camera
     W, H = 96, 70
     c2w, inv_proj = overview_camera().uniforms(W, H)
     osvo = oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments)
-    if mode in ("bands", "rgba8", "rgb8", "compact"):
+    if mode in ("bands", "rgba8", "rgb8", "compact", "sparse"):
         cam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
         ref, ref_rgba, _ = oracle_mod.render(osvo, cam, W, H)
         got = np.load(tmp_path / "frame.npy")
-        if mode == "bands":
+        if mode == "sparse":
+            assert np.array_equal(got.reshape(-1), oracle_mod.pack_rgba8(ref_rgba))
+        elif mode == "bands":
             assert got.reshape(-1).tobytes() == ref.tobytes()
         elif mode == "rgba8":
             assert np.array_equal(got.reshape(-1), oracle_mod.pack_rgba8(ref_rgba))
