@@ -32,6 +32,7 @@ The kernel is bound by its dependent node-fetch chain (latency), not by HBM:
 cpu_baseline: the strict-IEEE C oracle (oracle/, "port") on the host cores.
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -442,13 +443,22 @@ class Gather:
         per = (part_bytes + 3) // 4   # int32 words
         self.G = torch.cuda.Stream(dev)
         self.n_local = D.band_len(H, rank, world, owner=owner) * W
+        # the per-step plugin arguments, built once (host time per step matters at N = 8:
+        # tools/host_overhead.py)
+        self.band_c = _lib.make_band(self.band)
+        self.deal_c = _lib.make_band((D.DEFAULT_BAND_ROWS, 0, world) if owner is None
+                                     else (D.DEFAULT_BAND_ROWS, 0, world, tuple(owner)))
         if rank == 0:   # display frames, double-buffered
             self.frame8 = [torch.empty(W * H, dtype=torch.int32, device=dev) for _ in range(2)]
             self.fhits = [torch.empty(W * H * 24, dtype=torch.uint8, device=dev) for _ in range(2)]
             self.frgba = [None if no_rgba else torch.empty(W * H * 4, dtype=torch.float32, device=dev)
                           for _ in range(2)]
-            self.parts = [[None] + [torch.empty(per, dtype=torch.int32, device=dev) for _ in range(1, world)]
+            # parts[k][0]: the display rank's own (never used) slot of the one-call gather
+            self.dummy = torch.empty(per, dtype=torch.int32, device=dev)
+            self.parts = [[self.dummy] + [torch.empty(per, dtype=torch.int32, device=dev) for _ in range(1, world)]
                           for _ in range(2)]
+            self.parts_c = [(ctypes.c_void_p * world)(None, *[p.data_ptr() for p in self.parts[k][1:]])
+                            for k in range(2)]
             self.send = None
         else:
             self.hits = torch.empty(max(self.n_local, 1) * 24, dtype=torch.uint8, device=dev)
@@ -476,7 +486,7 @@ class Gather:
         ptr = lambda t: None if t is None else t.data_ptr()
         if self.rank == 0:
             self.rm.render_frame(self.W, self.H, hits=ptr(self.fhits[k]), rgba=ptr(self.frgba[k]),
-                                 rgba8=ptr(self.frame8[k]), layout=1, stack_mode=stack_mode, band=self.band,
+                                 rgba8=ptr(self.frame8[k]), layout=1, stack_mode=stack_mode, band=self.band_c,
                                  stream=self.R.cuda_stream)
         else:
             if self.used[k]:
@@ -486,7 +496,7 @@ class Gather:
                                  rgba8=sp if self.payload == "rgba8" else None,
                                  rgb8=sp if self.payload == "rgb8" else None,
                                  compact=sp if self.payload == "compact" else None,
-                                 stack_mode=stack_mode, band=self.band, stream=self.R.cuda_stream)
+                                 stack_mode=stack_mode, band=self.band_c, stream=self.R.cuda_stream)
         self.ev_r[k].record(self.R)
 
     def gather(self, k):
@@ -496,24 +506,24 @@ class Gather:
         else:
             self.G.wait_event(self.ev_r[k])
         with self.torch.cuda.stream(self.G):
-            self.D.gather_to_root(None if self.send is None else self.send[k],
-                                  self.parts[k] if self.rank == 0 else None, root=0)
+            self.D.gather_fixed_to_root(self.dummy if self.rank == 0 else self.send[k],
+                                        self.parts[k] if self.rank == 0 else None, root=0)
         self.ev_g[k].record(self.G)
         self.used[k] = True
 
     def assemble(self, k, stream):
-        ptrs = [None] + [p.data_ptr() for p in self.parts[k][1:]]
+        ptrs = self.parts_c[k]
         s = stream.cuda_stream
         if self.payload in ("rgba8", "rgb8", "sparse"):
             fmt = {"rgba8": self._lib.PART_RGBA8, "rgb8": self._lib.PART_RGB8,
                    "sparse": self._lib.PART_SPARSE_RGB8}[self.payload]
             self.rm.assemble_frame(self.W, self.H, ptrs, fmt, rgba8=self.frame8[k].data_ptr(),
-                                   skip_part=0, stream=s, owner=self.owner)
+                                   skip_part=0, stream=s, deal=self.deal_c)
         else:
             fr = self.frgba[k]
             self.rm.assemble_frame(self.W, self.H, ptrs, self._lib.PART_COMPACT, hits=self.fhits[k].data_ptr(),
                                    rgba=None if fr is None else fr.data_ptr(), rgba8=self.frame8[k].data_ptr(),
-                                   skip_part=0, stream=s, owner=self.owner)
+                                   skip_part=0, stream=s, deal=self.deal_c)
 
     def drain(self):
         """Rank 0: assemble the frame still pending (end of a run of steps)."""
@@ -614,8 +624,8 @@ class SparseGather(Gather):
         ptr = lambda t: None if t is None else t.data_ptr()
         nt = self.tiles[self.rank]
         self.rm.render_frame(self.W, self.H, hits=ptr(self.hits), rgba=ptr(self.rgba), rgb8=self.dense.data_ptr(),
-                             hitmask=self.send[k].data_ptr(), stack_mode=stack_mode, band=self.band, stream=s)
-        self.rm.pack_hits(self.W, self.H, self.band, self.dense.data_ptr(), self.send[k].data_ptr(), stream=s)
+                             hitmask=self.send[k].data_ptr(), stack_mode=stack_mode, band=self.band_c, stream=s)
+        self.rm.pack_hits(self.W, self.H, self.band_c, self.dense.data_ptr(), self.send[k].data_ptr(), stream=s)
         with self.torch.cuda.stream(self.R):
             self.cnt_host[k].copy_(self.send[k][3 * nt:3 * nt + 1], non_blocking=True)   # the count, byte 12 n
         self.ev_r[k].record(self.R)
@@ -627,14 +637,15 @@ class SparseGather(Gather):
         """Frame k's hit counts to rank 0 (device to device, then to pinned host)."""
         if self.rank == 0:
             with self.torch.cuda.stream(self.G):
-                self.D.gather_to_root(None, [self.cbuf[k][m:m + 1] for m in range(self.world)], root=0)
+                slots = [self.cbuf[k][m:m + 1] for m in range(self.world)]
+                self.D.gather_fixed_to_root(slots[0], slots, root=0)
                 self.cnt_host[k].copy_(self.cbuf[k], non_blocking=True)
             self.ev_c[k].record(self.G)
         else:
             nt = self.tiles[self.rank]
             self.G.wait_event(self.ev_r[k])
             with self.torch.cuda.stream(self.G):
-                self.D.gather_to_root(self.send[k][3 * nt:3 * nt + 1], None, root=0)
+                self.D.gather_fixed_to_root(self.send[k][3 * nt:3 * nt + 1], None, root=0)
 
     def gather(self, k):
         """Frame k's payloads at their exact sizes (its counts gathered a step earlier)."""

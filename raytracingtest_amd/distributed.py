@@ -126,6 +126,27 @@ def gather_to_root(send, parts, root=0, dist=None, group=None):
         dev_buf.copy_(host)
 
 
+def gather_fixed_to_root(send, parts, root=0, dist=None, group=None):
+    """gather_to_root for equal-size payloads as ONE collective call (RCCL: the
+    same ncclGroup of sends / receives, issued from C++ instead of one Python op
+    per peer -- the display rank's host issues every step's calls within one
+    render's time).  The root passes its own payload-sized `send` too and
+    parts[root] must be that same tensor (torch copies it onto itself: a no-op)."""
+    if dist is None:
+        import torch.distributed as dist
+    rank = dist.get_rank(group)
+    if send.is_cuda and dist.get_backend(group) == "gloo":   # host staging (one-GPU rehearsal)
+        host = send.cpu()
+        hparts = [p.cpu() for p in parts] if rank == root else None
+        dist.gather(host, gather_list=hparts, dst=root, group=group)
+        if rank == root:
+            for r, (p, h) in enumerate(zip(parts, hparts)):
+                if r != root:
+                    p.copy_(h)
+        return
+    dist.gather(send, gather_list=parts if rank == root else None, dst=root, group=group)
+
+
 def broadcast_svo(svo, src=0, dist=None, device=None):
     """Replicate a node pool from rank `src` to every rank (the
     SVO replicated per GPU, broadcast from rank 0 over xGMI).  `svo` is the

@@ -198,21 +198,25 @@ class RaytracingMaster:
         layout LAYOUT_BAND: buffers hold only `band`'s rows; LAYOUT_FRAME: full-frame
         buffers.  A multi-device context renders the whole frame (band None) onto
         devices[0]."""
-        b = None if band is None else ctypes.byref(make_band(band))
+        # band: a (rows, rank, count[, owner]) tuple or a prebuilt _lib.SvoBand (per-frame callers
+        # build it once: the owner table costs host time on every call otherwise)
+        b = None if band is None else ctypes.byref(band if isinstance(band, _lib.SvoBand) else make_band(band))
         f = _frame(hits, rgba, rgba8, compact, position, voxel, layout, rgb8, hitmask)
         check(_lib.lib().svo_render_frame(self._ctx, width, height, stack_mode, b, ctypes.byref(f), stream),
               "svo_render_frame")
 
     def assemble_frame(self, width, height, parts, part_format, band_rows=None, hits=None, rgba=None, rgba8=None,
-                       compact=None, skip_part=-1, stream=None, owner=None):
+                       compact=None, skip_part=-1, stream=None, owner=None, deal=None):
         """Rebuild a frame (full-frame device buffers) from band parts: parts[m] = the
         device pointer of rank m's band payload (compact records or RGBA8 words).
         The deal: band_rows-row bands, round-robin, or owner[b % len(owner)] = the
         part holding band b (weighted deal)."""
-        arr = (ctypes.c_void_p * len(parts))(*[p if p else None for p in parts])
+        # parts may be a prebuilt ctypes array and deal a prebuilt _lib.SvoBand (per-frame callers)
+        arr = parts if isinstance(parts, ctypes.Array) else (ctypes.c_void_p * len(parts))(*[p if p else None for p in parts])
         f = _frame(hits, rgba, rgba8, compact, None, None, LAYOUT_FRAME)
         rows = self.band_rows if band_rows is None else band_rows
-        deal = make_band((rows, 0, len(parts)) if owner is None else (rows, 0, len(parts), owner))
+        if deal is None:
+            deal = make_band((rows, 0, len(parts)) if owner is None else (rows, 0, len(parts), owner))
         check(_lib.lib().svo_assemble_frame(self._ctx, width, height, ctypes.byref(deal), len(parts), arr,
                                             part_format, skip_part, ctypes.byref(f), stream),
               "svo_assemble_frame")
@@ -223,7 +227,8 @@ class RaytracingMaster:
         (render_frame(hitmask=part)); write the tile offsets and the hit count
         behind them and pack the RGB of the hit pixels from the band's dense
         `rgb8` after that."""
-        b = ctypes.byref(make_band(band if band is not None else (self.band_rows, 0, 1)))
+        band = band if band is not None else (self.band_rows, 0, 1)
+        b = ctypes.byref(band if isinstance(band, _lib.SvoBand) else make_band(band))
         check(_lib.lib().svo_pack_hits(self._ctx, width, height, b, rgb8, part, stream), "svo_pack_hits")
 
     def count_fetches_device(self, width, height, fetch_ptr, stack_mode=STACK_HLSL, band=None, stream=None):

@@ -106,7 +106,12 @@ def _worker(rank, world, port, mode, out_dir):
             send = torch.zeros(per, dtype=torch.int32)
             send.numpy().view(np.uint8)[:len(raw)] = np.frombuffer(raw, np.uint8)
             parts = [None] + [torch.full((per,), -7, dtype=torch.int32) for _ in range(1, world)] if rank == 0 else None
-            D.gather_to_root(None if rank == 0 else send, parts, root=0)
+            if mode == "rgba8":   # the batch of point-to-point transfers
+                D.gather_to_root(None if rank == 0 else send, parts, root=0)
+            else:                 # bench.py's one-call gather (the display rank's own slot a dummy)
+                if rank == 0:
+                    parts[0] = torch.zeros(per, dtype=torch.int32)
+                D.gather_fixed_to_root(parts[0] if rank == 0 else send, parts, root=0)
             if rank == 0:
                 parts[0] = send   # the display rank's own rows never leave it
                 dt = {"rgba8": np.dtype(np.uint32), "rgb8": np.dtype([("rgb", "u1", 3)]),
