@@ -78,6 +78,7 @@ def test_multi_device_and_frame_entry_points_reject_bad_arguments_without_gpu(na
     assert native.svo_assemble_frame(None, 8, 8, None, 1, None, 0, -1, None, None) == -1
     assert native.svo_stage_time(None, 0, None, None) == -1
     assert native.svo_set_band_deal(None, 0, None) == -1
+    assert native.svo_pack_hits(None, 8, 8, None, None, None, None) == -1
     n = ctypes.c_int()
     assert native.svo_num_devices(None, ctypes.byref(n)) == -1
 
@@ -93,6 +94,24 @@ def test_compact_record_is_the_hit_record_prefix():
     assert np.array_equal(c["parent"], h["parent"]) and np.array_equal(c["t"], h["t"])
     assert np.array_equal(c["meta"], h["hit_idx"] | (h["hit_scale"].astype(np.uint32) << 8) |
                           (h["flags"].astype(np.uint32) << 16))
+
+
+def test_sparse_part_sizes_match_header(tmp_path):
+    """_lib.sparse_head_bytes / sparse_part_bytes == the header's SVO_SPARSE_* macros."""
+    import subprocess
+    src = tmp_path / "sizes.c"
+    src.write_text('#include <stdio.h>\n#include "svo_rt.h"\nint main(void) {\n'
+                   '  const int n[4][2] = {{0, 0}, {1, 7}, {1037, 66000}, {129600, 8294400}};\n'
+                   '  for (int i = 0; i < 4; ++i) printf("%zu %zu\\n", (size_t)SVO_SPARSE_HEAD_BYTES(n[i][0]),\n'
+                   '                                     (size_t)SVO_SPARSE_PART_BYTES(n[i][0], n[i][1]));\n'
+                   '  return 0;\n}\n')
+    exe = tmp_path / "sizes"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    from raytracingtest_amd import _lib
+    for i, (nt, px) in enumerate([(0, 0), (1, 7), (1037, 66000), (129600, 8294400)]):
+        assert int(out[2 * i]) == _lib.sparse_head_bytes(nt)
+        assert int(out[2 * i + 1]) == _lib.sparse_part_bytes(nt, px)
 
 
 def test_hit_dtype_matches_header():

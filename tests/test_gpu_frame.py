@@ -430,6 +430,38 @@ def test_sparse_parts_match_oracle(torch, oracle_mod, world, share):
         m.close()
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_sparse_parts_with_shadow_rays(torch, oracle_mod, mode):
+    """The sparse payload of the C3 '+1 shadow ray' frame: occluded hits travel
+    as black RGB, both stack modes, and the frame rebuilds bit-identically."""
+    svo = build_menger(8)
+    cam = overview_camera()
+    w, h = 400, 240
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h, mode, shadows=True)
+    assert np.count_nonzero(ref_hits["flags"] & 8) > 0
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        m.SetShadowRays(True)
+        parts = []
+        for r in range(3):
+            band = (8, r, 3)
+            rows = len(band_rows(h, band))
+            n_tiles = ((w + 7) // 8) * ((rows + 7) // 8)
+            dense = torch.empty(rows * w * 3, dtype=torch.uint8, device="cuda")
+            part = torch.empty(_lib.sparse_part_bytes(n_tiles, rows * w), dtype=torch.uint8, device="cuda")
+            m.render_frame(w, h, rgb8=dense.data_ptr(), hitmask=part.data_ptr(), band=band, stack_mode=mode)
+            m.pack_hits(w, h, band, dense.data_ptr(), part.data_ptr())
+            parts.append(part)
+        b = _bufs(torch, w * h)
+        m.assemble_frame(w, h, [p.data_ptr() for p in parts], _lib.PART_SPARSE_RGB8, rgba8=b["rgba8"].data_ptr())
+        m.synchronize()
+        _check(b, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("w,rows", [(7680, 1080), (64, 8), (13, 3), (1000, 7)])
 def test_pack_hits_random_masks(torch, w, rows):
     """svo_pack_hits on random masks and colours (no render): the offsets are the
