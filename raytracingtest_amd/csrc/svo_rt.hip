@@ -88,6 +88,8 @@ struct Peer {                       // one per member of a multi-device context 
     void *buf[2] = {nullptr, nullptr};   // band payload, double-buffered across frames
     size_t cap_bytes = 0;
     hipEvent_t rendered[2] = {nullptr, nullptr};
+    void *dense = nullptr;               // sparse payload: the band's dense RGB before the pack
+    size_t dense_cap = 0;
 };
 
 }  // namespace
@@ -151,6 +153,7 @@ struct svo_ctx {
     int parity = 0;
     int band_rows = 8;
     int deal_cycle = 0;                  // svo_set_band_deal: weighted deal over the members (0: round-robin)
+    int sparse_payload = 0;              // env SVO_SPARSE_PAYLOAD=1: display-only frames travel as sparse parts
     uint8_t deal_owner[svo::MAX_CYCLE] = {};
 };
 
@@ -645,8 +648,11 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
     if (out.position || out.voxel) return fail(SVO_ERR_ARG, "position / voxel outputs are not gathered across devices");
     if (out.rgb8 || out.hitmask) return fail(SVO_ERR_ARG, "a multi-device frame is assembled as rgba8, not rgb8 / hitmask");
     if (!out.hits && !out.rgba && !out.rgba8 && !out.compact) return fail(SVO_ERR_ARG, "no output requested");
-    // display-only frames travel as 3-byte RGB (the RGBA8 word without its constant alpha)
-    const int fmt = (out.hits || out.rgba || out.compact) ? SVO_PART_COMPACT : SVO_PART_RGB8;
+    // display-only frames travel as 3-byte RGB (the RGBA8 word without its constant alpha), or
+    // (SVO_SPARSE_PAYLOAD=1) as sparse parts: tile hit masks + offsets + the hits' RGB, pulled by the
+    // assemble kernel with no host round trip (the offsets travel in the part)
+    const int fmt = (out.hits || out.rgba || out.compact) ? SVO_PART_COMPACT
+                    : ctx->sparse_payload ? SVO_PART_SPARSE_RGB8 : SVO_PART_RGB8;
     const size_t elem = fmt == SVO_PART_COMPACT ? 12 : 3;
     const int k = ctx->parity;
     ctx->parity ^= 1;
@@ -664,7 +670,10 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
         Deal di;
         rc = check_band(&bi, height, &di);
         if (rc) return rc;
-        const size_t bytes = (size_t)band_rows_local(height, di) * (size_t)width * elem;
+        const int rows_i = band_rows_local(height, di);
+        const int tiles_i = ((width + 7) / 8) * ((rows_i + 7) / 8);
+        const size_t bytes = fmt == SVO_PART_SPARSE_RGB8 ? SVO_SPARSE_PART_BYTES(tiles_i, (size_t)rows_i * width)
+                                                         : (size_t)rows_i * (size_t)width * elem;
         HIP_TRY(hipSetDevice(m->device));
         if (pr.cap_bytes < bytes) {
             HIP_TRY(hipSetDevice(m0->device));
@@ -679,12 +688,31 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
             for (int j = 0; j < 2; ++j) HIP_TRY(hipMalloc(&pr.buf[j], std::max<size_t>(bytes, 16)));
             pr.cap_bytes = bytes;
         }
+        if (fmt == SVO_PART_SPARSE_RGB8 && pr.dense_cap < (size_t)rows_i * width * 3) {
+            HIP_TRY(hipStreamSynchronize(m->stream));   // an earlier pack may still read the old scratch
+            if (pr.dense) hipFree(pr.dense);
+            pr.dense = nullptr;
+            pr.dense_cap = 0;
+            HIP_TRY(hipMalloc(&pr.dense, std::max<size_t>((size_t)rows_i * width * 3, 16)));
+            pr.dense_cap = (size_t)rows_i * width * 3;
+        }
         if (ctx->gathered_used[k]) HIP_TRY(hipStreamWaitEvent(m->stream, ctx->gathered[k], 0));   // payload k is free
         svo::Outputs oi{};
-        if (fmt == SVO_PART_COMPACT) oi.compact = reinterpret_cast<uint32_t *>(pr.buf[k]);
-        else oi.rgb8 = reinterpret_cast<uint8_t *>(pr.buf[k]);
+        if (fmt == SVO_PART_COMPACT) {
+            oi.compact = reinterpret_cast<uint32_t *>(pr.buf[k]);
+        } else if (fmt == SVO_PART_SPARSE_RGB8) {
+            oi.rgb8 = reinterpret_cast<uint8_t *>(pr.dense);
+            oi.hitmask = reinterpret_cast<unsigned long long *>(pr.buf[k]);
+        } else {
+            oi.rgb8 = reinterpret_cast<uint8_t *>(pr.buf[k]);
+        }
         rc = launch(m, width, height, stack_mode, &bi, oi, m->stream);
         if (rc) return rc;
+        if (fmt == SVO_PART_SPARSE_RGB8) {
+            hipError_t e = svo::launch_pack_hits(reinterpret_cast<const uint8_t *>(pr.dense), width, rows_i, pr.buf[k],
+                                                 m->stream);
+            if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("pack hits launch: ") + hipGetErrorString(e));
+        }
         HIP_TRY(hipEventRecord(pr.rendered[k], m->stream));
         parts[i] = pr.buf[k];
     }
@@ -812,6 +840,7 @@ int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes,
     g->capacity = capacity_nodes;
     g->band_rows = band_rows;
     g->peers.resize(num_devices);
+    if (const char *k = std::getenv("SVO_SPARSE_PAYLOAD")) g->sparse_payload = std::atoi(k) != 0;
     auto bail = [&](int rc) {
         svo_destroy(g);
         return rc;
@@ -1202,6 +1231,7 @@ int svo_destroy(svo_ctx *ctx) {
             if (pr.buf[j]) hipFree(pr.buf[j]);
             if (pr.rendered[j]) hipEventDestroy(pr.rendered[j]);
         }
+        if (pr.dense) hipFree(pr.dense);
     }
     if (!ctx->members.empty()) hipSetDevice(ctx->members[0]->device);
     for (int j = 0; j < 2; ++j)

@@ -215,6 +215,35 @@ def test_multi_device_context_matches_oracle(torch, oracle_mod, text_svo, device
         m.close()
 
 
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0, 0]])
+def test_multi_device_sparse_payload(torch, oracle_mod, monkeypatch, devices):
+    """SVO_SPARSE_PAYLOAD=1: the multi-device context's display-only frames travel as
+    sparse parts (masks + offsets + hit RGB, packed on each member) that the display
+    member's assemble pulls with no host round trip -- round-robin and weighted
+    deals, frames alternating cameras (a stale part would show), bit-identical to
+    the oracle."""
+    from raytracingtest_amd.distributed import weighted_owner
+    monkeypatch.setenv("SVO_SPARSE_PAYLOAD", "1")
+    svo = build_menger(8)
+    w, h = 333, 250
+    cams = [overview_camera(), Camera(position=(30.0, 12.0, -25.0), rotation=look_rotation((-30.0, -12.0, 25.0)))]
+    refs = [_oracle(oracle_mod, svo, c, w, h) for c in cams]
+    m = RaytracingMaster(devices=devices, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        for owner in (None, weighted_owner(len(devices), 3 / 8)):
+            m.set_band_deal(owner)
+            for i in range(4):
+                ref_hits, ref_rgba, _, _ = refs[i % 2]
+                m.UpdateShaderParameters(cams[i % 2], w, h)
+                b = _bufs(torch, w * h)
+                m.render_frame(w, h, rgba8=b["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME)
+                m.synchronize()
+                _check(b, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+    finally:
+        m.close()
+
+
 def test_multi_device_weighted_deal(torch, oracle_mod):
     """svo_set_band_deal: a three-member context whose display member takes 3 of
     every 8 rounds' bands (it also assembles) renders the same frame as the
