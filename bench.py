@@ -811,6 +811,9 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
     import torch
     from raytracingtest_amd import RaytracingMaster
     n = args.gpus
+    # payload of the members' bands: 3-byte RGB (rgb8 / auto) or the sparse parts (read at context creation)
+    payload = "sparse" if args.payload == "sparse" else "rgb8"
+    os.environ["SVO_SPARSE_PAYLOAD"] = "1" if payload == "sparse" else "0"
     rm = RaytracingMaster(devices=args.device_list, capacity_nodes=len(svo))
     rm.SetSVOBuffer(svo)
     rm.UpdateShaderParameters(cam, W, H)
@@ -872,7 +875,7 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
         "scaling": scaling, "vs_baseline": None, "dtype": "f32",
         "data": "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement",
         "config": {"workload": f"{args.config} {W}x{H} primary rays, {args.camera} camera, display RGBA8 frame",
-                   "parallelism": f"multidevice{n}x8rows+xgmi_pull", "build_s": round(build_s, 2)},
+                   "parallelism": f"multidevice{n}x8rows+xgmi_pull({payload})", "build_s": round(build_s, 2)},
         "multi_gpu": {"devices": args.device_list, "per_device_kernel_ms": [round(k, 4) for k in kern],
                       "assemble_ms": round(asm_ms, 4), "display_device_deal": deal},
     }), flush=True)
