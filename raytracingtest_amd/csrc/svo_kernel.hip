@@ -338,12 +338,18 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             if (adv == 0 && push != 0) diag->fetch_cycles += 1;
             if (push == 0 && adv != 0) diag->fetch_cycles += 1u << 16;
         }
-        if (LM_ON(store & ~of)) {                        // N:97-98 (raw; round trip on POP)
+        if (LM_ON(store & ~of)) {                        // N:97-98 (t_max rounded here, parent on POP)
             // slot = scale - scale_lo = (bits(scale_exp2) >> 23) - 104 - scale_lo; two dwords by
             // ds_write2_b32: no copy into an aligned register pair.  scale_exp2 is an exact
             // power of two (zero mantissa), so the shift needs no mask
             const uint32_t a = push_base + (__float_as_uint(r.sexp) >> SLOT_SH);
-            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(r.t_max) : "memory");
+            // HLSL stack (MODE 0): the float2 round trip of asint(t_max) (N:98, :141-143) is applied
+            // here, when the entry is written -- a POP only ever reads a written entry or the zeroed
+            // init, so the values are the same, and store trips are rarer than POP trips
+            // (r02z A/B: Main pose -1.5 %, flyover +-0, profiles/r02z_ab_round_at_push.txt)
+            const uint32_t tmw = MODE == 0 ? (uint32_t)cvt_i32((float)(int32_t)__float_as_uint(r.t_max))
+                                           : __float_as_uint(r.t_max);
+            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(tmw) : "memory");
         }
         const lmask sx = adv & lx;                       // N:122-125
         const lmask sy = adv & ly;
@@ -390,7 +396,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
             uint32_t pa = e.x, tm = e.y;
             if (MODE == 0) {                             // int2 <- float2((int)parent, asint(t_max))
                 if (GUARD) pa = (uint32_t)cvt_i32((float)(int32_t)pa);
-                tm = (uint32_t)cvt_i32((float)(int32_t)tm);
+                // tm: rounded when it was written
             }
             const uint32_t keep = 0xFFFFFFFFu << scale;
             const uint32_t bx_ = __builtin_amdgcn_ubfe(__float_as_uint(qx), scale, 1);
