@@ -128,3 +128,49 @@ def test_c5_full_frame_parity_and_properties(gpu, oracle_mod):
     assert np.count_nonzero(ref_hits["flags"] & 1) > 100000
     _assert_same(hits, rgba, ref_hits, ref_rgba, "C5 full frame")
     _svo_cache.clear()
+
+
+def test_c3_weak_scaling_frame_split_over_eight_ranks(gpu, oracle_mod):
+    """The frame the driver's 8-GPU SCALE run renders (C3 weak scaling: 5440x3056,
+    16.6 M rays, flyover), split as bench.py's ranks split it: a weighted deal,
+    rank 0's rows straight into the display frame, the other seven ranks' rows
+    as dense 3-byte RGB parts and as sparse parts, rebuilt by svo_assemble_frame --
+    every display word equal to the oracle's."""
+    from raytracingtest_amd import _lib
+    from raytracingtest_amd import distributed as D
+    torch = gpu
+    cfg = CONFIGS["C3"]
+    svo = _svo(cfg)
+    cam = CAMERAS["flyover"]()
+    world = 8
+    W, H = D.weak_frame(cfg["width"], cfg["height"], world)
+    owner = tuple(D.weighted_owner(world, 0.75))
+    c2w, inv_proj = cam.uniforms(W, H)
+    ocam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
+    osvo = oracle_mod.OracleSVO(nodes=svo.to_v2(), attachments=svo.attachments)
+    _, ref_rgba, _ = oracle_mod.render(osvo, ocam, W, H, cfg["stack_mode"], nthreads=THREADS, want_fetches=False)
+    want = oracle_mod.pack_rgba8(ref_rgba)
+    with RaytracingMaster(device=0, capacity_nodes=len(svo)) as rm:
+        rm.SetSVOBuffer(svo)
+        rm.UpdateShaderParameters(cam, W, H)
+        dense, sparse = [None], [None]
+        for r in range(1, world):
+            band = D.rank_band(r, world, owner=owner)
+            rows = D.band_len(H, r, world, owner=owner)
+            nt = ((W + 7) // 8) * ((rows + 7) // 8)
+            d = torch.empty(rows * W * 3, dtype=torch.uint8, device="cuda")
+            p = torch.empty(_lib.sparse_part_bytes(nt, rows * W), dtype=torch.uint8, device="cuda")
+            rm.render_frame(W, H, rgb8=d.data_ptr(), hitmask=p.data_ptr(), band=band, stack_mode=cfg["stack_mode"])
+            rm.pack_hits(W, H, band, d.data_ptr(), p.data_ptr())
+            dense.append(d)
+            sparse.append(p)
+        for fmt, parts in ((_lib.PART_RGB8, dense), (_lib.PART_SPARSE_RGB8, sparse)):
+            frame = torch.full((W * H,), 0x1234567, dtype=torch.int32, device="cuda")
+            rm.render_frame(W, H, rgba8=frame.data_ptr(), layout=_lib.LAYOUT_FRAME,
+                            band=D.rank_band(0, world, owner=owner), stack_mode=cfg["stack_mode"])
+            rm.assemble_frame(W, H, [None] + [p.data_ptr() for p in parts[1:]], fmt, rgba8=frame.data_ptr(),
+                              skip_part=0, owner=owner)
+            rm.synchronize()
+            got = frame.cpu().numpy().view(np.uint32)
+            bad = np.count_nonzero(got != want)
+            assert bad == 0, f"format {fmt}: {bad} of {W * H} display words differ"
