@@ -240,6 +240,14 @@ def test_multi_device_sparse_payload(torch, oracle_mod, monkeypatch, devices):
                 m.render_frame(w, h, rgba8=b["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME)
                 m.synchronize()
                 _check(b, oracle_mod, ref_hits, ref_rgba, keys=("rgba8",))
+        # with the '+1 shadow ray' pass: occluded hits travel as black RGB in the sparse parts
+        sh_hits, sh_rgba, _, _ = _oracle(oracle_mod, svo, cams[0], w, h, shadows=True)
+        m.UpdateShaderParameters(cams[0], w, h)
+        m.SetShadowRays(True)
+        b = _bufs(torch, w * h)
+        m.render_frame(w, h, rgba8=b["rgba8"].data_ptr(), layout=_lib.LAYOUT_FRAME)
+        m.synchronize()
+        _check(b, oracle_mod, sh_hits, sh_rgba, keys=("rgba8",))
     finally:
         m.close()
 
