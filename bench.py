@@ -734,24 +734,33 @@ def choose_payload(args, rm, W, H, rank, world, dev, stream, dist, steps=20):
     best = None
     for p in cands:
         cls = SparseGather if p == "sparse" else Gather
-        g = cls(rm, W, H, rank, world, dev, p, stream, args.no_rgba)
-        g, info = weigh_display_rank(g, args, rm, dist, dev)
         ms = None
-        if len(cands) > 1:
-            for _ in range(3):
-                g.step(args.stack_mode)
-            g.drain()
+        try:
+            g = cls(rm, W, H, rank, world, dev, p, stream, args.no_rgba)
+            g, info = weigh_display_rank(g, args, rm, dist, dev)
+            if len(cands) > 1:
+                for _ in range(3):
+                    g.step(args.stack_mode)
+                g.drain()
+                torch.cuda.synchronize(dev)
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    g.step(args.stack_mode)
+                g.drain()
+                torch.cuda.synchronize(dev)
+                t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                ms = float(t[0]) / steps * 1e3
+                timed[p] = {"ms_per_step": round(ms, 4), "display_share": info["display_share"]}
+        except Exception as e:   # a candidate that fails the same way on every rank is skipped, not fatal
+            if len(cands) == 1 or p == cands[0]:
+                raise
+            print(f"bench.py: payload {p} failed in calibration ({type(e).__name__}: {e}); using {best[1].payload}",
+                  file=sys.stderr, flush=True)
+            timed[p] = {"error": f"{type(e).__name__}: {e}"[:200]}
             torch.cuda.synchronize(dev)
-            dist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                g.step(args.stack_mode)
-            g.drain()
-            torch.cuda.synchronize(dev)
-            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            ms = float(t[0]) / steps * 1e3
-            timed[p] = {"ms_per_step": round(ms, 4), "display_share": info["display_share"]}
+            continue
         if best is None or (ms is not None and ms < best[0]):
             best = (ms, g, info)
         else:
