@@ -876,7 +876,20 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
     sync_all()
     kern = [rm.member(i).kernel_time()[0] for i in range(n)]
     asm_ms = rm.stage_time(1)[0]
+    rm.set_kernel_timing(False)
+    # the assembled display frame vs the same frame rendered whole by a separate
+    # one-device context on the display device (one launch, no split)
+    step()
+    sync_all()
     rm.close()
+    one = RaytracingMaster(device=dev0.index, capacity_nodes=len(svo))
+    one.SetSVOBuffer(svo)
+    one.UpdateShaderParameters(cam, W, H)
+    whole8 = torch.empty_like(frame8)
+    one.render_frame(W, H, rgba8=whole8.data_ptr(), layout=1, stack_mode=args.stack_mode, stream=s.cuda_stream)
+    torch.cuda.synchronize(dev0)
+    frame_check = {"pixels": W * H, "rgba8_mismatches": int((whole8 != frame8).sum().item())}
+    one.close()
     ms = elapsed / args.steps * 1e3
     print(json.dumps({
         "metric": METRIC, "value": round(W * H / (ms * 1e-3) / 1e6, 2), "unit": "Mrays/s", "n_gpus": n,
@@ -886,7 +899,8 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
         "config": {"workload": f"{args.config} {W}x{H} primary rays, {args.camera} camera, display RGBA8 frame",
                    "parallelism": f"multidevice{n}x8rows+xgmi_pull({payload})", "build_s": round(build_s, 2)},
         "multi_gpu": {"devices": args.device_list, "per_device_kernel_ms": [round(k, 4) for k in kern],
-                      "assemble_ms": round(asm_ms, 4), "display_device_deal": deal},
+                      "assemble_ms": round(asm_ms, 4), "display_device_deal": deal,
+                      "assembled_frame_check": frame_check},
     }), flush=True)
 
 
