@@ -676,8 +676,11 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
                                                          : (size_t)rows_i * (size_t)width * elem;
         HIP_TRY(hipSetDevice(m->device));
         if (pr.cap_bytes < bytes) {
+            // the assembles of earlier frames read the old payloads, possibly on another caller
+            // stream than this call's: wait for the last assemble of each payload slot
             HIP_TRY(hipSetDevice(m0->device));
-            HIP_TRY(hipStreamSynchronize(s0));     // the assemble of earlier frames reads the old payloads
+            for (int j = 0; j < 2; ++j)
+                if (ctx->gathered_used[j]) HIP_TRY(hipEventSynchronize(ctx->gathered[j]));
             HIP_TRY(hipSetDevice(m->device));
             HIP_TRY(hipStreamSynchronize(m->stream));
             for (int j = 0; j < 2; ++j) {

@@ -215,6 +215,35 @@ def test_multi_device_context_matches_oracle(torch, oracle_mod, text_svo, device
         m.close()
 
 
+def test_multi_device_payload_regrowth_across_streams(torch, oracle_mod):
+    """Frames of growing size on alternating caller streams: a larger frame
+    reallocates the members' payloads, which the display member's assembles of
+    the earlier frames -- queued on the OTHER caller stream -- may still read;
+    the plugin waits for those assembles (their events), not for this call's
+    stream.  Every frame equals the oracle's."""
+    svo = build_menger(8)
+    cam = overview_camera()
+    sizes = [(96, 64), (200, 120), (333, 250), (96, 64), (480, 272)]
+    refs = {wh: _oracle(oracle_mod, svo, cam, *wh) for wh in set(sizes)}
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    m = RaytracingMaster(devices=[0, 0, 0], capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        frames = []
+        for i, (w, h) in enumerate(sizes):
+            m.UpdateShaderParameters(cam, w, h)
+            f = torch.full((w * h,), 0x1234567, dtype=torch.int32, device="cuda")
+            m.render_frame(w, h, rgba8=f.data_ptr(), layout=_lib.LAYOUT_FRAME, stream=streams[i % 2].cuda_stream)
+            frames.append(f)
+        m.synchronize()
+        torch.cuda.synchronize()
+        for (w, h), f in zip(sizes, frames):
+            got = f.cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, oracle_mod.pack_rgba8(refs[(w, h)][1])), f"{w}x{h} RGBA8 differs"
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0, 0]])
 def test_multi_device_sparse_payload(torch, oracle_mod, monkeypatch, devices):
     """SVO_SPARSE_PAYLOAD=1: the multi-device context's display-only frames travel as
