@@ -15,13 +15,18 @@ the frame split into 8-row bands dealt round-robin to the ranks (SURVEY.md
 8(e)), and every step ends with the north-star gather: rank 0 (the display
 GPU) renders its own bands straight into the display frame, every other rank's
 3-byte RGB band payload goes to rank 0 over RCCL (one batch of sends / receives)
-and rank 0's plugin writes their rows into the frame (svo_assemble_frame).  The gather of frame k overlaps the render
-of frame k+1 (two streams, double-buffered payloads).  For C1-C3 the frame is
-the same camera at sqrt(N) times the linear resolution, so every GPU traces
-~1920x1080 rays per step (weak scaling); C4 / C5 keep their configured frame
-(strong scaling over their 4 / 8 GPUs).  Without torchrun, --gpus N > 1 drives
-N GPUs from one process through the plugin's multi-device context (the Unity
-host's form).
+and rank 0's plugin writes their rows into the frame (svo_assemble_frame).  The
+gather of frame k overlaps the render of frame k+1 (two streams, double-buffered
+payloads).  `value` is the configured frame split over the N GPUs (strong
+scaling: for C3 the metric's own 1920x1080 frame, the reference's one dispatch
+grid cut into bands, RaytracingMaster.cs:66-68); for C1-C3 the weak frame (the
+same camera at sqrt(N) times the linear resolution, ~1920x1080 rays per GPU) is
+measured in the same run and reported beside it as multi_gpu.other_frame.
+Every rank writes the N = 1 step's per-pixel outputs (hit record + RGBA32F) for
+its own pixels plus its band payload.  Strong scaling of the 1080p frame is
+capped by its heaviest wave.  Without torchrun, --gpus N > 1
+drives N GPUs from one process through the plugin's multi-device context (the
+Unity host's form).
 
 roofline: algorithmic bytes per launch = sum over rays of
   8 * F (8-byte V2 node fetches) + 8 * [hit] (attachment) + 24 (hit record) + 16 (RGBA)
@@ -77,7 +82,9 @@ def parse():
     p.add_argument("--sampler", type=int, default=None, help="SampleFunctions.Type (4 = Custom1)")
     p.add_argument("--stack-mode", type=int, default=None, help="0 = HLSL float2 stack, 1 = exact")
     p.add_argument("--frame-scaling", choices=["weak", "strong"], default=None,
-                   help="N > 1: weak = frame grows with N (default for C1-C3), strong = configured frame")
+                   help="N > 1: strong (default) = the configured frame split over the GPUs (C3: the metric's "
+                        "1920x1080 frame); weak = the frame grows with sqrt(N) per axis.  C1-C3 report the other "
+                        "one beside value, labelled")
     p.add_argument("--payload", choices=["auto", "rgb8", "rgba8", "compact", "sparse"], default="auto",
                    help="N > 1: what moves to the display rank: 3-byte RGB (the display word without its "
                         "constant alpha), sparse (tile hit masks + the RGB of hit pixels only; rank 0 computes "
@@ -179,7 +186,10 @@ def main():
     from raytracingtest_amd.native_builder import build_sampler_svo
 
     W, H = args.width, args.height
-    scaling = args.frame_scaling or ("weak" if args.cfg_gpus == 1 else "strong")
+    # N > 1: the configured frame split over the GPUs (strong scaling -- for C3 the
+    # metric's own 1920x1080 frame, north_star "reported at 1, 2, 4 and 8 GPUs"); the
+    # weak frame is reported beside it, labelled (measure_frame's `other`)
+    scaling = args.frame_scaling or "strong"
     if world > 1 and scaling == "weak":
         W, H = D.weak_frame(W, H, world)
     t0 = time.time()
@@ -210,96 +220,49 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
-    gather = None
-    deal_info = None
-    if world > 1:
-        gather, deal_info, payload_choice = choose_payload(args, rm, W, H, rank, world, dev, stream, dist)
-        args.payload = gather.payload
-        hits = rgba = None
-        band = gather.band
-        n_px = gather.n_local
-    else:
-        band = None
-        n_px = W * H
-        hits = torch.empty(n_px * 24, dtype=torch.uint8, device=dev)
-        rgba = None if args.no_rgba else torch.empty(n_px * 4, dtype=torch.float32, device=dev)
+    preflight = rank_preflight(args, rank, world, dev, dist) if world > 1 else None
 
-    def step():
-        if gather is None:
-            rm.render_device(W, H, rgba_ptr=None if rgba is None else rgba.data_ptr(), hits_ptr=hits.data_ptr(),
-                             stack_mode=args.stack_mode, stream=sptr)
-        else:
-            gather.step(args.stack_mode)
+    m = measure_frame(args, rm, W, H, rank, world, dev, stream, dist)
+    gather, hits, rgba, n_px, n_hit, F, host_hits = (m["gather"], m["hits"], m["rgba"], m["n_px"], m["n_hit"],
+                                                      m["F"], m["host_hits"])
+    band, deal_info, payload_choice = m["band"], m["deal_info"], m["payload_choice"]
+    bytes_per_launch, elapsed, kern_ms, kern_ms_max = (m["bytes_per_launch"], m["elapsed"], m["kern_ms"],
+                                                       m["kern_ms_max"])
+    stages, frame_check, per_rank, step_ms = m["stages"], m["frame_check"], m["per_rank"], m["step_ms"]
 
-    def drain():
-        if gather is not None:
-            gather.drain()
-
-    # instrumented pass (outside the timed region): per-ray fetch counts
-    fetch = torch.zeros(n_px, dtype=torch.int32, device=dev)
-    rm.count_fetches_device(W, H, fetch.data_ptr(), stack_mode=args.stack_mode, band=band, stream=sptr)
-    for _ in range(max(1, args.warmup)):
-        step()
-    drain()
-    torch.cuda.synchronize(dev)
-    host_hits = (hits if gather is None else gather.local_hits()).cpu().numpy().view(_lib.HIT_DTYPE)
-    n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
-    F = int(fetch.to(torch.int64).sum().item())
-    bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if args.no_rgba else 16 * n_px)
-    if gather is not None:
-        # the RGBA8 display words (rank 0, in the frame) or band payload (3 B RGB / 4 B RGBA8 /
-        # 12-B compact records) the kernel also writes
-        bytes_per_launch += (4 if rank == 0 else {"rgb8": 3, "rgba8": 4, "compact": 12, "sparse": 3}[args.payload]) * n_px
-
-    # timed region: K steps between barrier + synchronize.  HIP events around each
-    # step only with SVO_STEP_EVENTS=1 (diagnostics): their stream markers add
-    # ~8 us to every step they bracket
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    step_events = os.environ.get("SVO_STEP_EVENTS", "0") != "0"
-    for i in range(args.steps):
-        if step_events:
-            ev[i][0].record(stream)
-        step()
-        if step_events:
-            ev[i][1].record(stream)
-    drain()   # the last frame's assemble (each step assembles the previous frame)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if step_events else None
-    # the roofline's kernel time: the primary-ray kernel's own mean duration, from
-    # HIP events the library records on the launch stream around that kernel
-    # alone (SVO_OPT_KERNEL_TIMING), over K more steps of the same workload right
-    # after the timed region (event pairs inside the timed steps would add
-    # stream markers to the measured step time)
-    rm.set_kernel_timing(True)
-    rm.kernel_time()   # forget anything recorded before
-    for i in range(args.steps):
-        step()
-    drain()
-    kern_ms, n_timed = rm.kernel_time()
-    rm.set_kernel_timing(False)
-    torch.cuda.synchronize(dev)
-    if n_timed != args.steps:
-        raise RuntimeError(f"kernel timing: {n_timed} launches recorded, {args.steps} expected")
-    stages = gather.stage_times(args.stack_mode, max(3, args.steps // 2)) if gather else None
-    frame_check = gather.check_frame(args.stack_mode) if gather is not None and rank == 0 else None
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms_max = float(t[0]), float(t[1])
-        per_rank = [torch.zeros(3, dtype=torch.float64, device=dev) for _ in range(world)]
-        dist.all_gather(per_rank, torch.tensor([kern_ms, stages["gather_ms"], stages["assemble_ms"]],
-                                               dtype=torch.float64, device=dev))
-        per_rank = [[round(float(v), 4) for v in t.tolist()] for t in per_rank]
-    else:
-        kern_ms_max = kern_ms
-        per_rank = None
+    # the other frame of an N > 1 run, reported beside `value` and labelled: the
+    # weak frame (sqrt(N) x the linear resolution, ~W x H rays per GPU) when the run
+    # is the metric's strong split, and vice versa
+    other = None
+    if world > 1 and args.extras and args.cfg_gpus == 1:
+        other_scaling = "weak" if scaling == "strong" else "strong"
+        Wo, Ho = D.weak_frame(args.width, args.height, world) if other_scaling == "weak" else (args.width, args.height)
+        gather.release()
+        rm.UpdateShaderParameters(cam, Wo, Ho)
+        mo = measure_frame(args, rm, Wo, Ho, rank, world, dev, stream, dist)
+        rm.UpdateShaderParameters(cam, W, H)
+        if rank == 0:
+            ms_o = mo["elapsed"] / args.steps * 1e3
+            other = {"scaling": other_scaling, "frame": f"{Wo}x{Ho}", "rays_per_step": Wo * Ho,
+                     "value": round(Wo * Ho / (ms_o * 1e-3) / 1e6, 2), "unit": "Mrays/s",
+                     "ms_per_step": round(ms_o, 4), "steps": args.steps,
+                     "rays_per_gpu_step_rank0": mo["n_px"],
+                     "kernel_ms_rank0": round(mo["kern_ms"], 4), "kernel_ms_max_rank": round(mo["kern_ms_max"], 4),
+                     "roofline_rank0": {"achieved": round(mo["bytes_per_launch"] / (mo["kern_ms"] * 1e-3) / 1e9, 1),
+                                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                        "frac": round(mo["bytes_per_launch"] / (mo["kern_ms"] * 1e-3) / 1e9
+                                                      / HBM_PEAK_GBS, 5),
+                                        "algorithmic_bytes_per_launch": mo["bytes_per_launch"]},
+                     "payload": mo["gather"].payload, "display_rank_deal": mo["deal_info"],
+                     "per_rank_kernel_gather_assemble_ms": mo["per_rank"],
+                     "assembled_frame_check": mo["frame_check"],
+                     "note": ("same per-pixel outputs as value (24-B hit record + RGBA32F + the band payload); "
+                              "the weak frame grows with N so every GPU traces ~1920x1080 rays -- a different "
+                              "workload from the metric's 1920x1080 frame" if other_scaling == "weak" else
+                              "the configured frame split over the N GPUs")}
+        mo["gather"].release()
+        gather = m["gather"] = None
+        torch.cuda.synchronize(dev)
 
     # C3's '+1 shadow ray' (BASELINE.json configs[2]): the same frame with the
     # shadow pass, timed separately on one GPU (reported beside, not as `value`)
@@ -307,12 +270,12 @@ def main():
     if world == 1 and not args.shadows and args.svo != "menger" and args.steps > 0:
         rm.SetShadowRays(True)
         for _ in range(2):
-            step()
+            m["step"]()
         k = max(1, args.steps // 2)
         torch.cuda.synchronize(dev)
         t_sh = time.perf_counter()
         for _ in range(k):
-            step()
+            m["step"]()
         torch.cuda.synchronize(dev)
         sh_ms = (time.perf_counter() - t_sh) / k * 1e3
         rm.SetShadowRays(False)
@@ -391,6 +354,11 @@ def main():
         if world > 1:
             out["multi_gpu"] = {
                 "frame": f"{W}x{H}", "band_rows": 8, "payload": args.payload,
+                "per_pixel_outputs": "every rank: 24-B hit record + 16-B RGBA32F Result of each of its pixels (the "
+                                     "N = 1 step's outputs) + its band payload; rank 0 also the display frame's "
+                                     "RGBA8 words",
+                "preflight": preflight,
+                "other_frame": other,
                 "per_rank_kernel_gather_assemble_ms": per_rank,
                 "render_only_Mrays": round(rays_per_step / (kern_ms_max * 1e-3) / 1e6, 2),
                 "gather_ms_rank0": round(stages["gather_ms"], 4), "assemble_ms_rank0": round(stages["assemble_ms"], 4),
@@ -411,6 +379,159 @@ def main():
     rm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
+    """One measured frame size: the instrumented fetch count, warmup, K timed steps
+    between barrier + synchronize, K more steps with the render kernel bracketed by
+    library HIP events, and (N > 1) the serialized stage times and the assembled-frame
+    check.  Every rank writes the same per-pixel outputs as the N = 1 step (24-byte hit
+    record + RGBA32F Result of each of its pixels) plus, at N > 1, its band payload
+    (rank 0: the display frame's RGBA8 words)."""
+    import torch
+    from raytracingtest_amd import _lib
+    sptr = stream.cuda_stream
+    gather = deal_info = payload_choice = None
+    if world > 1:
+        gather, deal_info, payload_choice = choose_payload(args, rm, W, H, rank, world, dev, stream, dist)
+        args.payload = gather.payload
+        hits = rgba = None
+        band = gather.band
+        n_px = gather.n_local
+    else:
+        band = None
+        n_px = W * H
+        hits = torch.empty(n_px * 24, dtype=torch.uint8, device=dev)
+        rgba = None if args.no_rgba else torch.empty(n_px * 4, dtype=torch.float32, device=dev)
+
+    def step():
+        if gather is None:
+            rm.render_device(W, H, rgba_ptr=None if rgba is None else rgba.data_ptr(), hits_ptr=hits.data_ptr(),
+                             stack_mode=args.stack_mode, stream=sptr)
+        else:
+            gather.step(args.stack_mode)
+
+    def drain():
+        if gather is not None:
+            gather.drain()
+
+    # instrumented pass (outside the timed region): per-ray fetch counts
+    fetch = torch.zeros(max(n_px, 1), dtype=torch.int32, device=dev)
+    rm.count_fetches_device(W, H, fetch.data_ptr(), stack_mode=args.stack_mode, band=band, stream=sptr)
+    for _ in range(max(1, args.warmup)):
+        step()
+    drain()
+    torch.cuda.synchronize(dev)
+    host_hits = (hits if gather is None else gather.local_hits()).cpu().numpy().view(_lib.HIT_DTYPE)
+    n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
+    F = int(fetch[:n_px].to(torch.int64).sum().item())
+    bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if args.no_rgba else 16 * n_px)
+    if gather is not None:
+        # the RGBA8 display words (rank 0, in the frame) or band payload (3 B RGB / 4 B RGBA8 /
+        # 12-B compact records) the kernel also writes
+        bytes_per_launch += (4 if rank == 0 else {"rgb8": 3, "rgba8": 4, "compact": 12, "sparse": 3}[args.payload]) * n_px
+
+    # timed region: K steps between barrier + synchronize.  HIP events around each
+    # step only with SVO_STEP_EVENTS=1 (diagnostics): their stream markers add
+    # ~8 us to every step they bracket
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    step_events = os.environ.get("SVO_STEP_EVENTS", "0") != "0"
+    for i in range(args.steps):
+        if step_events:
+            ev[i][0].record(stream)
+        step()
+        if step_events:
+            ev[i][1].record(stream)
+    drain()   # the last frame's assemble (each step assembles the previous frame)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if step_events else None
+    # the roofline's kernel time: the primary-ray kernel's own mean duration, from
+    # HIP events the library records on the launch stream around that kernel
+    # alone (SVO_OPT_KERNEL_TIMING), over K more steps of the same workload right
+    # after the timed region (event pairs inside the timed steps would add
+    # stream markers to the measured step time)
+    rm.set_kernel_timing(True)
+    rm.kernel_time()   # forget anything recorded before
+    for i in range(args.steps):
+        step()
+    drain()
+    kern_ms, n_timed = rm.kernel_time()
+    rm.set_kernel_timing(False)
+    torch.cuda.synchronize(dev)
+    if n_timed != args.steps:
+        raise RuntimeError(f"kernel timing: {n_timed} launches recorded, {args.steps} expected")
+    stages = gather.stage_times(args.stack_mode, max(3, args.steps // 2)) if gather else None
+    frame_check = gather.check_frame(args.stack_mode) if gather is not None and rank == 0 else None
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+        per_rank = [torch.zeros(3, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(per_rank, torch.tensor([kern_ms, stages["gather_ms"], stages["assemble_ms"]],
+                                               dtype=torch.float64, device=dev))
+        per_rank = [[round(float(v), 4) for v in t.tolist()] for t in per_rank]
+    else:
+        kern_ms_max = kern_ms
+        per_rank = None
+    return dict(gather=gather, hits=hits, rgba=rgba, n_px=n_px, n_hit=n_hit, F=F, host_hits=host_hits, band=band,
+                deal_info=deal_info, payload_choice=payload_choice, bytes_per_launch=bytes_per_launch,
+                elapsed=elapsed, kern_ms=kern_ms, kern_ms_max=kern_ms_max, stages=stages, frame_check=frame_check,
+                per_rank=per_rank, step_ms=step_ms, step=step)
+
+
+def peer_matrix(devices):
+    """hipDeviceCanAccessPeer between every pair of the given device indices."""
+    import torch
+    return [[None if a == b else bool(torch.cuda.can_device_access_peer(a, b)) for b in devices] for a in devices]
+
+
+def device_identity(d):
+    import torch
+    p = torch.cuda.get_device_properties(d)
+    return {"index": int(d), "name": p.name,
+            "pci": "%04x:%02x:%02x" % (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0),
+                                        getattr(p, "pci_device_id", 0))}
+
+
+def rank_preflight(args, rank, world, dev, dist):
+    """N > 1 over torchrun: every rank reports its GPU (index + PCI address); under RCCL
+    ("nccl") two ranks on one GPU is a launch error and the run stops here naming them
+    (the gloo backend rehearses the N > 1 path with ranks sharing one GPU).  Rank 0
+    records the backend, the world size the process group sees and the peer-access
+    matrix of the ranks' devices."""
+    import torch
+    backend = dist.get_backend()
+    ident = device_identity(dev.index)
+    code = int(ident["pci"].replace(":", ""), 16)
+    t = torch.tensor([dev.index, code], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+    allt = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allt, t)
+    devs = [(int(x[0]), int(x[1])) for x in allt]
+    shared = len(set(devs)) < world
+    if shared and backend == "nccl":
+        dup = {}
+        for r, d in enumerate(devs):
+            dup.setdefault(d, []).append(r)
+        bad = {f"device {d[0]} (pci {d[1]:x})": rs for d, rs in dup.items() if len(rs) > 1}
+        raise SystemExit(f"bench.py: ranks share a GPU under RCCL: {bad}; launch one rank per GPU "
+                         f"(LOCAL_RANK -> device) or use SVO_BENCH_BACKEND=gloo for a one-GPU rehearsal")
+    if rank != 0:
+        return None
+    used = sorted({d[0] for d in devs})
+    return {"backend": backend, "process_group_world_size": dist.get_world_size(), "rank_devices": [d[0] for d in devs],
+            "ranks_share_a_gpu": shared, "visible_devices": torch.cuda.device_count(),
+            "device_identity_rank0": ident,
+            "peer_access_matrix": {"devices": used, "can_access": peer_matrix(used)},
+            "rccl_device_tensors": backend == "nccl",
+            "note": "under nccl the payload gather and the SVO broadcast move device tensors (RCCL over xGMI); "
+                    "under gloo they are staged through host memory (one-GPU rehearsal only)"}
 
 
 class Gather:
@@ -473,6 +594,15 @@ class Gather:
         self.last = None         # slot of the last complete frame
         # bytes one sending rank moves per frame (rank 1's share; rank 0 sends nothing)
         self.payload_bytes = D.band_len(H, 1, world, owner=owner) * W * self.elem
+
+    def release(self):
+        """Finish pending work and drop the device buffers (before another frame size)."""
+        self.drain()
+        self.torch.cuda.synchronize(self.dev)
+        for name in ("frame8", "fhits", "frgba", "dummy", "parts", "parts_c", "send", "hits", "rgba", "dense",
+                     "cbuf", "cnt_host"):
+            if hasattr(self, name):
+                setattr(self, name, None)
 
     def local_hits(self):
         """This rank's hit records (uint8 tensor, band order) of the last render."""
@@ -801,7 +931,7 @@ def weigh_display_rank(gather, args, rm, dist, dev):
     dist.broadcast(t, 0)
     share = max(float(t[0]), 1.0 / 8.0)   # at least one band per round: every rank renders
     from raytracingtest_amd import distributed as D
-    owner = D.weighted_owner(gather.world, share)
+    owner = D.weighted_owner(gather.world, share) or [0] * 8
     info = {"display_share": round(owner.count(0) / 8, 3), "calibration": measured,
             "cycle_bands": len(owner), "rows_rank0": gather.D.band_len(gather.H, 0, gather.world, owner=owner),
             "rows_rank1": gather.D.band_len(gather.H, 1, gather.world, owner=owner)}
@@ -816,91 +946,153 @@ def weigh_display_rank(gather, args, rm, dist, dev):
 
 def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
     """One process, N GPUs through the plugin's multi-device context (the Unity
-    host's form): the display frame (RGBA8) of W x H rays per step on device 0."""
+    host's form).  A step renders W x H rays split over the members and leaves the
+    N = 1 step's outputs -- 24-B hit records and the RGBA32F Result, plus the
+    display RGBA8 words -- for the whole frame on device 0: members send 12-byte
+    compact records, from which the display device rebuilds normal and Result."""
     import torch
-    from raytracingtest_amd import RaytracingMaster
+    from raytracingtest_amd import RaytracingMaster, _lib
+    from raytracingtest_amd import distributed as D
     n = args.gpus
-    # payload of the members' bands: 3-byte RGB (rgb8 / auto) or the sparse parts (read at context creation)
-    payload = "sparse" if args.payload == "sparse" else "rgb8"
-    os.environ["SVO_SPARSE_PAYLOAD"] = "1" if payload == "sparse" else "0"
     rm = RaytracingMaster(devices=args.device_list, capacity_nodes=len(svo))
     rm.SetSVOBuffer(svo)
-    rm.UpdateShaderParameters(cam, W, H)
     dev0 = torch.device("cuda", args.device_list[0])
-    frame8 = torch.empty(W * H, dtype=torch.int32, device=dev0)
     s = torch.cuda.Stream(dev0)
-
-    def step():
-        rm.render_frame(W, H, rgba8=frame8.data_ptr(), layout=1, stack_mode=args.stack_mode, stream=s.cuda_stream)
+    links = rm.member_links()
+    distinct = sorted(set(args.device_list))
+    preflight = {"members": [{"device": d, "link": k} for d, k in links],
+                 "members_share_a_gpu": len(distinct) < n,
+                 "peer_access_matrix": {"devices": distinct, "can_access": peer_matrix(distinct)},
+                 "note": "link: how a member's compact payload reaches the display device -- xgmi_peer_pull "
+                         "(the assemble kernel reads it over xGMI), peer_copy (hipMemcpyPeerAsync into the display "
+                         "device: no peer access), self (same device index: the one-GPU rehearsal)"}
 
     def sync_all():
-        for d in sorted(set(args.device_list)):
+        for d in distinct:
             torch.cuda.synchronize(d)
 
-    # the display device also assembles: the same calibrated weighted deal as the ranks
-    deal = None
-    share = args.display_share
-    for _ in range(max(1, args.warmup)):
-        step()
-    sync_all()
-    if share is None:
-        rm.set_kernel_timing(True)
-        rm.stage_time(1)
-        for i in range(n):
-            rm.member(i).kernel_time()
-        for _ in range(5):
+    def measure(Wf, Hf):
+        rm.UpdateShaderParameters(cam, Wf, Hf)
+        hits = torch.empty(Wf * Hf * 24, dtype=torch.uint8, device=dev0)
+        rgba = None if args.no_rgba else torch.empty(Wf * Hf * 4, dtype=torch.float32, device=dev0)
+        frame8 = torch.empty(Wf * Hf, dtype=torch.int32, device=dev0)
+
+        def step():
+            rm.render_frame(Wf, Hf, hits=hits.data_ptr(), rgba=None if rgba is None else rgba.data_ptr(),
+                            rgba8=frame8.data_ptr(), layout=1, stack_mode=args.stack_mode, stream=s.cuda_stream)
+
+        rm.set_band_deal(None)
+        for _ in range(max(1, args.warmup)):
             step()
         sync_all()
-        kern = max(rm.member(i).kernel_time()[0] for i in range(n))
-        asm = rm.stage_time(1)[0]
+        # the display device also assembles: the same calibrated weighted deal as the ranks
+        share = args.display_share
+        if share is None:
+            rm.set_kernel_timing(True)
+            rm.stage_time(0)
+            rm.stage_time(1)
+            for _ in range(5):
+                step()
+            sync_all()
+            kern = rm.stage_time(0)[0]       # the slowest member's render kernel
+            asm = rm.stage_time(1)[0]
+            rm.set_kernel_timing(False)
+            share = max(0.0, 1.0 - (asm + 0.003) / kern)
+        owner = D.weighted_owner(n, max(share, 1.0 / 8.0))
+        deal = None
+        if owner is not None and owner.count(0) < 8:
+            rm.set_band_deal(owner)
+            deal = {"display_share": owner.count(0) / 8, "cycle_bands": len(owner)}
+        else:
+            owner = None
+        for _ in range(max(1, args.warmup)):
+            step()
+        sync_all()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        sync_all()
+        elapsed = time.perf_counter() - t
+        rm.set_kernel_timing(True)
+        rm.stage_time(0)
+        rm.stage_time(1)
+        for _ in range(args.steps):
+            step()
+        sync_all()
+        kern = [rm.member(i).kernel_time()[0] for i in range(n)]
+        asm_ms = rm.stage_time(1)[0]
         rm.set_kernel_timing(False)
-        share = max(0.0, 1.0 - (asm + 0.003) / kern)
-    from raytracingtest_amd import distributed as D
-    owner = D.weighted_owner(n, max(share, 1.0 / 8.0))
-    if owner.count(0) < 8:
-        rm.set_band_deal(owner)
-        deal = {"display_share": owner.count(0) / 8, "cycle_bands": len(owner)}
-    for _ in range(max(1, args.warmup)):
+        # the display member's algorithmic bytes (its own band: 8 F + 8 hits + 24 + 16 + 4 per pixel)
+        band0 = (D.DEFAULT_BAND_ROWS, 0, n) if owner is None else (D.DEFAULT_BAND_ROWS, 0, n, tuple(owner))
+        rows0 = D.band_len(Hf, 0, n, owner=owner)
+        fetch = torch.zeros(max(rows0 * Wf, 1), dtype=torch.int32, device=dev0)
+        m0 = rm.member(0)
+        m0.count_fetches_device(Wf, Hf, fetch.data_ptr(), stack_mode=args.stack_mode, band=band0,
+                                stream=s.cuda_stream)
         step()
-    sync_all()
-    t = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync_all()
-    elapsed = time.perf_counter() - t
-    rm.set_kernel_timing(True)
-    rm.stage_time(0)
-    rm.stage_time(1)
-    for _ in range(args.steps):
-        step()
-    sync_all()
-    kern = [rm.member(i).kernel_time()[0] for i in range(n)]
-    asm_ms = rm.stage_time(1)[0]
-    rm.set_kernel_timing(False)
-    # the assembled display frame vs the same frame rendered whole by a separate
-    # one-device context on the display device (one launch, no split)
-    step()
-    sync_all()
+        sync_all()
+        F = int(fetch.to(torch.int64).sum().item())
+        from raytracingtest_amd import band_rows
+        ys = torch.as_tensor(band_rows(Hf, band0), device=dev0)
+        h0 = hits.view(Hf, Wf * 24)[ys].reshape(-1).cpu().numpy().view(_lib.HIT_DTYPE)
+        n_hit0 = int(np.count_nonzero(h0["flags"] & 1))
+        bytes0 = 8 * F + 8 * n_hit0 + (24 + (0 if args.no_rgba else 16) + 4) * rows0 * Wf
+        # the assembled frame vs the same frame rendered whole by a separate one-device
+        # context on the display device (one launch, no split): every output
+        one = RaytracingMaster(device=dev0.index, capacity_nodes=len(svo))
+        one.SetSVOBuffer(svo)
+        one.UpdateShaderParameters(cam, Wf, Hf)
+        w_hits, w8 = torch.empty_like(hits), torch.empty_like(frame8)
+        w_rgba = None if rgba is None else torch.empty_like(rgba)
+        one.render_frame(Wf, Hf, hits=w_hits.data_ptr(), rgba=None if w_rgba is None else w_rgba.data_ptr(),
+                         rgba8=w8.data_ptr(), layout=1, stack_mode=args.stack_mode, stream=s.cuda_stream)
+        torch.cuda.synchronize(dev0)
+        check = {"pixels": Wf * Hf, "rgba8_mismatches": int((w8 != frame8).sum().item()),
+                 "hit_record_mismatches": int((w_hits.view(-1, 24) != hits.view(-1, 24)).any(1).sum().item()),
+                 "rgba32f_mismatches": None if rgba is None else
+                 int((w_rgba.view(-1, 4) != rgba.view(-1, 4)).any(1).sum().item())}
+        one.close()
+        ms = elapsed / args.steps * 1e3
+        return {"ms": ms, "kern": kern, "asm_ms": asm_ms, "deal": deal, "check": check, "bytes0": bytes0,
+                "F0": F, "rows0": rows0}
+
+    r = measure(W, H)
+    other = None
+    if args.extras and args.cfg_gpus == 1:
+        other_scaling = "weak" if scaling == "strong" else "strong"
+        Wo, Ho = D.weak_frame(args.width, args.height, n) if other_scaling == "weak" else (args.width, args.height)
+        ro = measure(Wo, Ho)
+        other = {"scaling": other_scaling, "frame": f"{Wo}x{Ho}", "rays_per_step": Wo * Ho,
+                 "value": round(Wo * Ho / (ro["ms"] * 1e-3) / 1e6, 2), "unit": "Mrays/s",
+                 "ms_per_step": round(ro["ms"], 4), "per_device_kernel_ms": [round(k, 4) for k in ro["kern"]],
+                 "assemble_ms": round(ro["asm_ms"], 4), "assembled_frame_check": ro["check"]}
     rm.close()
-    one = RaytracingMaster(device=dev0.index, capacity_nodes=len(svo))
-    one.SetSVOBuffer(svo)
-    one.UpdateShaderParameters(cam, W, H)
-    whole8 = torch.empty_like(frame8)
-    one.render_frame(W, H, rgba8=whole8.data_ptr(), layout=1, stack_mode=args.stack_mode, stream=s.cuda_stream)
-    torch.cuda.synchronize(dev0)
-    frame_check = {"pixels": W * H, "rgba8_mismatches": int((whole8 != frame8).sum().item())}
-    one.close()
-    ms = elapsed / args.steps * 1e3
+    ms = r["ms"]
+    achieved = r["bytes0"] / (r["kern"][0] * 1e-3) / 1e9
+    kind = "Menger" if args.svo == "menger" else "Custom1"
     print(json.dumps({
         "metric": METRIC, "value": round(W * H / (ms * 1e-3) / 1e6, 2), "unit": "Mrays/s", "n_gpus": n,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement",
-        "config": {"workload": f"{args.config} {W}x{H} primary rays, {args.camera} camera, display RGBA8 frame",
-                   "parallelism": f"multidevice{n}x8rows+xgmi_pull({payload})", "build_s": round(build_s, 2)},
-        "multi_gpu": {"devices": args.device_list, "per_device_kernel_ms": [round(k, 4) for k in kern],
-                      "assemble_ms": round(asm_ms, 4), "display_device_deal": deal,
-                      "assembled_frame_check": frame_check},
+        "data": ("synthetic: 256^3 Menger sponge surface SVO (SURVEY.md 8(d) C2)" if args.svo == "menger" else
+                 "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement"),
+        "config": {"workload": (f"{args.config} depth-{args.max_level - 1} ({1 << (args.max_level - 1)}^3) {kind} SVO, "
+                                f"{W}x{H} primary rays, {args.camera} camera"),
+                   "parallelism": f"multidevice{n}x8rows+xgmi_pull(compact)", "build_s": round(build_s, 2),
+                   "svo_nodes": len(svo), "stack_mode": "hlsl" if args.stack_mode == 0 else "exact"},
+        "roofline": {"bound": "latency", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel": "render_tile_kernel on the display device (its own bands), library HIP events",
+                     "kernel_ms": round(r["kern"][0], 4), "kernel_ms_max_member": round(max(r["kern"]), 4),
+                     "algorithmic_bytes_per_launch": r["bytes0"],
+                     "bytes_formula": "display device's rays: 8*F + 8*hits + 24 (hit record) + 16 (RGBA32F) + 4 (RGBA8)"},
+        "multi_gpu": {"devices": args.device_list, "preflight": preflight,
+                      "per_pixel_outputs": "hit records + RGBA32F Result + RGBA8 of the whole frame on device 0 "
+                                           "(the N = 1 step's outputs + display words); members send 12-B compact "
+                                           "records",
+                      "per_device_kernel_ms": [round(k, 4) for k in r["kern"]],
+                      "assemble_ms": round(r["asm_ms"], 4), "display_device_deal": r["deal"],
+                      "assembled_frame_check": r["check"], "other_frame": other},
     }), flush=True)
 
 

@@ -111,9 +111,20 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out);
  * svo_render / svo_render_device / svo_render_frame render the whole frame in
  * `band_rows`-row bands dealt round-robin over the devices and leave it on
  * devices[0] (outputs are devices[0] pointers, frame layout).  The reference
- * dispatches one grid over the whole frame (RaytracingMaster.cs:66-68). */
+ * dispatches one grid over the whole frame (RaytracingMaster.cs:66-68).
+ * Payload transport per member (svo_get_member_link): the display device pulls a
+ * member's payload over xGMI when hipDeviceCanAccessPeer allows it; when it does
+ * not (or env SVO_PEER_COPY=1 forces it), the member's stream copies the payload
+ * into a buffer on the display device (hipMemcpyPeerAsync) and the assemble
+ * reads that copy -- creation no longer fails for lack of peer access. */
 int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes, int band_rows, svo_ctx **out);
 int svo_num_devices(svo_ctx *ctx, int *num_devices);
+/* How member `index`'s band payload reaches the display device: SVO_LINK_SELF
+ * (the display device itself, or the same device index), SVO_LINK_PEER (pulled
+ * over xGMI with peer access), SVO_LINK_COPY (copied by hipMemcpyPeerAsync).
+ * *device = the member's HIP device.  Single-device contexts: index 0, SELF. */
+enum { SVO_LINK_SELF = 0, SVO_LINK_PEER = 1, SVO_LINK_COPY = 2 };
+int svo_get_member_link(svo_ctx *ctx, int index, int *device, int *link);
 /* Weighted band deal for a multi-device context (svo_band.cycle / owner): band b
  * goes to member owner[b % cycle]; e.g. fewer bands for devices[0], which also
  * assembles the frame.  cycle 0 = round-robin (the default). */
@@ -220,7 +231,10 @@ int svo_set_options(svo_ctx *ctx, uint32_t options);
  * counterpart. */
 int svo_kernel_time(svo_ctx *ctx, double *mean_ms, uint64_t *launches);
 /* The same for a stage: SVO_STAGE_KERNEL (= svo_kernel_time) or SVO_STAGE_ASSEMBLE
- * (the assemble kernel of svo_assemble_frame / a multi-device frame). */
+ * (the assemble kernel of svo_assemble_frame / a multi-device frame).  On a
+ * multi-device context every member's recorded launches of the stage are drained
+ * and the slowest member's mean is returned (launches: that member's count);
+ * svo_get_member gives one device's own figure. */
 enum { SVO_STAGE_KERNEL = 0, SVO_STAGE_ASSEMBLE = 1 };
 int svo_stage_time(svo_ctx *ctx, int stage, double *mean_ms, uint64_t *launches);
 
@@ -237,8 +251,9 @@ int svo_accumulate(svo_ctx *ctx, void *d_accum, const void *d_sample, size_t n_p
 /* ~ RaytracingMaster.OnRenderImage end to end (RaytracingMaster.cs:55-74 with
  * AddShader.shader:44-47): render one sample of the frame at the current camera,
  * blend it into the context's device-resident accumulation frame with
- * _Sample = `sample` (svo_accumulate's blend; the frame is zeroed whenever its
- * size changes), and copy the accumulated frame to the host as display RGBA8
+ * _Sample = `sample` (svo_accumulate's blend; the frame is reallocated whenever
+ * its size changes, and the first sample after that is blended as sample 0 --
+ * it replaces the frame -- whatever `sample` says), and copy the accumulated frame to the host as display RGBA8
  * words (4 B/px, R in the low byte = Unity TextureFormat.RGBA32; each colour
  * channel (uint)(saturate(c) * 255 + 0.5), alpha 255) and/or RGBA32F (16 B/px); either output may be
  * NULL, not both.  Only the accumulated frame crosses PCIe: 8.3 MB per 1080p

@@ -27,18 +27,20 @@ assert HIT_DTYPE.itemsize == 24
 COMPACT_DTYPE = np.dtype([("parent", "<u4"), ("meta", "<u4"), ("t", "<f4")])   # svo_hit_compact
 assert COMPACT_DTYPE.itemsize == 12
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
            "svo_destroy", "svo_last_error", "svo_abi_version", "svo_set_options", "svo_accumulate",
            "svo_kernel_time", "svo_create_multi", "svo_num_devices", "svo_get_member", "svo_render_frame",
            "svo_assemble_frame", "svo_stage_time", "svo_render_progressive", "svo_set_band_deal",
-           "svo_pack_hits")
+           "svo_pack_hits", "svo_get_member_link")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
 PART_COMPACT, PART_RGBA8, PART_RGB8, PART_SPARSE_RGB8 = 0, 1, 2, 3
+LINK_SELF, LINK_PEER, LINK_COPY = 0, 1, 2
+LINK_NAMES = {LINK_SELF: "self", LINK_PEER: "xgmi_peer_pull", LINK_COPY: "peer_copy"}
 
 
 def sparse_head_bytes(n_tiles):
@@ -118,6 +120,7 @@ def lib():
         "svo_create_multi": [ctypes.POINTER(i), i, sz, i, ctypes.POINTER(vp)],
         "svo_num_devices": [vp, ctypes.POINTER(i)],
         "svo_get_member": [vp, i, ctypes.POINTER(vp)],
+        "svo_get_member_link": [vp, i, ctypes.POINTER(i), ctypes.POINTER(i)],
         "svo_render_frame": [vp, i, i, i, vp, ctypes.POINTER(SvoFrame), vp],
         "svo_assemble_frame": [vp, i, i, ctypes.POINTER(SvoBand), i, ctypes.POINTER(vp), i, i,
                                ctypes.POINTER(SvoFrame), vp],

@@ -61,6 +61,17 @@ struct Upload {
 
 enum { STAGE_KERNEL = 0, STAGE_ASSEMBLE = 1, N_STAGES = 2 };
 
+// The tile-order cache key: the exact geometry (and deal) an order was built for.
+struct Geo {
+    int width = -1, local_rows = -1, rows = -1, rank = -1, count = -1, xcd = -1, n_tiles = -1;
+    uint64_t deal = 0;
+    bool operator==(const Geo &o) const {
+        return width == o.width && local_rows == o.local_rows && rows == o.rows && rank == o.rank &&
+               count == o.count && xcd == o.xcd && n_tiles == o.n_tiles && deal == o.deal;
+    }
+    bool operator!=(const Geo &o) const { return !(*this == o); }
+};
+
 // Cost-ordered dispatch state of the renders on one stream: every launch records each
 // 8x8 tile's trip count; the order kernel, enqueued right behind it, turns them into
 // the heaviest-first dispatch order of the next launch at the same geometry.  One set
@@ -77,8 +88,8 @@ struct Sched {
     uint16_t *shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
     uint32_t *shadow_order = nullptr;
     size_t cap = 0;
-    long long order_key = -1;        // geometry tile_order was built for (-1: none)
-    long long shadow_key = -1;
+    Geo order_key;                   // geometry tile_order was built for (width -1: none)
+    Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
     unsigned long long built_view = 0;   // the context's view generation the order was built under
     int built_mode = -1;                 // shadows | stack_mode << 2 of the costs it was built from
@@ -90,7 +101,11 @@ struct Peer {                       // one per member of a multi-device context 
     hipEvent_t rendered[2] = {nullptr, nullptr};
     void *dense = nullptr;               // sparse payload: the band's dense RGB before the pack
     size_t dense_cap = 0;
+    int link = SVO_LINK_SELF;            // how the payload reaches the display device (svo_get_member_link)
+    void *local[2] = {nullptr, nullptr}; // SVO_LINK_COPY: the payload's copy on the display device
+    size_t local_cap = 0;
 };
+
 
 }  // namespace
 
@@ -200,7 +215,7 @@ void free_sched(Sched &q) {
     q.shadow_cost = nullptr;
     q.shadow_order = nullptr;
     q.cap = 0;
-    q.order_key = q.shadow_key = -1;
+    q.order_key = q.shadow_key = Geo();
 }
 
 // The scheduling state of stream s: its own set, or a free one, or the least recently
@@ -218,7 +233,7 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         for (Sched &q : ctx->sched)
             if (q.last_use < pick->last_use) pick = &q;
         if (pick->done) HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
-        pick->order_key = pick->shadow_key = -1;   // built for another stream's frames
+        pick->order_key = pick->shadow_key = Geo();   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
     }
     if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
@@ -324,8 +339,12 @@ int ensure_out(svo_ctx *ctx, size_t px) {
     return SVO_OK;
 }
 
-int ensure_accum(svo_ctx *ctx, int width, int height) {
+// *fresh = true when the frame was (re)allocated: the caller's sample counter then
+// describes a frame that no longer exists, so the next blend must replace it (sample 0)
+int ensure_accum(svo_ctx *ctx, int width, int height, bool *fresh) {
+    *fresh = false;
     if (ctx->d_accum && ctx->accum_w == width && ctx->accum_h == height) return SVO_OK;
+    *fresh = true;
     HIP_TRY(hipDeviceSynchronize());   // an earlier asynchronous launch may still use the old frame
     if (ctx->d_accum) hipFree(ctx->d_accum);
     if (ctx->d_accum8) hipFree(ctx->d_accum8);
@@ -494,14 +513,21 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.prio = ctx->prio;
     const bool ordered = ctx->tile_order && !p.out.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
-    long long key = -1;
+    Geo key;
     Sched *q = nullptr;
     if (ordered) {
         rc = sched_for(ctx, s, &q);
         if (rc) return rc;
-        key = ((long long)width << 40) ^ ((long long)p.local_rows << 16) ^ ((long long)b.rows << 8) ^
-              (long long)b.rank ^ ((long long)b.count << 4) ^ ((long long)p.xcd_remap << 60) ^ (long long)(b.key() << 1);
-        if (key < 0) key = ~key;   // -1 means "no order"
+        // field by field (a hash of overlapping shifted fields could match another geometry
+        // and reuse a permutation of a different tile count)
+        key.width = width;
+        key.local_rows = p.local_rows;
+        key.rows = b.rows;
+        key.rank = b.rank;
+        key.count = b.count;
+        key.xcd = p.xcd_remap;
+        key.n_tiles = n_tiles;
+        key.deal = b.key();
         if (q->cap < (size_t)n_tiles) {
             HIP_TRY(hipStreamSynchronize(s));   // a pending launch on this stream may still use the old buffers
             free_sched(*q);
@@ -716,8 +742,29 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
                                                  m->stream);
             if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("pack hits launch: ") + hipGetErrorString(e));
         }
-        HIP_TRY(hipEventRecord(pr.rendered[k], m->stream));
         parts[i] = pr.buf[k];
+        if (pr.link == SVO_LINK_COPY) {
+            // no peer access to this member: its stream copies the payload into a buffer on the
+            // display device (the whole capacity for a sparse part, whose size only the device
+            // knows).  local[k] is reused only after frame k's assemble: the member's stream
+            // waited for gathered[k] above, before this frame's render
+            if (pr.local_cap < bytes) {
+                HIP_TRY(hipSetDevice(m0->device));
+                for (int j = 0; j < 2; ++j)
+                    if (ctx->gathered_used[j]) HIP_TRY(hipEventSynchronize(ctx->gathered[j]));
+                for (int j = 0; j < 2; ++j) {
+                    if (pr.local[j]) hipFree(pr.local[j]);
+                    pr.local[j] = nullptr;
+                }
+                pr.local_cap = 0;
+                for (int j = 0; j < 2; ++j) HIP_TRY(hipMalloc(&pr.local[j], std::max<size_t>(bytes, 16)));
+                pr.local_cap = bytes;
+                HIP_TRY(hipSetDevice(m->device));
+            }
+            HIP_TRY(hipMemcpyPeerAsync(pr.local[k], m0->device, pr.buf[k], m->device, bytes, m->stream));
+            parts[i] = pr.local[k];
+        }
+        HIP_TRY(hipEventRecord(pr.rendered[k], m->stream));
     }
     HIP_TRY(hipSetDevice(m0->device));
     for (int i = 1; i < n; ++i) HIP_TRY(hipStreamWaitEvent(s0, ctx->peers[i].rendered[k], 0));
@@ -790,7 +837,7 @@ int destroy_single(svo_ctx *ctx) {
 
 extern "C" {
 
-int svo_abi_version(void) { return 6; }
+int svo_abi_version(void) { return 7; }
 
 const char *svo_last_error(void) { return g_last_error.c_str(); }
 
@@ -854,18 +901,34 @@ int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes,
         if (rc) return bail(rc);
         g->members.push_back(m);
     }
-    // the display device reads every other device's payload over xGMI
+    // the display device reads every other device's payload over xGMI (peer access);
+    // a member it cannot map gets the copy fallback (SVO_LINK_COPY, multi_render).
+    // SVO_PEER_COPY=1 forces the copy for every member but the display device itself
+    // (the one-GPU test of that path: a repeated device index)
+    const char *force = std::getenv("SVO_PEER_COPY");
+    const bool force_copy = force && std::atoi(force) != 0;
     for (int i = 1; i < num_devices; ++i) {
-        if (devices[i] == devices[0]) continue;
+        Peer &pr = g->peers[i];
+        if (devices[i] == devices[0]) {
+            pr.link = force_copy ? SVO_LINK_COPY : SVO_LINK_SELF;
+            continue;
+        }
         int ok = 0;
         hipError_t e = hipDeviceCanAccessPeer(&ok, devices[0], devices[i]);
-        if (e != hipSuccess || !ok)
-            return bail(fail(SVO_ERR_HIP, "device " + std::to_string(devices[0]) + " cannot access device " +
-                                              std::to_string(devices[i]) + " (no xGMI peer access)"));
+        if (e != hipSuccess || !ok || force_copy) {
+            (void)hipGetLastError();
+            pr.link = SVO_LINK_COPY;
+            continue;
+        }
         hipSetDevice(devices[0]);
         e = hipDeviceEnablePeerAccess(devices[i], 0);
-        if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
-        else if (e != hipSuccess) return bail(fail(SVO_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e)));
+        if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) {
+            (void)hipGetLastError();
+            pr.link = SVO_LINK_PEER;
+        } else {   // reported as possible, refused when enabled: copy instead
+            (void)hipGetLastError();
+            pr.link = SVO_LINK_COPY;
+        }
     }
     for (int i = 1; i < num_devices; ++i) {
         hipSetDevice(devices[i]);
@@ -902,6 +965,15 @@ int svo_set_band_deal(svo_ctx *ctx, int cycle, const uint8_t *owner) {
 int svo_num_devices(svo_ctx *ctx, int *n) {
     if (!ctx || !n) return fail(SVO_ERR_ARG, "null argument");
     *n = is_multi(ctx) ? (int)ctx->members.size() : 1;
+    return SVO_OK;
+}
+
+int svo_get_member_link(svo_ctx *ctx, int index, int *device, int *link) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    const int n = is_multi(ctx) ? (int)ctx->members.size() : 1;
+    if (index < 0 || index >= n) return fail(SVO_ERR_ARG, "member index out of range");
+    if (device) *device = is_multi(ctx) ? ctx->members[index]->device : ctx->device;
+    if (link) *link = is_multi(ctx) && index > 0 ? ctx->peers[index].link : SVO_LINK_SELF;
     return SVO_OK;
 }
 
@@ -1084,8 +1156,10 @@ int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, 
     HIP_TRY(hipSetDevice(c->device));
     int rc = ensure_out(c, px);
     if (rc) return rc;
-    rc = ensure_accum(c, width, height);
+    bool fresh = false;
+    rc = ensure_accum(c, width, height, &fresh);
     if (rc) return rc;
+    if (fresh) sample = 0;   // a resized target: this sample replaces the (zeroed) frame
     rc = order_scratch(c, c->stream);
     if (rc) return rc;
     svo_frame f{};
@@ -1158,7 +1232,23 @@ int svo_set_options(svo_ctx *ctx, uint32_t options) {
 int svo_stage_time(svo_ctx *ctx, int stage, double *mean_ms, uint64_t *launches) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
     if (stage < 0 || stage >= N_STAGES) return fail(SVO_ERR_ARG, "unknown stage");
-    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    if (is_multi(ctx)) {
+        // every member records its own launches (svo_set_options sets the option on all):
+        // drain them all, so none accumulates events, and report the slowest member
+        double worst = 0.0;
+        uint64_t worst_n = 0;
+        for (svo_ctx *m : ctx->members) {
+            double ms = 0.0;
+            uint64_t n = 0;
+            int rc = svo_stage_time(m, stage, &ms, &n);
+            if (rc) return rc;
+            if (n && (worst_n == 0 || ms > worst)) { worst = ms; worst_n = n; }
+        }
+        if (mean_ms) *mean_ms = worst;
+        if (launches) *launches = worst_n;
+        return SVO_OK;
+    }
+    svo_ctx *c = ctx;
     HIP_TRY(hipSetDevice(c->device));
     double sum = 0.0;
     uint64_t n = 0;
@@ -1237,6 +1327,9 @@ int svo_destroy(svo_ctx *ctx) {
         if (pr.dense) hipFree(pr.dense);
     }
     if (!ctx->members.empty()) hipSetDevice(ctx->members[0]->device);
+    for (size_t i = 1; i < ctx->peers.size(); ++i)
+        for (int j = 0; j < 2; ++j)
+            if (ctx->peers[i].local[j]) hipFree(ctx->peers[i].local[j]);
     for (int j = 0; j < 2; ++j)
         if (ctx->gathered[j]) hipEventDestroy(ctx->gathered[j]);
     for (svo_ctx *m : ctx->members) destroy_single(m);

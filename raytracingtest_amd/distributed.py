@@ -51,7 +51,11 @@ def weighted_owner(world, display_share, per_round=8):
     the display rank (0) takes one band and rank 0 takes one in only
     round(display_share * per_round) of them -- rank 0 also receives and assembles
     the frame, so it gets fewer rows.  Rounds interleave the ranks,
-    so a partial cycle at the frame's bottom stays balanced."""
+    so a partial cycle at the frame's bottom stays balanced.  One rank: None
+    (round-robin, the whole frame) -- an empty table would read as "no owner" on
+    the plugin side but divide by zero in band_rows."""
+    if world <= 1:
+        return None
     k = int(round(min(max(display_share, 0.0), 1.0) * per_round))
     owner = []
     for j in range(per_round):

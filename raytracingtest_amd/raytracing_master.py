@@ -152,6 +152,17 @@ class RaytracingMaster:
         check(_lib.lib().svo_num_devices(self._ctx, ctypes.byref(n)), "svo_num_devices")
         return n.value
 
+    def member_links(self):
+        """[(device, link name)] per member: how each member's band payload reaches the
+        display device (svo_get_member_link: "self", "xgmi_peer_pull" or "peer_copy")."""
+        out = []
+        for i in range(self.num_devices()):
+            d, k = ctypes.c_int(), ctypes.c_int()
+            check(_lib.lib().svo_get_member_link(self._ctx, i, ctypes.byref(d), ctypes.byref(k)),
+                  "svo_get_member_link")
+            out.append((d.value, _lib.LINK_NAMES.get(k.value, str(k.value))))
+        return out
+
     def member(self, index):
         """The per-device context `index` (owned by this one) as a RaytracingMaster view."""
         c = ctypes.c_void_p()
@@ -176,6 +187,11 @@ class RaytracingMaster:
         accumulated frame or None); only those cross PCIe."""
         rgba8 = np.zeros((height, width), np.uint32) if want_rgba8 else None
         rgba = np.zeros((height, width, 4), np.float32) if want_rgba else None
+        if getattr(self, "_accum_size", None) != (width, height):
+            # a new render-target size (InitRenderTexture, RaytracingMaster.cs:76-88): the
+            # plugin starts a fresh accumulation frame, so the sample count restarts too
+            self._accum_size = (width, height)
+            self.currentSample = 0
         check(_lib.lib().svo_render_progressive(self._ctx, width, height, stack_mode, self.currentSample,
                                                 None if rgba8 is None else rgba8.ctypes.data,
                                                 None if rgba is None else rgba.ctypes.data),

@@ -40,7 +40,7 @@ def test_exports_every_declared_symbol(native):
 
 
 def test_abi_version_and_error_text(native):
-    assert native.svo_abi_version() == 6
+    assert native.svo_abi_version() == 7
     assert isinstance(native.svo_last_error(), bytes)
 
 

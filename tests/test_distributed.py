@@ -264,3 +264,90 @@ def test_svo_broadcast_replicas_identical(tmp_path):
     for name in ("v1", "v2"):
         blobs = [np.load(tmp_path / f"{name}_{r}.npy").tobytes() for r in range(world)]
         assert blobs[1] == blobs[0] and blobs[2] == blobs[0]
+
+
+def test_weighted_owner_one_rank_is_round_robin():
+    """with one rank the owner table would be empty (plugin: round-robin,
+    band_rows: a division by zero); it is None (round-robin) instead."""
+    from raytracingtest_amd import band_rows
+    from raytracingtest_amd.distributed import band_len, rank_band, weighted_owner
+    for share in (0.0, 0.03, 0.5, 1.0):
+        owner = weighted_owner(1, share)
+        assert owner is None
+        assert np.array_equal(band_rows(37, rank_band(0, 1, 8, owner)), np.arange(37))
+        assert band_len(1080, 0, 1, owner=owner) == 1080
+
+
+class _FakeDist:
+    """torch.distributed stand-in that records which collective each helper
+    issues, on which backend, and the tensors it hands over."""
+
+    def __init__(self, backend, rank, world):
+        self.backend, self.rank, self.world, self.calls = backend, rank, world, []
+
+    def get_backend(self, group=None):
+        return self.backend
+
+    def get_rank(self, group=None):
+        return self.rank
+
+    def get_world_size(self, group=None):
+        return self.world
+
+    def gather(self, t, gather_list=None, dst=0, group=None):
+        self.calls.append(("gather", t, gather_list))
+
+    def broadcast(self, t, src, group=None):
+        self.calls.append(("broadcast", t, None))
+
+
+class _DevTensor:
+    """A tensor that claims to live on a GPU (no GPU in the CPU suite): any host
+    staging (.cpu()) of it fails the test."""
+    is_cuda = True
+
+    def cpu(self):
+        raise AssertionError("a device tensor was staged through the host on the RCCL branch")
+
+
+def test_rccl_branch_chosen_for_device_tensors():
+    """under backend "nccl" (= RCCL) the payload gather hands the
+    device tensors themselves to ONE dist.gather (no host staging) and the SVO
+    broadcast builds its tensors on the rank's device; under gloo the same
+    helpers stage through host tensors."""
+    import torch
+    from raytracingtest_amd import distributed as D
+    send, parts = _DevTensor(), [_DevTensor(), _DevTensor()]
+    fd = _FakeDist("nccl", 0, 2)
+    D.gather_fixed_to_root(send, parts, root=0, dist=fd)
+    assert [c[0] for c in fd.calls] == ["gather"]
+    assert fd.calls[0][1] is send and fd.calls[0][2] is parts
+    fd = _FakeDist("nccl", 1, 2)
+    D.gather_fixed_to_root(send, None, root=0, dist=fd)
+    assert fd.calls[0][1] is send and fd.calls[0][2] is None
+    fd = _FakeDist("nccl", 0, 2)
+    D.gather_parts(send, parts, dst=0, dist=fd)
+    assert fd.calls[0][1] is send
+    # gloo + a device tensor: host staging (the one-GPU rehearsal path) is taken
+    fd = _FakeDist("gloo", 1, 2)
+    with pytest.raises(AssertionError, match="staged through the host"):
+        D.gather_fixed_to_root(_DevTensor(), None, root=0, dist=fd)
+    # broadcast_svo: on nccl its tensors live on the device it is given (here a stand-in
+    # device, "meta": the header's .tolist() would need data, so stop at the first call)
+    fd = _FakeDist("nccl", 1, 2)
+
+    class _Stop(Exception):
+        pass
+
+    def bcast(t, src, group=None):
+        fd.calls.append(("broadcast", t, None))
+        raise _Stop()
+    fd.broadcast = bcast
+    with pytest.raises(_Stop):
+        D.broadcast_svo(None, 0, dist=fd, device=torch.device("meta"))
+    assert fd.calls[0][1].device.type == "meta"
+    fd = _FakeDist("gloo", 1, 2)
+    fd.broadcast = bcast
+    with pytest.raises(_Stop):
+        D.broadcast_svo(None, 0, dist=fd, device=torch.device("meta"))
+    assert fd.calls[-1][1].device.type == "cpu"

@@ -838,3 +838,37 @@ def test_render_progressive_matches_oracle(torch, oracle_mod, text_svo, devices)
             rm.RenderProgressive(W, H, want_rgba8=False, want_rgba=False)
     finally:
         rm.close()
+
+
+def test_render_progressive_resize_restarts(torch, oracle_mod, text_svo):
+    """a new render-target size reallocates the accumulation frame; the
+    first sample after it must replace the frame (sample 0), not be blended into
+    zeros with weight 1/(n+1) -- on the Python mirror (currentSample restarts) and in
+    the plugin itself (a caller that keeps counting still gets the sample)."""
+    cam = overview_camera()
+    rm = RaytracingMaster(capacity_nodes=1 << 16)
+    osvo = oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments)
+
+    def oracle_sample(w, h):
+        c2w, inv_proj = cam.uniforms(w, h)
+        _, smp, _ = oracle_mod.render(osvo, oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light()), w, h)
+        return np.ascontiguousarray(smp, np.float32)
+
+    try:
+        rm.SetSVOBuffer(text_svo)
+        rm.UpdateShaderParameters(cam, 96, 70)
+        for _ in range(3):
+            rm.RenderProgressive(96, 70, want_rgba8=False, want_rgba=True)
+        assert rm.currentSample == 3
+        rm.UpdateShaderParameters(cam, 120, 64)
+        _, rgba = rm.RenderProgressive(120, 64, want_rgba8=False, want_rgba=True)
+        assert rm.currentSample == 1
+        assert rgba.reshape(-1, 4).tobytes() == oracle_sample(120, 64).tobytes()
+        # the C-ABI alone, with a caller that does not restart its count
+        rm.UpdateShaderParameters(cam, 96, 70)
+        out = np.zeros((96 * 70, 4), np.float32)
+        _lib.check(_lib.lib().svo_render_progressive(rm._ctx, 96, 70, 0, 41, None, out.ctypes.data),
+                   "svo_render_progressive")
+        assert out.tobytes() == oracle_sample(96, 70).tobytes()
+    finally:
+        rm.close()
