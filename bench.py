@@ -346,6 +346,17 @@ def main():
                                           (" + payload" if world > 1 else "") +
                                           " (8 = the V2 node width; 4-byte reference descriptors would give 4*F)" +
                                           (" (primary pass only; kernel_ms covers both passes)" if args.shadows else ""),
+                         # the same launch under the other accountings: node and
+                         # attachment reads only, and the reference's 4-byte descriptor width
+                         "read_frac": round((8 * F + 8 * n_hit) / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                         "frac_ref_node_width": round((bytes_per_launch - 4 * F) / (kern_ms * 1e-3) / 1e9
+                                                      / HBM_PEAK_GBS, 5),
+                         "read_frac_ref_node_width": round((4 * F + 8 * n_hit) / (kern_ms * 1e-3) / 1e9
+                                                           / HBM_PEAK_GBS, 5),
+                         "accountings": "frac: 8-B V2 node fetches + attachment + hit record + RGBA32F (+ payload) "
+                                        "writes; read_frac: node + attachment reads only (8*F + 8*hits); "
+                                        "*_ref_node_width: the same with the reference's 4-byte descriptors (4*F); "
+                                        "hbm_frac: what the PMC counters saw cross the fabric",
                          "kernel_source_sha1": digest,
                          "traffic_source": None if pmc is None else pmc.get("source")},
             "cpu_baseline": cpu,

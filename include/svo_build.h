@@ -24,7 +24,7 @@ typedef enum svob_sampler {
     SVOB_FLAT_GROUND = 0,
     SVOB_SPHERE = 1,
     SVOB_SIMPLEX = 2,
-    SVOB_ROTATED_CUBOID = 3,   /* not supported yet: returns SVOB_ERR_ARG */
+    SVOB_ROTATED_CUBOID = 3,   /* Cuboid(Rotate(Euler(45,45,45)) p, 0.6); the rotation restated in float */
     SVOB_CUSTOM1 = 4
 } svob_sampler;
 

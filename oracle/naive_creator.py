@@ -205,8 +205,54 @@ def simplex():
     return _SIMPLEX
 
 
+def _qmul(lhs, rhs):   # UnityEngine.Quaternion operator* (x, y, z, w), float steps left to right
+    lx, ly, lz, lw = lhs
+    rx, ry, rz, rw = rhs
+    return (F(F(F(F(lw * rx) + F(lx * rw)) + F(ly * rz)) - F(lz * ry)),
+            F(F(F(F(lw * ry) + F(ly * rw)) + F(lz * rx)) - F(lx * rz)),
+            F(F(F(F(lw * rz) + F(lz * rw)) + F(lx * ry)) - F(ly * rx)),
+            F(F(F(F(lw * rw) - F(lx * rx)) - F(ly * ry)) - F(lz * rz)))
+
+
+def unity_rotation_matrix(ex, ey, ez):
+    """Matrix4x4.Rotate(Quaternion.Euler(ex, ey, ez)) in single precision, rows of the
+    3x3 rotation (SampleFunctions.cs:56).  Euler: each half angle (deg * Mathf.Deg2Rad) / 2
+    with its sine / cosine correctly rounded to float, q = (qY * qX) * qZ (Unity's Z, X, Y
+    order); Rotate: Matrix4x4.Rotate's products and sums.  Unity's native Euler
+    conversion is not public, so bit parity with Unity itself is unpinned."""
+    deg2rad = F(math.pi * 2 / 360)
+    half = [F(F(F(v) * deg2rad) / F(2)) for v in (ex, ey, ez)]
+    c = [F(math.cos(float(h))) for h in half]
+    s_ = [F(math.sin(float(h))) for h in half]
+    z0 = F(0)
+    qx, qy, qz = (s_[0], z0, z0, c[0]), (z0, s_[1], z0, c[1]), (z0, z0, s_[2], c[2])
+    x_, y_, z_, w_ = _qmul(_qmul(qy, qx), qz)
+    x, y, z = F(x_ * F(2)), F(y_ * F(2)), F(z_ * F(2))
+    xx, yy, zz = F(x_ * x), F(y_ * y), F(z_ * z)
+    xy, xz, yz = F(x_ * y), F(x_ * z), F(y_ * z)
+    wx, wy, wz = F(w_ * x), F(w_ * y), F(w_ * z)
+    one = F(1)
+    return [[F(one - F(yy + zz)), F(xy - wz), F(xz + wy)],
+            [F(xy + wz), F(one - F(xx + zz)), F(yz - wx)],
+            [F(xz - wy), F(yz + wx), F(one - F(xx + yy))]]
+
+
+def rotated_cuboid(x, y, z, radius=0.6):
+    """SampleFunctions.functions[3] (SampleFunctions.cs:35-38,54-68)."""
+    m = unity_rotation_matrix(45, 45, 45)
+    p = [F(F(F(v) - F(1.5)) * F(2)) for v in (x, y, z)]
+    r = [F(F(F(row[0] * p[0]) + F(row[1] * p[1])) + F(row[2] * p[2])) for row in m]   # MultiplyVector
+    d = [F(F(abs(v)) - F(radius)) for v in r]
+    myz = d[1] if d[1] > d[2] else d[2]                 # Mathf.Max
+    mx = d[0] if d[0] > myz else myz
+    mag = F(math.sqrt(float(F(F(F(d[0] * d[0]) + F(d[1] * d[1])) + F(d[2] * d[2])))))   # Vector3.Magnitude
+    return mx if mx < mag else mag                      # Mathf.Min
+
+
 def sampler(kind):
     """SampleFunctions.functions[kind] (SampleFunctions.cs:20-47)."""
+    if kind == 3:   # RotatedCuboid
+        return rotated_cuboid
     if kind == 4:   # Custom1
         def f(x, y, z):
             result = F(y) - F(1.5)

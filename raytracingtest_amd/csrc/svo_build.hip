@@ -254,6 +254,37 @@ __host__ __device__ inline double simplex_eval(const Simplex3 &s, double x, doub
     return value * NORM_3D;
 }
 
+// RotatedCuboid's rotation, Matrix4x4.Rotate(Quaternion.Euler(45, 45, 45)) (SampleFunctions.cs:54-58),
+// restated in single precision (oracle/naive_creator.py unity_rotation_matrix derives the same
+// nine words and tests/test_builder.py pins them): the half angle (45 * Mathf.Deg2Rad) / 2, its
+// sine and cosine correctly rounded to float, q = (qY * qX) * qZ (Unity's Z, X, Y order,
+// Quaternion operator*), then Matrix4x4.Rotate's products and sums.  Unity's own native
+// arithmetic for Euler -> quaternion is not public: parity with it is unpinned.
+#define ROT45_M00 0x1.b504f4p-1f
+#define ROT45_M01 -0x1.2bec30p-3f
+#define ROT45_M02 0x1.000000p-1f
+#define ROT45_M10 0x1.000000p-1f
+#define ROT45_M11 0x1.fffffcp-2f
+#define ROT45_M12 -0x1.6a09eap-1f
+#define ROT45_M20 -0x1.2bec30p-3f
+#define ROT45_M21 0x1.b504f6p-1f
+#define ROT45_M22 0x1.fffffcp-2f
+
+// SampleFunctions.cs:54-68: Cuboid(R p, radius); Mathf.Max / Mathf.Min as a > b ? a : b,
+// Vector3.Magnitude as a float sum of squares through a double square root
+__host__ __device__ inline float rotated_cuboid(float x, float y, float z) {
+    const float px = (x - 1.5f) * 2.0f, py = (y - 1.5f) * 2.0f, pz = (z - 1.5f) * 2.0f;
+    const float rx = ROT45_M00 * px + ROT45_M01 * py + ROT45_M02 * pz;   // MultiplyVector
+    const float ry = ROT45_M10 * px + ROT45_M11 * py + ROT45_M12 * pz;
+    const float rz = ROT45_M20 * px + ROT45_M21 * py + ROT45_M22 * pz;
+    const float radius = 0.6f;
+    const float dx = fabsf(rx) - radius, dy = fabsf(ry) - radius, dz = fabsf(rz) - radius;
+    const float myz = dy > dz ? dy : dz;
+    const float m = dx > myz ? dx : myz;
+    const float mag = (float)sqrt((double)(dx * dx + dy * dy + dz * dz));
+    return m < mag ? m : mag;
+}
+
 // SampleFunctions.cs:20-47 (float in, float out; C# single-precision steps)
 __host__ __device__ inline float sample(const Simplex3 &s, int type, float x, float y, float z) {
     switch (type) {
@@ -267,6 +298,8 @@ __host__ __device__ inline float sample(const Simplex3 &s, int type, float x, fl
         const float r = 1132.0f;
         return (float)simplex_eval(s, (double)(x * r), (double)(y * r), (double)(z * r));
     }
+    case 3:   // RotatedCuboid, radius 0.6 (SampleFunctions.cs:35-38)
+        return rotated_cuboid(x, y, z);
     default: { // 4: Custom1 simplex terrain
         float result = y - 1.5f;
         const float r = 3.0f;
@@ -674,7 +707,6 @@ int empty_tree(int depth, svob_result *out) {
 }
 
 int check_sampler(int type, int max_level) {
-    if (type == 3) return fail(SVOB_ERR_ARG, "RotatedCuboid sampler is not supported yet");
     if (type < 0 || type > 4) return fail(SVOB_ERR_ARG, "unknown sampler");
     if (max_level < 2 || max_level > 22) return fail(SVOB_ERR_ARG, "max_level must be in [2, 22]");
     return SVOB_OK;
@@ -718,7 +750,7 @@ int svob_opensimplex_table(int8_t *out) {
 
 int svob_eval_sampler(int sampler, size_t n, const float *xyz, float *out) {
     if (!xyz || !out) return fail(SVOB_ERR_ARG, "null argument");
-    if (sampler == 3 || sampler < 0 || sampler > 4) return fail(SVOB_ERR_ARG, "unsupported sampler");
+    if (sampler < 0 || sampler > 4) return fail(SVOB_ERR_ARG, "unsupported sampler");
     static Simplex3 s;
     static bool ready = false;
     if (!ready) {

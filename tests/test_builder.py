@@ -112,7 +112,7 @@ def _host_surface(sampler, max_level):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sampler,max_level", [(4, 5), (4, 7), (2, 6)])
+@pytest.mark.parametrize("sampler,max_level", [(4, 5), (4, 7), (2, 6), (3, 7)])
 def test_gpu_classification_matches_host(sampler, max_level):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -158,7 +158,7 @@ def test_python_sampler_matches_native_host_sampler():
     g = (1 + (np.arange(16) + 0.5) / 16).astype(np.float32)
     pts = np.concatenate([rng.uniform(1, 2, (600, 3)).astype(np.float32),
                           np.array([[a, b, c] for a in g[:5] for b in g[:5] for c in g[:5]], np.float32)])
-    for kind in (nb.SIMPLEX, nb.CUSTOM1, nb.FLAT_GROUND):
+    for kind in (nb.SIMPLEX, nb.CUSTOM1, nb.FLAT_GROUND, nb.ROTATED_CUBOID):
         f = nc.sampler(kind)
         py = np.array([f(*q) for q in pts], np.float32)
         assert np.array_equal(py.view(np.uint32), nb.eval_sampler(kind, pts).view(np.uint32)), kind
@@ -193,7 +193,7 @@ def test_python_naive_creator_layout_matches_native():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,max_level", [(4, 3), (4, 5), (4, 6), (2, 5), (0, 4)])
+@pytest.mark.parametrize("kind,max_level", [(4, 3), (4, 5), (4, 6), (2, 5), (0, 4), (3, 4), (3, 6)])
 def test_gpu_builder_matches_python_naive_creator(kind, max_level):
     """End to end: GPU classification + native layout == the pure-Python
     NaiveCreator restatement (descriptors and attachments bit for bit)."""
@@ -206,3 +206,23 @@ def test_gpu_builder_matches_python_naive_creator(kind, max_level):
     assert got.format == 1
     assert np.array_equal(got.childDescriptors, desc)
     assert np.array_equal(got.attachments, att)
+
+
+def test_rotated_cuboid_sampler():
+    """SampleFunctions.functions[3] (SampleFunctions.cs:35-38,54-68): the restated
+    Matrix4x4.Rotate(Quaternion.Euler(45, 45, 45)) is a rotation (rows orthonormal
+    to float accuracy, determinant 1) and the native sampler is the rotated
+    0.6-radius cube: inside at the centre, outside at the corners of [1, 2]^3, and
+    at the cube's own rotated corner direction the surface lies at 0.6 * sqrt(3)."""
+    from oracle import naive_creator as nc
+    m = np.array(nc.unity_rotation_matrix(45, 45, 45), np.float64)
+    np.testing.assert_allclose(m @ m.T, np.eye(3), atol=1e-6)
+    assert abs(np.linalg.det(m) - 1) < 1e-6
+    pts = np.array([[1.5, 1.5, 1.5], [1, 1, 1], [2, 2, 2], [1, 2, 1]], np.float32)
+    v = nb.eval_sampler(nb.ROTATED_CUBOID, pts)
+    assert v[0] == np.float32(-0.6) and np.all(v[1:] > 0)
+    # a point on the ray through the cube's rotated corner: world = R^T (corner) / 2 + 1.5
+    corner = m.T @ np.array([1.0, 1.0, 1.0]) / np.sqrt(3)
+    for t, sign in ((0.6 * np.sqrt(3) * 0.99, -1), (0.6 * np.sqrt(3) * 1.01, 1)):
+        q = (corner * t / 2 + 1.5).astype(np.float32)[None]
+        assert np.sign(nb.eval_sampler(nb.ROTATED_CUBOID, q)[0]) == sign

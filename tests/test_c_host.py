@@ -1,5 +1,6 @@
-"""The C-ABI from a plain C host (examples/render_min.c): no Python, no torch
-between the caller and libsvo_rt.so -- the boundary a native engine binds."""
+"""The C-ABI from a plain C host (examples/render_min.c, examples/build_and_render.c):
+no Python, no torch between the caller and libsvo_rt.so / libsvo_build.so -- the
+boundary a native engine binds."""
 import os
 import shutil
 import subprocess
@@ -11,17 +12,23 @@ LIB_DIR = os.path.join(ROOT, "raytracingtest_amd")
 SRC = os.path.join(ROOT, "examples", "render_min.c")
 
 
-def _build(tmp_path):
-    if not os.path.exists(os.path.join(LIB_DIR, "libsvo_rt.so")):
-        pytest.skip("libsvo_rt.so not built (run __graft_entry__.build())")
+def _build(tmp_path, src=SRC, name="render_min", libs=("-lsvo_rt",)):
+    for lib in libs:
+        if not os.path.exists(os.path.join(LIB_DIR, "lib" + lib[2:] + ".so")):
+            pytest.skip(f"lib{lib[2:]}.so not built (run __graft_entry__.build())")
     cc = shutil.which("gcc") or shutil.which("cc")
     if cc is None:
         pytest.skip("no C compiler")
-    exe = str(tmp_path / "render_min")
-    subprocess.run([cc, "-O2", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), SRC,
-                    "-L", LIB_DIR, "-lsvo_rt", "-L/opt/rocm/lib", "-lamdhip64", "-lm",
+    exe = str(tmp_path / name)
+    subprocess.run([cc, "-O2", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), src,
+                    "-L", LIB_DIR, *libs, "-L/opt/rocm/lib", "-lamdhip64", "-lm",
                     "-Wl,-rpath," + LIB_DIR, "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
     return exe
+
+
+def _build_key_r(tmp_path):
+    return _build(tmp_path, os.path.join(ROOT, "examples", "build_and_render.c"), "build_and_render",
+                  ("-lsvo_rt", "-lsvo_build"))
 
 
 def test_c_host_compiles_and_links(tmp_path):
@@ -35,3 +42,43 @@ def test_c_host_renders(tmp_path):
     assert out.returncode == 0, out.stdout + out.stderr
     assert "render_min: ok" in out.stdout
     assert (tmp_path / "frame.ppm").stat().st_size == len("P6\n64 64\n255\n") + 64 * 64 * 3
+
+
+def test_c_host_key_r_compiles_and_links(tmp_path):
+    assert os.path.exists(_build_key_r(tmp_path))
+
+
+@pytest.mark.gpu
+def test_c_host_builds_uploads_v2_and_renders(tmp_path, oracle_mod):
+    """The reference's key-R path from C (RaytracingMaster.cs:50-52,90-109): the native
+    NaiveCreator builds the depth-10 Custom1 pool (C3's, child pointers beyond 16 bits),
+    svo_set_buffer_v2 uploads it, svo_get_info picks the stack mode, svo_render traces a
+    reduced 480x270 frame from the flyover camera; every hit record equals the oracle's
+    on the same pool (built again here, deterministically) and camera."""
+    import numpy as np
+    from raytracingtest_amd import HIT_DTYPE
+    from raytracingtest_amd.camera import CAMERAS, column_major, main_light
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    exe = _build_key_r(tmp_path)
+    W, H = 480, 270
+    cam = CAMERAS["flyover"]()
+    c2w, inv_proj = cam.uniforms(W, H)
+    light = np.asarray(main_light(), np.float32)
+    blob = np.concatenate([column_major(np.asarray(c2w, np.float32)).reshape(-1),
+                           column_major(np.asarray(inv_proj, np.float32)).reshape(-1), light]).astype(np.float32)
+    assert blob.size == 36
+    (tmp_path / "cam.bin").write_bytes(blob.tobytes())
+    out = subprocess.run([exe, "4", "11", str(tmp_path / "cam.bin"), str(W), str(H), str(tmp_path / "hits.bin"),
+                          str(tmp_path / "rgba.bin")], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "v1 pointers overflow" in out.stdout and "stack mode hlsl" in out.stdout, out.stdout
+    got = np.frombuffer((tmp_path / "hits.bin").read_bytes(), HIT_DTYPE)
+    rgba = np.frombuffer((tmp_path / "rgba.bin").read_bytes(), np.float32).reshape(-1, 4)
+    svo = build_sampler_svo(4, 11)
+    assert svo.format == 2
+    ocam = oracle_mod.make_camera(c2w, inv_proj, (0.5, 0.5), main_light())
+    osvo = oracle_mod.OracleSVO(nodes=svo.to_v2(), attachments=svo.attachments)
+    ref, ref_rgba, _ = oracle_mod.render(osvo, ocam, W, H, 0, want_fetches=False)
+    assert np.count_nonzero(ref["flags"] & 1) > 10000
+    assert got.tobytes() == ref.tobytes()
+    np.testing.assert_allclose(rgba, ref_rgba, rtol=1e-5, atol=1e-7)

@@ -7,7 +7,9 @@ using System.Runtime.InteropServices;
 using UnityEngine;
 
 public static class SvoNative {
-    const string Lib = "svo_rt";   // libsvo_rt.so in Assets/Plugins/x86_64
+    const string Lib = "svo_rt";        // libsvo_rt.so in Assets/Plugins/x86_64
+    const string Builder = "svo_build"; // libsvo_build.so: the native NaiveCreator (include/svo_build.h)
+    public const int StackHlsl = 0, StackExact = 1;
 
     [StructLayout(LayoutKind.Sequential)]
     public struct SvoHit { public uint parent; public byte hitIdx; public byte hitScale; public ushort flags;
@@ -18,6 +20,12 @@ public static class SvoNative {
                                                                int bandRows, out IntPtr ctx);
     [DllImport(Lib)] public static extern int svo_set_buffer(IntPtr ctx, int[] desc, UIntPtr nDesc,
                                                              uint[] att, UIntPtr nAtt, UIntPtr dstOffset);
+    // wide node format (svo_rt.h): first_child_abs << 32 | valid << 8 | nonleaf -- any pool the builder makes,
+    // straight from the builder's native arrays (no managed copy)
+    [DllImport(Lib)] public static extern int svo_set_buffer_v2(IntPtr ctx, IntPtr nodes, UIntPtr nNodes,
+                                                                IntPtr att, UIntPtr nAtt, UIntPtr dstOffset);
+    [DllImport(Lib)] public static extern int svo_get_info(IntPtr ctx, out UIntPtr nNodes, out int maxDepth,
+                                                           out int device);
     [DllImport(Lib)] public static extern int svo_set_camera(IntPtr ctx, float[] c2w, float[] invProj,
                                                              float pxOffX, float pxOffY, float[] light);
     [DllImport(Lib)] public static extern int svo_render(IntPtr ctx, int width, int height, int stackMode,
@@ -28,8 +36,28 @@ public static class SvoNative {
     [DllImport(Lib)] public static extern int svo_destroy(IntPtr ctx);
     [DllImport(Lib)] public static extern IntPtr svo_last_error();
 
+    [StructLayout(LayoutKind.Sequential)]
+    public struct SvobResult {   // == svob_result
+        public UIntPtr nNodes; public int depth; public int v1Ok;
+        public IntPtr descriptors, nodes, attachments; public UIntPtr nLeaves;
+    }
+    [DllImport(Builder)] public static extern int svob_build_sampler(int device, int sampler, int maxLevel,
+                                                                     out SvobResult result);
+    [DllImport(Builder)] public static extern void svob_free(ref SvobResult result);
+    [DllImport(Builder)] public static extern IntPtr svob_last_error();
+
     public static void Check(int rc, string what) {
         if (rc != 0) throw new InvalidOperationException(what + ": " + Marshal.PtrToStringAnsi(svo_last_error()));
+    }
+    public static void CheckBuild(int rc, string what) {
+        if (rc != 0) throw new InvalidOperationException(what + ": " + Marshal.PtrToStringAnsi(svob_last_error()));
+    }
+
+    // The HLSL float2 stack (NVIDIASVO.compute:98) rounds parent indices above 2^24 nodes
+    // (SURVEY.md Appendix A): such pools (C4, C5) trace with the exact stack
+    public static int StackModeFor(IntPtr ctx) {
+        Check(svo_get_info(ctx, out UIntPtr n, out int depth, out int device), "svo_get_info");
+        return (ulong)n > (1UL << 24) ? StackExact : StackHlsl;
     }
 
     // Unity Matrix4x4 is column-major in memory (m00, m10, m20, m30, m01, ...), which is the C-ABI order.
@@ -42,7 +70,9 @@ public static class SvoNative {
 
 public class RaytracingMasterNative : MonoBehaviour {
     public Light DirectionalLight;
-    [Range(1, 8)] public int maxLevel = 5;
+    // the reference's [Range(1, 8)] (RaytracingMaster.cs:16-17) is widened: the native builder
+    // makes the BASELINE pools up to 8192^3 (maxLevel 14) in seconds
+    [Range(1, 14)] public int maxLevel = 5;
     public SampleFunctions.Type sampleType = SampleFunctions.Type.Custom1;
     [Range(1, 8)] public int gpus = 1;   // > 1: the frame is split in 8-row bands over GPUs 0..gpus-1
 
@@ -51,23 +81,28 @@ public class RaytracingMasterNative : MonoBehaviour {
     Texture2D _frame;
     uint[] _rgba8;
     uint _currentSample = 0;   // RaytracingMaster.cs:12
+    int _stackMode = SvoNative.StackHlsl;   // chosen from the uploaded pool (SvoNative.StackModeFor)
 
     void Awake() {
         _camera = GetComponent<Camera>();
         InitializeSVOBuffer();
     }
 
-    // RaytracingMaster.cs:44-53: a moved camera restarts the accumulation
+    // RaytracingMaster.cs:44-53: a moved camera restarts the accumulation; key R rebuilds the SVO
     void Update() {
         if (transform.hasChanged) {
             _currentSample = 0;
             transform.hasChanged = false;
         }
+        if (Input.GetKeyDown(KeyCode.R)) SetSVOBuffer();
     }
 
     // RaytracingMaster.cs:111-116
     public void InitializeSVOBuffer() {
-        var capacity = (UIntPtr)(1073741824 / 8);
+        CreateContext((UIntPtr)(1073741824 / 8));
+    }
+
+    void CreateContext(UIntPtr capacity) {
         if (gpus <= 1) {
             SvoNative.Check(SvoNative.svo_create(0, capacity, out _ctx), "svo_create");
         } else {   // one SVO replica per GPU, bands gathered to GPU 0 over xGMI; every other call is unchanged
@@ -77,12 +112,34 @@ public class RaytracingMasterNative : MonoBehaviour {
         }
     }
 
+    // RaytracingMaster.cs:90-109 (key R): NaiveCreator.Create(SampleFunctions.functions[sampleType], maxLevel)
+    // by the native builder on GPU 0, uploaded in the wide node format -- every BASELINE pool from
+    // 256^3 up has child pointers beyond the reference's 16 bits.  The pool replaces the old one (the
+    // capacity is the 1 GiB of InitializeSVOBuffer; a bigger pool gets a context of its size).
+    void SetSVOBuffer() {
+        SvoNative.CheckBuild(SvoNative.svob_build_sampler(0, (int)sampleType, maxLevel, out var r), "svob_build_sampler");
+        try {
+            ulong n = (ulong)r.nNodes;
+            if (n > (ulong)(1073741824 / 8)) {   // beyond InitializeSVOBuffer's capacity
+                SvoNative.svo_destroy(_ctx);
+                CreateContext((UIntPtr)n);
+            }
+            SvoNative.Check(SvoNative.svo_set_buffer_v2(_ctx, r.nodes, r.nNodes, r.attachments, (UIntPtr)(2 * n),
+                                                        UIntPtr.Zero), "svo_set_buffer_v2");
+        } finally {
+            SvoNative.svob_free(ref r);
+        }
+        _stackMode = SvoNative.StackModeFor(_ctx);
+        _currentSample = 0;
+    }
+
     // RaytracingMaster.cs:118-135 (attachments land at 2*offset: the reference's offset bug is fixed)
     public void SetSVOBuffer(RT.SVOData data, int offset = 0) {
         var desc = data.childDescriptors.ToArray();
         var att = data.attachments.ToArray();
         SvoNative.Check(SvoNative.svo_set_buffer(_ctx, desc, (UIntPtr)desc.Length, att, (UIntPtr)att.Length,
                                                  (UIntPtr)offset), "svo_set_buffer");
+        _stackMode = SvoNative.StackModeFor(_ctx);
     }
 
     // RaytracingMaster.cs:32-41 + 55-74: the sample is rendered, blended into the plugin's
@@ -98,8 +155,9 @@ public class RaytracingMasterNative : MonoBehaviour {
         if (_frame == null || _frame.width != w || _frame.height != h) {
             _frame = new Texture2D(w, h, TextureFormat.RGBA32, false, true);
             _rgba8 = new uint[w * h];
+            _currentSample = 0;   // a new render target: the plugin starts a fresh accumulation frame
         }
-        SvoNative.Check(SvoNative.svo_render_progressive(_ctx, w, h, 0, _currentSample, _rgba8, null),
+        SvoNative.Check(SvoNative.svo_render_progressive(_ctx, w, h, _stackMode, _currentSample, _rgba8, null),
                         "svo_render_progressive");
         _frame.SetPixelData(_rgba8, 0);
         _frame.Apply(false);
