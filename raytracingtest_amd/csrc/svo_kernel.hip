@@ -639,11 +639,11 @@ __global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int t
         if (lane == 0) p.out.hitmask[t] = hm;
     }
     if (p.tile_cost && (!SH || lane == 0)) p.tile_cost[t] = (uint16_t)min(trips, 65535);
-    if (p.wave_log && lane == 0) {   // 100 MHz constant clock, HW_ID, XCC_ID
+    if (p.wave_log && lane == 0) {   // 100 MHz constant clock, tile, XCC_ID
         uint32_t *w = p.wave_log + 8 * (size_t)blockIdx.x;
         w[0] = t0;
         w[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-        w[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        w[2] = (uint32_t)t;   // the tile (band-local, row-major)
         w[3] = ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFFu) | ((uint32_t)f.trips << 8);
         w[4] = (uint32_t)dg.loop_cycles;
         w[5] = (uint32_t)dg.fetch_cycles;
@@ -877,10 +877,20 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleParams a) {
 
 }  // namespace
 
+// Diagnostics only (env SVO_LDS_PAD=<bytes>, read once): extra LDS per render workgroup, to
+// lower the resident waves per CU in occupancy sweeps; never set by callers.
+static size_t lds_pad() {
+    static const size_t pad = [] {
+        const char *v = std::getenv("SVO_LDS_PAD");
+        return v ? (size_t)std::strtoul(v, nullptr, 10) : (size_t)0;
+    }();
+    return pad;
+}
+
 template <int MODE, bool COUNT>
 static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
     const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
-    const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2);   // + the spare slot
+    const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2) + lds_pad();   // + the spare slot
     const dim3 grid((unsigned)(bx * by)), block(TILE);
     if (COUNT)
         hipLaunchKernelGGL((render_tile_kernel<MODE, true>), grid, block, lds, stream, p, bx);

@@ -5,7 +5,7 @@ s_memrealtime at trace start / end (100 MHz), HW_ID, XCC_ID | trip count << 8)
 and prints the kernel span, the wave-duration distribution, the mean number
 of resident waves over the span and a coarse occupancy timeline.
 
-  python tools/wave_log.py [--camera flyover] [--max-level 11] [--order ...]
+  python tools/wave_log.py [--config C3] [--camera flyover] [--tile-row N | -2]
 """
 import argparse
 import os
@@ -19,28 +19,42 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--camera", default="flyover")
-    ap.add_argument("--max-level", type=int, default=11)
+    ap.add_argument("--config", default="C3", help="bench.py CONFIGS entry: frame size, pool, stack mode")
+    ap.add_argument("--camera", default=None, help="default: the config's camera")
+    ap.add_argument("--max-level", type=int, default=None)
     ap.add_argument("--out", default="gpurun_out/wave_log.bin")
-    ap.add_argument("--tile-row", type=int, default=-1, help="render only this 8-row band (a near-empty GPU)")
+    ap.add_argument("--tile-row", type=int, default=-1,
+                    help="render only this 8-row band (a near-empty GPU); -2: the band holding the frame's "
+                         "heaviest tile (found from a logged full-frame launch first)")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     os.environ["SVO_WAVE_LOG"] = os.path.abspath(args.out)
     import torch
+    from bench import CONFIGS
     from raytracingtest_amd import RaytracingMaster
     from raytracingtest_amd.camera import CAMERAS
     from raytracingtest_amd.native_builder import build_sampler_svo
 
-    W, H = 1920, 1080
-    svo = build_sampler_svo(4, args.max_level)
+    cfg = CONFIGS[args.config]
+    W, H = cfg["width"], cfg["height"]
+    mode = cfg["stack_mode"]
+    svo = build_sampler_svo(4, args.max_level or cfg["max_level"])
     rm = RaytracingMaster(capacity_nodes=len(svo))
     rm.SetSVOBuffer(svo)
-    rm.UpdateShaderParameters(CAMERAS[args.camera](), W, H)
+    rm.UpdateShaderParameters(CAMERAS[args.camera or cfg["camera"]](), W, H)
     hits = torch.empty(W * H * 24, dtype=torch.uint8, device="cuda")
     rgba = torch.empty(W * H * 4, dtype=torch.float32, device="cuda")
-    band = None if args.tile_row < 0 else (8, args.tile_row, H // 8)
+    if args.tile_row == -2:
+        for _ in range(3):
+            rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr(), stack_mode=mode)
+        rm.synchronize()
+        full = np.fromfile(args.out, np.uint32).reshape(-1, 8)
+        k = int(np.argmax(full[:, 3] >> 8))
+        args.tile_row = int(full[k, 2]) // ((W + 7) // 8)
+        print(f"heaviest tile {int(full[k, 2])}: {int(full[k, 3] >> 8)} trips, tile row {args.tile_row}")
+    band = None if args.tile_row < 0 else (8, args.tile_row, (H + 7) // 8)
     for _ in range(3):
-        rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr(), band=band)
+        rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr(), band=band, stack_mode=mode)
     rm.synchronize()
     # uninstrumented timing of the same launch (the log is only taken while SVO_WAVE_LOG is set)
     del os.environ["SVO_WAVE_LOG"]
@@ -48,7 +62,7 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
     for a, b in evs:
         a.record(s)
-        rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr(), band=band, stream=s.cuda_stream)
+        rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr(), band=band, stack_mode=mode, stream=s.cuda_stream)
         b.record(s)
     torch.cuda.synchronize()
     print(f"uninstrumented launch: {np.median([a.elapsed_time(b) for a, b in evs]) * 1e3:.1f} us (median of 10)")
@@ -101,7 +115,6 @@ def main():
         print(f"{name}: cycles/trip {loop_c[m].sum() / tr:.0f}, fetching trips {ft[m].sum() / tr:.2f},"
               f" popping trips {pt[m].sum() / tr:.2f}, push-only trips {push_only[m].sum() / tr:.2f},"
               f" advance-only trips {adv_only[m].sum() / tr:.2f}")
-    hw = log[:, 2]
     xcc = log[:, 3] & 0xFF
     print("waves per XCC:", np.bincount(xcc, minlength=8)[:8])
     for x in range(8):
