@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from bench import CONFIGS  # noqa: E402
-from raytracingtest_amd import RaytracingMaster  # noqa: E402
+from raytracingtest_amd import HIT_DTYPE, RaytracingMaster  # noqa: E402
 from raytracingtest_amd.camera import CAMERAS, main_light  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -128,14 +128,28 @@ def _strong_split_check(torch, oracle_mod, name, world):
     want_hits = ref_hits.view(np.uint8).reshape(-1, 24)
     mode = cfg["stack_mode"]
 
+    def where(bad_px):
+        """Which part owns the differing pixels, and which fields differ (failure text)."""
+        rows = bad_px // W
+        part = np.array([np.asarray(owner)[(y // 8) % len(owner)] for y in rows[:200000]])
+        return f"parts {np.bincount(part, minlength=world).tolist()}, first rows {np.unique(rows)[:8].tolist()}"
+
     def compare(frame8, fhits, what):
         got = frame8.cpu().numpy().view(np.uint32)
-        bad = np.count_nonzero(got != want8)
-        assert bad == 0, f"{what}: {bad} of {W * H} display words differ"
+        bad = np.flatnonzero(got != want8)
+        assert len(bad) == 0, f"{what}: {len(bad)} of {W * H} display words differ; {where(bad)}"
         if fhits is not None:
             gh = fhits.cpu().numpy().reshape(-1, 24)
-            badh = np.count_nonzero((gh != want_hits).any(1))
-            assert badh == 0, f"{what}: {badh} hit records differ"
+            badh = np.flatnonzero((gh != want_hits).any(1))
+            if len(badh):
+                g = gh[badh].view(HIT_DTYPE).reshape(-1)
+                w = want_hits[badh].view(HIT_DTYPE).reshape(-1)
+                fields = {f: int(np.count_nonzero(g[f].view(np.uint8).reshape(len(g), -1) !=
+                                                  w[f].view(np.uint8).reshape(len(w), -1)))
+                          for f in HIT_DTYPE.names}
+                raise AssertionError(f"{what}: {len(badh)} hit records differ; {where(badh)}; fields {fields}; "
+                                     f"hits among them {int(np.count_nonzero(w['flags'] & 1))}; first got "
+                                     f"{g[:2].tolist()} want {w[:2].tolist()}")
 
     with RaytracingMaster(device=0, capacity_nodes=len(svo)) as rm:
         rm.SetSVOBuffer(svo)
