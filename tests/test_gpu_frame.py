@@ -43,15 +43,19 @@ def _oracle(oracle_mod, svo, cam, w, h, mode=0, off=(0.5, 0.5), shadows=False):
 
 
 def _bufs(torch, n_px):
-    """Every output buffer, pre-filled with a pattern no render produces."""
+    """Every output buffer, pre-filled with a pattern no render produces.  The fills
+    run on torch's stream and the plugin renders on its context's own non-blocking
+    stream, which does not wait for torch's: synchronize before handing them over."""
     t = torch
-    return {"hits": t.full((n_px * 24,), 0xA5, dtype=t.uint8, device="cuda"),
-            "rgba": t.full((n_px * 4,), -7.0, dtype=t.float32, device="cuda"),
-            "rgba8": t.full((n_px,), 0x1234567, dtype=t.int32, device="cuda"),
-            "compact": t.full((n_px * 12,), 0x5A, dtype=t.uint8, device="cuda"),
-            "position": t.full((n_px * 4,), -9.0, dtype=t.float32, device="cuda"),
-            "voxel": t.full((n_px,), 77, dtype=t.int64, device="cuda"),
-            "rgb8": t.full((n_px * 3,), 0xA5, dtype=t.uint8, device="cuda")}
+    b = {"hits": t.full((n_px * 24,), 0xA5, dtype=t.uint8, device="cuda"),
+         "rgba": t.full((n_px * 4,), -7.0, dtype=t.float32, device="cuda"),
+         "rgba8": t.full((n_px,), 0x1234567, dtype=t.int32, device="cuda"),
+         "compact": t.full((n_px * 12,), 0x5A, dtype=t.uint8, device="cuda"),
+         "position": t.full((n_px * 4,), -9.0, dtype=t.float32, device="cuda"),
+         "voxel": t.full((n_px,), 77, dtype=t.int64, device="cuda"),
+         "rgb8": t.full((n_px * 3,), 0xA5, dtype=t.uint8, device="cuda")}
+    t.cuda.synchronize()
+    return b
 
 
 def _ptrs(b, keys=None):
@@ -233,6 +237,7 @@ def test_multi_device_payload_regrowth_across_streams(torch, oracle_mod):
         for i, (w, h) in enumerate(sizes):
             m.UpdateShaderParameters(cam, w, h)
             f = torch.full((w * h,), 0x1234567, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()   # the fill before the plugin's stream writes the frame
             m.render_frame(w, h, rgba8=f.data_ptr(), layout=_lib.LAYOUT_FRAME, stream=streams[i % 2].cuda_stream)
             frames.append(f)
         m.synchronize()
@@ -353,6 +358,7 @@ def test_assemble_from_rank_parts(torch, oracle_mod, world):
             comp.append(torch.zeros(max(n, 1) * 12, dtype=torch.uint8, device="cuda"))
             rgb8.append(torch.zeros(max(n, 1), dtype=torch.int32, device="cuda"))
             rgb3.append(torch.zeros(max(n, 1) * 3, dtype=torch.uint8, device="cuda"))
+            torch.cuda.synchronize()   # the zero fills (torch's stream) before the plugin's stream writes
             m.render_frame(w, h, compact=comp[-1].data_ptr(), rgba8=rgb8[-1].data_ptr(), rgb8=rgb3[-1].data_ptr(),
                            band=(8, r, world))
         b = _bufs(torch, w * h)
@@ -404,6 +410,7 @@ def test_weighted_deal_parts_match_oracle(torch, oracle_mod, world, share):
             comp.append(torch.zeros(max(n, 1) * 12, dtype=torch.uint8, device="cuda"))
             rgb8.append(torch.zeros(max(n, 1), dtype=torch.int32, device="cuda"))
             rgb3.append(torch.zeros(max(n, 1) * 3, dtype=torch.uint8, device="cuda"))
+            torch.cuda.synchronize()   # the zero fills (torch's stream) before the plugin's stream writes
             m.render_frame(w, h, compact=comp[-1].data_ptr(), rgba8=rgb8[-1].data_ptr(), rgb8=rgb3[-1].data_ptr(),
                            band=(8, r, world, owner))
         b2 = _bufs(torch, w * h)
@@ -434,6 +441,7 @@ def _sparse_part(torch, m, w, h, band):
     n_tiles = ((w + 7) // 8) * ((rows + 7) // 8)
     dense = torch.full((max(rows * w, 1) * 3,), 0xA5, dtype=torch.uint8, device="cuda")
     part = torch.full((_lib.sparse_part_bytes(n_tiles, rows * w),), 0x5A, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()   # the fills before the plugin's stream writes
     m.render_frame(w, h, rgb8=dense.data_ptr(), hitmask=part.data_ptr(), band=band)
     m.pack_hits(w, h, band, dense.data_ptr(), part.data_ptr())
     return part, part[8 * n_tiles:12 * n_tiles + 4].view(torch.int32), n_tiles
@@ -551,6 +559,7 @@ def test_pack_hits_random_masks(torch, w, rows):
         part = torch.full((_lib.sparse_part_bytes(n_tiles, rows * w),), 0xEE, dtype=torch.uint8, device="cuda")
         part[:n_tiles * 8] = torch.from_numpy(masks.view(np.uint8)).cuda()
         dense = torch.from_numpy(rgb.reshape(-1)).cuda()
+        torch.cuda.synchronize()   # torch's copies before the plugin's stream reads them
         m.pack_hits(w, rows, (8, 0, 1), dense.data_ptr(), part.data_ptr())
         m.synchronize()
         offs = part[8 * n_tiles:12 * n_tiles + 4].view(torch.int32)

@@ -144,8 +144,8 @@ def _strong_split_check(torch, oracle_mod, name, world):
             if len(badh):
                 g = gh[badh].view(HIT_DTYPE).reshape(-1)
                 w = want_hits[badh].view(HIT_DTYPE).reshape(-1)
-                fields = {f: int(np.count_nonzero(g[f].view(np.uint8).reshape(len(g), -1) !=
-                                                  w[f].view(np.uint8).reshape(len(w), -1)))
+                fields = {f: int(np.count_nonzero(np.ascontiguousarray(g[f]).view(np.uint8).reshape(len(g), -1) !=
+                                                  np.ascontiguousarray(w[f]).view(np.uint8).reshape(len(w), -1)))
                           for f in HIT_DTYPE.names}
                 raise AssertionError(f"{what}: {len(badh)} hit records differ; {where(badh)}; fields {fields}; "
                                      f"hits among them {int(np.count_nonzero(w['flags'] & 1))}; first got "
@@ -164,6 +164,7 @@ def _strong_split_check(torch, oracle_mod, name, world):
                 parts.append(p)
             frame8 = torch.full((W * H,), 0x1234567, dtype=torch.int32, device="cuda")
             fhits = torch.full((W * H * 24,), 0xAB, dtype=torch.uint8, device="cuda") if elem == 12 else None
+            torch.cuda.synchronize()   # the fills (torch's stream) before the plugin's own stream writes
             rm.render_frame(W, H, rgba8=frame8.data_ptr(), hits=None if fhits is None else fhits.data_ptr(),
                             layout=_lib.LAYOUT_FRAME, band=D.rank_band(0, world, owner=owner), stack_mode=mode)
             rm.assemble_frame(W, H, [None] + [p.data_ptr() for p in parts[1:]], fmt, rgba8=frame8.data_ptr(),
@@ -177,6 +178,7 @@ def _strong_split_check(torch, oracle_mod, name, world):
         md.set_band_deal(list(owner))
         frame8 = torch.full((W * H,), 0x1234567, dtype=torch.int32, device="cuda")
         fhits = torch.full((W * H * 24,), 0xAB, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
         md.render_frame(W, H, rgba8=frame8.data_ptr(), hits=fhits.data_ptr(), layout=_lib.LAYOUT_FRAME,
                         stack_mode=mode)
         md.synchronize()
@@ -256,6 +258,7 @@ def test_c3_weak_scaling_frame_split_over_eight_ranks(gpu, oracle_mod):
             sparse.append(p)
         for fmt, parts in ((_lib.PART_RGB8, dense), (_lib.PART_SPARSE_RGB8, sparse)):
             frame = torch.full((W * H,), 0x1234567, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()   # the fill (torch's stream) before the plugin's own stream writes
             rm.render_frame(W, H, rgba8=frame.data_ptr(), layout=_lib.LAYOUT_FRAME,
                             band=D.rank_band(0, world, owner=owner), stack_mode=cfg["stack_mode"])
             rm.assemble_frame(W, H, [None] + [p.data_ptr() for p in parts[1:]], fmt, rgba8=frame.data_ptr(),

@@ -97,6 +97,7 @@ def test_menger_depth8_parity_and_fetch_counts(rm, oracle_mod):
     ref_hits, ref_rgba, ref_fetch = _oracle_render(oracle_mod, svo, cam, w, h)
     _compare(hits, rgba, ref_hits, ref_rgba)
     fetch = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()   # the fill (torch's stream) before the plugin's own stream writes
     rm.count_fetches_device(w, h, fetch.data_ptr())
     rm.synchronize()
     assert np.array_equal(fetch.cpu().numpy().view(np.uint32), ref_fetch)
@@ -114,6 +115,7 @@ def test_band_split_reassembles_frame(rm, text_svo):
         band = (8, rank, 3)
         ys = band_rows(h, band)
         buf = torch.zeros(len(ys) * w * 24, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
         rm.render_device(w, h, hits_ptr=buf.data_ptr(), band=band)
         rm.synchronize()
         out[ys] = buf.cpu().numpy().view(full.dtype).reshape(len(ys), w)
