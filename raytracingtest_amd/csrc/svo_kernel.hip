@@ -1325,13 +1325,11 @@ static hipError_t launch_split_variant(const LaunchParams &p, int k, hipStream_t
     LaunchParams m = p;
     m.order_base = k;
     const dim3 hgrid((unsigned)(k / 4)), mgrid((unsigned)(p.order_tiles - k));
-    // more than half a CU's 160 KB of LDS: one heavy workgroup per CU, one heavy wave per SIMD
-    const size_t hlds = std::max(4 * lds, (size_t)(80 * 1024 + 512));
     if (p.fetch_all && !p.guard) {
-        hipLaunchKernelGGL((render_tile_kernel<MODE, false, true, false, 4>), hgrid, dim3(4 * TILE), hlds, hs, h, bx);
+        hipLaunchKernelGGL((render_tile_kernel<MODE, false, true, false, 4>), hgrid, dim3(4 * TILE), 4 * lds, hs, h, bx);
         hipLaunchKernelGGL((render_tile_kernel<MODE, false, true>), mgrid, dim3(TILE), lds, ms, m, bx);
     } else {
-        hipLaunchKernelGGL((render_tile_kernel<MODE, false, false, false, 4>), hgrid, dim3(4 * TILE), hlds, hs, h, bx);
+        hipLaunchKernelGGL((render_tile_kernel<MODE, false, false, false, 4>), hgrid, dim3(4 * TILE), 4 * lds, hs, h, bx);
         hipLaunchKernelGGL((render_tile_kernel<MODE, false>), mgrid, dim3(TILE), lds, ms, m, bx);
     }
     return hipGetLastError();

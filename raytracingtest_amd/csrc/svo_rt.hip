@@ -581,8 +581,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             const int heavy_cus = std::max(1, k_heavy / 4);
             std::vector<uint32_t> mh((n_cu + 31) / 32, 0u), mm((n_cu + 31) / 32, 0u);
             for (int c = 0; c < n_cu; ++c) mm[c / 32] |= 1u << (c % 32);
-            for (int i = 0; i < heavy_cus; ++i) {   // logical CU c sits on XCD c % 8: spread over the XCDs
-                const int c = i;
+            for (int i = 0; i < heavy_cus; ++i) {
+                const int c = (int)((long long)i * n_cu / heavy_cus);
                 mh[c / 32] |= 1u << (c % 32);
                 mm[c / 32] &= ~(1u << (c % 32));
             }
