@@ -560,19 +560,14 @@ __device__ __forceinline__ int strip_tile(int x, int e, int tiles_x, int tiles_y
 // traces one shadow ray per hit lane, and the tile's recorded cost is the sum of
 // both, so one cost-ordered launch balances the whole frame.
 // COUNT: the instrumented launch (per-ray descriptor fetch counts, no outputs).
-// WAVES: waves per workgroup, each its own tile (1: the normal launch; 4: the heavy half of a
-// split launch, one wave per SIMD of a CU of its own -- launch_render_split).
-template <int MODE, bool COUNT, bool FA = false, bool SH = false, int WAVES = 1>
-__global__ __launch_bounds__(TILE * WAVES) void render_tile_kernel(LaunchParams p, int tiles_x) {
-    extern __shared__ uint2 stk_base[];   // per wave [p.slots + 1][64]
-    const int lane = (int)threadIdx.x & (TILE - 1);
-    const int wv = WAVES == 1 ? 0 : (int)threadIdx.x / TILE;
-    // position in the dispatch order (p.order_base: a split launch's second half)
-    const int pos = (int)blockIdx.x * WAVES + wv + p.order_base;
-    const int n_tiles = p.order_tiles;
-    const int t = p.tile_order ? (int)p.tile_order[pos]
-                : p.xcd_remap == 2 ? strip_tile(pos % 8, pos / 8, tiles_x, n_tiles / tiles_x)
-                                   : pos;
+template <int MODE, bool COUNT, bool FA = false, bool SH = false>
+__global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int tiles_x) {
+    extern __shared__ uint2 stk_base[];   // [p.slots + 1][64]
+    const int lane = threadIdx.x;
+    const int n_tiles = (int)gridDim.x;
+    const int t = p.tile_order ? (int)p.tile_order[blockIdx.x]
+                : p.xcd_remap == 2 ? strip_tile((int)blockIdx.x % 8, (int)blockIdx.x / 8, tiles_x, n_tiles / tiles_x)
+                                   : (int)blockIdx.x;
     const int bx = t % tiles_x, by = t / tiles_x;
     const int x = bx * 8 + (lane & 7);
     const int lr = by * 8 + (lane >> 3);
@@ -580,10 +575,10 @@ __global__ __launch_bounds__(TILE * WAVES) void render_tile_kernel(LaunchParams 
     if (p.tile_order && p.prio) {
         // issue priority by the previous launch's cost class: the heaviest tiles
         // bound the launch, so their waves win issue arbitration on a busy SIMD
-        const uint32_t n = (uint32_t)n_tiles;
+        const uint32_t n = gridDim.x;
         const bool strips = p.xcd_remap == 2;
-        const uint32_t b = strips ? (uint32_t)pos / 8 : (uint32_t)pos;
-        const uint32_t *bound = strips ? p.tile_order + n + 4 + 4 * (pos % 8) : p.tile_order + n;
+        const uint32_t b = strips ? blockIdx.x / 8 : blockIdx.x;
+        const uint32_t *bound = strips ? p.tile_order + n + 4 + 4 * (blockIdx.x % 8) : p.tile_order + n;
         if (b < bound[0]) __builtin_amdgcn_s_setprio(3);
         else if (b < bound[1]) __builtin_amdgcn_s_setprio(2);
         else if (b < bound[2]) __builtin_amdgcn_s_setprio(1);
@@ -595,7 +590,7 @@ __global__ __launch_bounds__(TILE * WAVES) void render_tile_kernel(LaunchParams 
         camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
         setup_ray(org, dir, r);
     }
-    uint2 *stk = stk_base + (size_t)wv * (size_t)(p.slots + 1) * TILE + lane;
+    uint2 *stk = stk_base + lane;
     uint32_t t0 = 0;
     if (!COUNT && p.wave_log) t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
     FRay f;
@@ -645,7 +640,7 @@ __global__ __launch_bounds__(TILE * WAVES) void render_tile_kernel(LaunchParams 
     }
     if (p.tile_cost && (!SH || lane == 0)) p.tile_cost[t] = (uint16_t)min(trips, 65535);
     if (p.wave_log && lane == 0) {   // 100 MHz constant clock, tile, XCC_ID
-        uint32_t *w = p.wave_log + 8 * (size_t)pos;
+        uint32_t *w = p.wave_log + 8 * (size_t)blockIdx.x;
         w[0] = t0;
         w[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         w[2] = (uint32_t)t;   // the tile (band-local, row-major)
@@ -1311,35 +1306,6 @@ hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
     const dim3 grid((unsigned)((a.width + 255) / 256), (unsigned)a.height);
     hipLaunchKernelGGL(assemble_kernel, grid, dim3(256), 0, stream, a);
     return hipGetLastError();
-}
-
-// Heavy-tile split (svo_traverse.h): order positions [0, k) as 4-wave workgroups on the heavy
-// stream, [k, n) as one-wave workgroups on the main stream.  Primary rays only (no shadow
-// pass, no fetch counting: launch() checks).
-template <int MODE>
-static hipError_t launch_split_variant(const LaunchParams &p, int k, hipStream_t hs, hipStream_t ms) {
-    const int bx = (p.width + 7) / 8;
-    const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2);
-    LaunchParams h = p;
-    h.order_base = 0;
-    LaunchParams m = p;
-    m.order_base = k;
-    const dim3 hgrid((unsigned)(k / 4)), mgrid((unsigned)(p.order_tiles - k));
-    if (p.fetch_all && !p.guard) {
-        hipLaunchKernelGGL((render_tile_kernel<MODE, false, true, false, 4>), hgrid, dim3(4 * TILE), 4 * lds, hs, h, bx);
-        hipLaunchKernelGGL((render_tile_kernel<MODE, false, true>), mgrid, dim3(TILE), lds, ms, m, bx);
-    } else {
-        hipLaunchKernelGGL((render_tile_kernel<MODE, false, false, false, 4>), hgrid, dim3(4 * TILE), 4 * lds, hs, h, bx);
-        hipLaunchKernelGGL((render_tile_kernel<MODE, false>), mgrid, dim3(TILE), lds, ms, m, bx);
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_render_split(const LaunchParams &p, int stack_mode, int k_heavy, hipStream_t heavy_stream,
-                               hipStream_t main_stream) {
-    if (k_heavy <= 0 || k_heavy % 4 != 0 || k_heavy >= p.order_tiles || !p.tile_order) return hipErrorInvalidValue;
-    return stack_mode == 0 ? launch_split_variant<0>(p, k_heavy, heavy_stream, main_stream)
-                           : launch_split_variant<1>(p, k_heavy, heavy_stream, main_stream);
 }
 
 template <int MODE>

@@ -149,9 +149,6 @@ struct svo_ctx {
     int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
     int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
     int shadow_compact = 0;          // env SVO_SHADOW_COMPACT=1: that launch over the compacted hit list
-    int heavy_split = 0;             // env SVO_HEAVY_SPLIT=K (diagnostics): heavy-tile split launches, see launch
-    hipStream_t split_stream[2] = {nullptr, nullptr};   // CU-masked: [0] the heavy tiles' CUs, [1] the rest
-    hipEvent_t split_event[3] = {nullptr, nullptr, nullptr};   // fork, heavy done, main done
     int order_every = 32;            // env SVO_ORDER_EVERY: rebuild the order every k-th launch (and after
                                      // every camera move or change of render mode)
     unsigned long long view_gen = 0; // bumped when svo_set_camera changes the matrices
@@ -516,8 +513,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.prio = ctx->prio;
     const bool ordered = ctx->tile_order && !p.out.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
-    p.order_tiles = n_tiles;
-    p.order_base = 0;
     Geo key;
     Sched *q = nullptr;
     if (ordered) {
@@ -571,39 +566,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         rc = take_events(ctx, STAGE_KERNEL, &ev0, &ev1);
         if (rc) return rc;
     }
-    hipError_t e = hipSuccess;
-    const int k_heavy = ctx->heavy_split;
-    if (k_heavy > 0 && p.tile_order && p.shadows == 0 && !p.out.fetches && n_tiles > 8 * k_heavy) {
-        // heavy-tile split: the order's first k tiles on CUs of their own (one wave per SIMD),
-        // the rest on the other CUs, forked from and joined back into the caller's stream
-        if (!ctx->split_stream[0]) {
-            const int n_cu = std::max(ctx->num_cus, 8);
-            const int heavy_cus = std::max(1, k_heavy / 4);
-            std::vector<uint32_t> mh((n_cu + 31) / 32, 0u), mm((n_cu + 31) / 32, 0u);
-            for (int c = 0; c < n_cu; ++c) mm[c / 32] |= 1u << (c % 32);
-            for (int i = 0; i < heavy_cus; ++i) {
-                const int c = (int)((long long)i * n_cu / heavy_cus);
-                mh[c / 32] |= 1u << (c % 32);
-                mm[c / 32] &= ~(1u << (c % 32));
-            }
-            HIP_TRY(hipExtStreamCreateWithCUMask(&ctx->split_stream[0], (uint32_t)mh.size(), mh.data()));
-            HIP_TRY(hipExtStreamCreateWithCUMask(&ctx->split_stream[1], (uint32_t)mm.size(), mm.data()));
-            for (auto &ev : ctx->split_event) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        }
-        if (ev0) HIP_TRY(hipEventRecord(ev0, s));
-        HIP_TRY(hipEventRecord(ctx->split_event[0], s));
-        HIP_TRY(hipStreamWaitEvent(ctx->split_stream[0], ctx->split_event[0], 0));
-        HIP_TRY(hipStreamWaitEvent(ctx->split_stream[1], ctx->split_event[0], 0));
-        e = svo::launch_render_split(p, stack_mode, k_heavy, ctx->split_stream[0], ctx->split_stream[1]);
-        if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("split render launch: ") + hipGetErrorString(e));
-        HIP_TRY(hipEventRecord(ctx->split_event[1], ctx->split_stream[0]));
-        HIP_TRY(hipEventRecord(ctx->split_event[2], ctx->split_stream[1]));
-        HIP_TRY(hipStreamWaitEvent(s, ctx->split_event[1], 0));
-        HIP_TRY(hipStreamWaitEvent(s, ctx->split_event[2], 0));
-        if (ev1) HIP_TRY(hipEventRecord(ev1, s));
-    } else {
-        e = svo::launch_render(p, stack_mode, s, ev0, ev1);
-    }
+    hipError_t e = svo::launch_render(p, stack_mode, s, ev0, ev1);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
     // refresh: a new geometry, every order_every-th launch, and right after the first launch
     // following a camera move or a change of render mode (that launch still uses the old
@@ -864,10 +827,6 @@ int destroy_single(svo_ctx *ctx) {
         for (auto &ev : v) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     for (auto &ev : ctx->timing_free) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     if (ctx->switch_event) hipEventDestroy(ctx->switch_event);
-    for (auto &st : ctx->split_stream)
-        if (st) hipStreamDestroy(st);
-    for (auto &ev : ctx->split_event)
-        if (ev) hipEventDestroy(ev);
     if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -912,7 +871,6 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_FUSED_SHADOWS")) ctx->fused_shadows = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SHADOW_COMPACT")) ctx->shadow_compact = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
-    if (const char *k = std::getenv("SVO_HEAVY_SPLIT")) ctx->heavy_split = std::max(0, std::atoi(k) / 8 * 8);
     if (e != hipSuccess) {
         destroy_single(ctx);
         return fail(SVO_ERR_HIP, std::string("svo_create: ") + hipGetErrorString(e));

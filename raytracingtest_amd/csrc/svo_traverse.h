@@ -76,9 +76,6 @@ struct LaunchParams {
     // and records its wave trip count in tile_cost.
     const uint32_t *tile_order;   // n_tiles entries + 36 class boundaries
     uint16_t *tile_cost;
-    // Split launches (heavy-tile split, svo_rt.hip): this launch traces the tiles at order
-    // positions [order_base, order_base + grid waves); order_tiles = the geometry's tile count
-    int order_base, order_tiles;
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
     int fetch_all;                // lean loop (!guard): every lane loads its node every trip
@@ -138,12 +135,6 @@ size_t shadow_list_bytes(int width, int local_rows);
 // Display RGBA8 words of an RGBA32F frame (svo_render_progressive).
 hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int num_cus, hipStream_t stream);
 
-// Heavy-tile split of one primary launch (env SVO_HEAVY_SPLIT=K, svo_rt.hip): the first K
-// tiles of the cost order (each XCD's heaviest) as 4-wave workgroups on `heavy_stream`
-// (CU-masked to K/4 CUs of their own: one heavy wave per SIMD), the other tiles as the usual
-// one-wave workgroups on `main_stream` (masked to the other CUs).  Needs p.tile_order.
-hipError_t launch_render_split(const LaunchParams &p, int stack_mode, int k_heavy, hipStream_t heavy_stream,
-                               hipStream_t main_stream);
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, hipEvent_t primary_start = nullptr,
                          hipEvent_t primary_end = nullptr);
 
