@@ -1012,11 +1012,7 @@ size_t order_cost_capacity(int n_tiles) {
 __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint16_t *__restrict__ cost,
                                                                      uint32_t *__restrict__ order, int n, int tiles_x) {
     __shared__ uint32_t red[ORDER_THREADS / 64];
-#ifdef SVO_ORDER_FINE
-    constexpr int NC = 8;
-#else
     constexpr int NC = 6;
-#endif
     __shared__ uint32_t cnt[NC], base[NC];
     const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int len = n / 8, tiles_y = n / tiles_x;
@@ -1046,12 +1042,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     // XCD's first dispatches (they bound the launch); the render kernel's s_setprio
     // classes are >= 1/2, >= 1/4, >= 1/8 of the XCD's max and the rest
     auto cls = [mx](uint32_t k) {
-#ifdef SVO_ORDER_FINE   // the light tail split further: the lightest (sky) tiles dispatch last
-        return 8 * k >= 7 * mx ? 0 : 4 * k >= 3 * mx ? 1 : 2 * k >= mx ? 2 : 4 * k >= mx ? 3 : 8 * k >= mx ? 4
-               : 16 * k >= mx ? 5 : 32 * k >= mx ? 6 : 7;
-#else
         return 8 * k >= 7 * mx ? 0 : 4 * k >= 3 * mx ? 1 : 2 * k >= mx ? 2 : 4 * k >= mx ? 3 : 8 * k >= mx ? 4 : 5;
-#endif
     };
     for (Walk w = start(); w.e < len; next(w)) atomicAdd(&cnt[cls(cost[tile_of(w)])], 1u);
     __syncthreads();
@@ -1060,8 +1051,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         for (int c = 0; c < NC; ++c) {
             base[c] = run;
             run += cnt[c];
-            if (c >= 2 && c < 6) order[n + 4 + 4 * x + (c - 2)] = run;   // prio class ends
-            if (c == NC - 1) order[n + 4 + 4 * x + 3] = run;
+            if (c >= 2) order[n + 4 + 4 * x + (c - 2)] = run;   // prio class ends
         }
         if (x == 0) for (int c = 0; c < 4; ++c) order[n + c] = 0;   // global bounds unused in this mode
     }
