@@ -427,6 +427,139 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     if (LM_ON(ovf)) r.flags |= 4u;
 }
 
+// ------------------------------------------------------- latency form
+// trace_lean for launches that leave wave slots empty (svo_rt.hip launch: a strong split's
+// per-GPU band, a lone tile row): there a wave's serial trip chain, not the SIMD's issue
+// rate, bounds the launch, and the node fetch at the top of every trip is
+// the longest link of that chain (~L1 latency, after a POP also behind the stack read).
+// Same decisions, same arithmetic, same results; two changes to where the node comes from:
+//   * the stack entry also keeps the parent's node word (a second [slot][lane] uint2 array
+//     behind the {parent, t_max} one: 16 B per entry, 10 KB per wave at depth 10), so a
+//     POP takes the node from LDS with its parent instead of fetching it afterwards;
+//   * the next trip's node is loaded as soon as it is known, mid-trip: nodes[child] for
+//     PUSH lanes, the current node again for the others (an L1 hit), so the load's
+//     latency overlaps the rest of the trip instead of opening the next one.
+// !GUARD pools only (one tree, exact parents): the load offset is 32-bit and no parent
+// round trip is needed.  LDS doubles, so occupancy halves -- the reason this form is not
+// the full-frame default.
+template <int MODE>
+__device__ __forceinline__ void trace_lat(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk) {
+    constexpr int STRIDE = TILE;
+    const int slots = p.slots;
+    const int nodes_off = (slots + 1) * STRIDE;   // the node half of an entry, in uint2 units
+    for (int s = 0; s <= slots; ++s) {
+        stk[s * STRIDE] = make_uint2(0u, 0u);
+        stk[nodes_off + s * STRIDE] = make_uint2(0u, 0u);
+    }
+    const int scale_lo = S_MAX - slots;
+    lmask act = LM_OF(true);
+    const int oct = r.octant_mask | 16;
+    int sh = r.idx ^ oct;
+    const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
+    constexpr uint32_t SLOT = (uint32_t)(STRIDE * sizeof(uint2));
+    constexpr int SLOT_SH = 23 - 9;
+    const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
+    const uint32_t node_bytes = (uint32_t)nodes_off * (uint32_t)sizeof(uint2);
+    const uint2 *stk_pop = stk - (127 + scale_lo) * STRIDE;
+    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots);
+    int it = 0;
+    asm volatile("" : "+v"(r.parent));
+    // the root's node: every ray starts at node 0
+    uint2 pf = *(const uint2 *)((const char *)p.nodes + (uint32_t)(r.parent << 3));
+    uint2 nd_pop = make_uint2(0u, 0u);
+    lmask popped = 0;
+    lmask go;
+    do {
+        asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
+        // node-independent work first (it overlaps the wait for this trip's node)
+        const float tx = r.px * r.cx - r.bx;             // N:67-70
+        const float ty = r.py * r.cy - r.by;
+        const float tz = r.pz * r.cz - r.bz;
+        const float tc_max = fminf(fminf(tx, ty), tz);
+        const float tv_max = vmin(r.t_max, tc_max);
+        const float half = r.sexp * 0.5f;                // N:111-116
+        const lmask cx = LM_OF(center(half, r.cx, tx) > r.t_min);
+        const lmask cy = LM_OF(center(half, r.cy, ty) > r.t_min);
+        const lmask cz = LM_OF(center(half, r.cz, tz) > r.t_min);
+        const lmask lx = LM_OF(tx <= tc_max), ly = LM_OF(ty <= tc_max), lz = LM_OF(tz <= tc_max);
+        const lmask in_span = LM_OF(r.t_min <= tv_max), below_h = LM_OF(tc_max < r.h);
+        // this trip's node (N:60-62): popped from the stack, or loaded during the last trip
+        const uint2 nd = LM_ON(popped) ? nd_pop : pf;
+        const uint32_t cm = nd.x << sh;                  // valid bit -> bit 31, leaf bit -> bit 23
+        const lmask descend = act & LM_OF((int32_t)cm < 0) & in_span;
+        const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
+        const lmask hit = descend & leaf;                // N:93-94
+        const lmask store = descend & ~leaf & below_h;
+        const lmask push = descend & ~leaf;
+        const lmask adv = act & ~descend;
+        const uint32_t child = nd.y + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
+        // the next trip's node, as early as it is known: the child for PUSH lanes, this node
+        // again for the others (a POP lane takes its node from the stack instead)
+        pf = *(const uint2 *)((const char *)p.nodes + (uint32_t)((LM_ON(push) ? child : r.parent) << 3));
+        if (LM_ON(store)) {                              // N:97-98, + the parent's node
+            const uint32_t a = push_base + (__float_as_uint(r.sexp) >> SLOT_SH);
+            const uint32_t tmw = MODE == 0 ? (uint32_t)cvt_i32((float)(int32_t)__float_as_uint(r.t_max))
+                                           : __float_as_uint(r.t_max);
+            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(tmw) : "memory");
+            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a + node_bytes), "v"(nd.x), "v"(nd.y) : "memory");
+        }
+        const lmask sx = adv & lx;                       // N:122-125
+        const lmask sy = adv & ly;
+        const lmask sz = adv & lz;
+        const float se = r.sexp;
+        const float delta = LM_ON(push) ? half : -se;
+        const float ox = r.px, oy = r.py, oz = r.pz;
+        const lmask mvx = (push & cx) | sx, mvy = (push & cy) | sy, mvz = (push & cz) | sz;
+        const float qx = r.px + (LM_ON(mvx) ? delta : 0.0f);
+        const float qy = r.py + (LM_ON(mvy) ? delta : 0.0f);
+        const float qz = r.pz + (LM_ON(mvz) ? delta : 0.0f);
+        const int mv = lanes_to_idx(mvx, mvy, mvz);
+        const lmask pop = adv & LM_OF((mv & ~(sh ^ oct)) != 0);   // N:130-131
+        sh = (LM_ON(push) ? oct : sh) ^ mv;
+        if (LM_ON(push)) {
+            r.parent = child;
+            r.h = tc_max;
+            r.t_max = tv_max;
+            r.sexp = half;
+        }
+        r.t_min = LM_ON(adv) ? tc_max : r.t_min;
+        r.px = qx; r.py = qy; r.pz = qz;
+        lmask out = 0;
+        if (pop != 0) {                                  // N:134-154
+            const uint32_t diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) |
+                                  (__float_as_uint(oy) ^ __float_as_uint(qy)) |
+                                  (__float_as_uint(oz) ^ __float_as_uint(qz));
+            const uint32_t fd = __float_as_uint((float)diff);
+            const uint32_t ef = __builtin_amdgcn_ubfe(fd, 23, 8);   // scale + 127
+            const int scale = (int)ef - 127;
+            const uint32_t slot = min(ef, e_max) * STRIDE;
+            const uint2 e = stk_pop[slot];
+            nd_pop = stk_pop[nodes_off + slot];
+            const uint32_t keep = 0xFFFFFFFFu << scale;
+            const uint32_t bx_ = __builtin_amdgcn_ubfe(__float_as_uint(qx), scale, 1);
+            const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
+            const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
+            const bool pl = LM_ON(pop);
+            r.sexp = pl ? __uint_as_float((ef << 23) - (23u << 23)) : r.sexp;
+            r.parent = pl ? e.x : r.parent;
+            r.t_max = pl ? __uint_as_float(e.y) : r.t_max;
+            const uint32_t k = pl ? keep : 0xFFFFFFFFu;
+            r.px = __uint_as_float(__float_as_uint(r.px) & k);
+            r.py = __uint_as_float(__float_as_uint(r.py) & k);
+            r.pz = __uint_as_float(__float_as_uint(r.pz) & k);
+            r.h = pl ? 0.0f : r.h;
+            sh = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) ^ oct : sh;
+            out = pop & LM_OF(scale >= S_MAX);
+        }
+        popped = pop;
+        act &= ~(hit | out);
+        asm volatile("s_cmp_lt_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(go) : "s"(it), "n"(MAX_ITERS), "s"(act) : "scc");
+    } while (go != 0);
+    r.idx = sh ^ oct;
+    r.trips = it;
+    if (LM_ON(act)) r.flags |= 2u;                       // still tracing after MAX_ITERS trips
+}
+
 // Everything one finished primary ray writes.
 struct Record {
     uint32_t w[6];      // the svo_hit words; w[0..2] = the compact record
@@ -560,9 +693,11 @@ __device__ __forceinline__ int strip_tile(int x, int e, int tiles_x, int tiles_y
 // traces one shadow ray per hit lane, and the tile's recorded cost is the sum of
 // both, so one cost-ordered launch balances the whole frame.
 // COUNT: the instrumented launch (per-ray descriptor fetch counts, no outputs).
-template <int MODE, bool COUNT, bool FA = false, bool SH = false>
+// LAT: the latency form of the loop (trace_lat) for launches that leave wave slots empty;
+// twice the LDS (the stack entries keep their node).
+template <int MODE, bool COUNT, bool FA = false, bool SH = false, bool LAT = false>
 __global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int tiles_x) {
-    extern __shared__ uint2 stk_base[];   // [p.slots + 1][64]
+    extern __shared__ uint2 stk_base[];   // [p.slots + 1][64] (LAT: twice, the nodes behind)
     const int lane = threadIdx.x;
     const int n_tiles = (int)gridDim.x;
     const int t = p.tile_order ? (int)p.tile_order[blockIdx.x]
@@ -597,6 +732,7 @@ __global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int t
     to_fray(r, f);
     LeanDiag dg;
     if (COUNT) trace_lean<MODE, true, false, false, true>(p, f, stk);
+    else if (LAT) trace_lat<MODE>(p, f, stk);
     else if (!SH && p.wave_log) {
         if (p.guard) trace_lean<MODE, true, true>(p, f, stk, &dg);
         else trace_lean<MODE, false, true>(p, f, stk, &dg);
@@ -894,6 +1030,8 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
     const dim3 grid((unsigned)(bx * by)), block(TILE);
     if (COUNT)
         hipLaunchKernelGGL((render_tile_kernel<MODE, true>), grid, block, lds, stream, p, bx);
+    else if (p.lat)   // latency form (svo_rt.hip launch decides): the stack entries keep their node
+        hipLaunchKernelGGL((render_tile_kernel<MODE, false, false, false, true>), grid, block, 2 * lds, stream, p, bx);
     else if (p.shadows == 2) {   // shadow pass fused into the primary launch
         if (p.fetch_all && !p.guard)
             hipLaunchKernelGGL((render_tile_kernel<MODE, false, true, true>), grid, block, lds, stream, p, bx);

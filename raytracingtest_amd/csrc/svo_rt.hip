@@ -149,6 +149,7 @@ struct svo_ctx {
     int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
     int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
     int shadow_compact = 0;          // env SVO_SHADOW_COMPACT=1: that launch over the compacted hit list
+    int lat_tiles = 0;               // env SVO_LAT_TILES: launches of at most this many tiles take the latency form
     int order_every = 32;            // env SVO_ORDER_EVERY: rebuild the order every k-th launch (and after
                                      // every camera move or change of render mode)
     unsigned long long view_gen = 0; // bumped when svo_set_camera changes the matrices
@@ -513,6 +514,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.prio = ctx->prio;
     const bool ordered = ctx->tile_order && !p.out.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
+    // the latency form of the loop for launches too small to fill the chip's wave slots (a
+    // strong split's per-GPU band, a lone tile row): their time is a wave's serial chain
+    p.lat = !p.guard && p.shadows == 0 && !p.out.fetches && n_tiles <= ctx->lat_tiles;
     Geo key;
     Sched *q = nullptr;
     if (ordered) {
@@ -871,6 +875,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_FUSED_SHADOWS")) ctx->fused_shadows = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SHADOW_COMPACT")) ctx->shadow_compact = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
+    if (const char *k = std::getenv("SVO_LAT_TILES")) ctx->lat_tiles = std::max(0, std::atoi(k));
     if (e != hipSuccess) {
         destroy_single(ctx);
         return fail(SVO_ERR_HIP, std::string("svo_create: ") + hipGetErrorString(e));

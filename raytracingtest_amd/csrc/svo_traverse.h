@@ -79,6 +79,7 @@ struct LaunchParams {
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
     int fetch_all;                // lean loop (!guard): every lane loads its node every trip
+    int lat;                      // latency form of the loop (trace_lat; !guard, primary rays only)
     // The same cost-ordered dispatch for the two-pass shadow form (its own costs and order).
     const uint32_t *shadow_order;
     uint16_t *shadow_cost;
