@@ -1147,9 +1147,13 @@ size_t order_cost_capacity(int n_tiles) {
 // XCD strips (remap 2): workgroup x orders the tiles of XCD x's column strips
 // (see strip_tile) heaviest class first and writes them to the block positions
 // b = 8 j + x; the per-XCD class ends (in units of j) go to order[n + 4 + 4 x + c].
+// stats (nullable, host-visible): [2 x] = the max and [2 x + 1] = the sum of XCD x's tile
+// costs -- the launch's heaviest wave and its total wave trips, which the host uses to pick
+// the loop form of the next launches (svo_rt.hip launch).
 __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint16_t *__restrict__ cost,
-                                                                     uint32_t *__restrict__ order, int n, int tiles_x) {
-    __shared__ uint32_t red[ORDER_THREADS / 64];
+                                                                     uint32_t *__restrict__ order, int n, int tiles_x,
+                                                                     uint32_t *stats) {
+    __shared__ uint32_t red[ORDER_THREADS / 64], red_sum[ORDER_THREADS / 64];
     constexpr int NC = 6;
     __shared__ uint32_t cnt[NC], base[NC];
     const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1166,16 +1170,34 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         if (w.r >= tiles_y) { w.r -= tiles_y; w.c += 1; }
     };
     auto tile_of = [&](const Walk &w) { return w.r * tiles_x + w.c * 8 + x; };
-    uint32_t mx = 0;
-    for (Walk w = start(); w.e < len; next(w)) mx = max(mx, (uint32_t)cost[tile_of(w)]);
+    uint32_t mx = 0, sum = 0;
+    for (Walk w = start(); w.e < len; next(w)) {
+        const uint32_t k = cost[tile_of(w)];
+        mx = max(mx, k);
+        sum += k;
+    }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
-    if (lane == 0) red[wave] = mx;
+    for (int d = 32; d >= 1; d >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+        sum += (uint32_t)__shfl_xor((int)sum, d);
+    }
+    if (lane == 0) {
+        red[wave] = mx;
+        red_sum[wave] = sum;
+    }
     if (tid < NC) cnt[tid] = 0;
     __syncthreads();
     mx = 0;
+    sum = 0;
 #pragma unroll
-    for (int w = 0; w < ORDER_THREADS / 64; ++w) mx = max(mx, red[w]);
+    for (int w = 0; w < ORDER_THREADS / 64; ++w) {
+        mx = max(mx, red[w]);
+        sum += red_sum[w];
+    }
+    if (stats && tid == 0) {
+        stats[2 * x] = mx;
+        stats[2 * x + 1] = sum;
+    }
     // six classes, the top half split three ways so the very heaviest tiles are the
     // XCD's first dispatches (they bound the launch); the render kernel's s_setprio
     // classes are >= 1/2, >= 1/4, >= 1/8 of the XCD's max and the rest
@@ -1201,9 +1223,11 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     }
 }
 
-hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream) {
+hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
+                               uint32_t *stats) {
     if (n_tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x);
+    hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
+                       stats);
     return hipGetLastError();
 }
 

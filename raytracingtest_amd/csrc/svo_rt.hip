@@ -93,6 +93,7 @@ struct Sched {
     unsigned long long launches = 0, shadow_launches = 0;
     unsigned long long built_view = 0;   // the context's view generation the order was built under
     int built_mode = -1;                 // shadows | stack_mode << 2 of the costs it was built from
+    uint32_t *stats = nullptr;           // host-visible: per XCD max / sum of the tile costs the order kernel saw
 };
 
 struct Peer {                       // one per member of a multi-device context (index 0: the display device)
@@ -149,7 +150,8 @@ struct svo_ctx {
     int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
     int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
     int shadow_compact = 0;          // env SVO_SHADOW_COMPACT=1: that launch over the compacted hit list
-    int lat_tiles = 0;               // env SVO_LAT_TILES: launches of at most this many tiles take the latency form
+    int lat_mode = -1;               // env SVO_LAT: 0 never, 1 always, unset: by the last launch's costs (see launch)
+    double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold
     int order_every = 32;            // env SVO_ORDER_EVERY: rebuild the order every k-th launch (and after
                                      // every camera move or change of render mode)
     unsigned long long view_gen = 0; // bumped when svo_set_camera changes the matrices
@@ -514,9 +516,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.prio = ctx->prio;
     const bool ordered = ctx->tile_order && !p.out.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
-    // the latency form of the loop for launches too small to fill the chip's wave slots (a
-    // strong split's per-GPU band, a lone tile row): their time is a wave's serial chain
-    p.lat = !p.guard && p.shadows == 0 && !p.out.fetches && n_tiles <= ctx->lat_tiles;
     Geo key;
     Sched *q = nullptr;
     if (ordered) {
@@ -544,11 +543,41 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             HIP_TRY(hipMalloc(&q->shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
             q->cap = (size_t)n_tiles;
         }
+        if (!q->stats) {
+            HIP_TRY(hipHostMalloc(&q->stats, 16 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+            std::memset(q->stats, 0, 16 * sizeof(uint32_t));
+        }
         p.tile_order = q->order_key == key ? q->tile_order : nullptr;
         p.tile_cost = q->tile_cost;
         if (p.shadows == 1 && ctx->shadow_order_enabled) {
             p.shadow_cost = q->shadow_cost;
             p.shadow_order = q->shadow_key == key ? q->shadow_order : nullptr;
+        }
+    }
+    // Loop form.  A launch whose total work is small against its heaviest wave -- a strong
+    // split's per-GPU band, a sky-heavy pose, a lone tile row -- is bound by that wave's serial
+    // chain, and the latency form (svo_kernel.hip trace_lat: the node kept in the stack entry,
+    // the next node loaded mid-trip, half the occupancy) runs it faster; a launch that fills
+    // the chip's wave slots many times over is bound by issue, and the lean loop's full
+    // occupancy wins.  Measured: latency form faster when the last launch's
+    // wave trips T (sum over tiles) and heaviest tile M satisfy T < 0.3 * slots * M, slots =
+    // the lean loop's resident waves on the chip.  T and M come from the order kernel of the
+    // last order build at this geometry (host-visible, read without a sync: a stale value only
+    // picks the other, equally correct, form).
+    p.lat = 0;
+    if (!p.guard && p.shadows == 0 && !p.out.fetches && ctx->lat_mode != 0) {
+        if (ctx->lat_mode == 1) {
+            p.lat = 1;
+        } else if (q && q->stats && p.tile_order) {
+            uint32_t m = 0;
+            uint64_t t = 0;
+            for (int x = 0; x < 8; ++x) {
+                m = std::max(m, (uint32_t)((volatile uint32_t *)q->stats)[2 * x]);
+                t += ((volatile uint32_t *)q->stats)[2 * x + 1];
+            }
+            const size_t lds = (size_t)(p.slots + 1) * svo::TILE * sizeof(uint2);
+            const double slots = (double)ctx->num_cus * (double)std::min<size_t>(32, (160 * 1024) / lds);
+            p.lat = m > 0 && (double)t < ctx->lat_ratio * slots * (double)m ? 1 : 0;
         }
     }
     const char *log_path = std::getenv("SVO_WAVE_LOG");
@@ -580,7 +609,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                          (q->order_key != key || q->launches++ % ctx->order_every == 0 ||
                           q->built_view != ctx->view_gen || q->built_mode != mode_now);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
-        e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s)
+        if (q->order_key != key) std::memset(q->stats, 0, 16 * sizeof(uint32_t));   // another geometry's
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s,
+                                                        q->stats)
                              : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         q->order_key = key;
@@ -826,6 +857,7 @@ int destroy_single(svo_ctx *ctx) {
     for (Sched &q : ctx->sched) {
         free_sched(q);
         if (q.done) hipEventDestroy(q.done);
+        if (q.stats) hipHostFree(q.stats);
     }
     for (auto &v : ctx->timing_events)
         for (auto &ev : v) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
@@ -875,7 +907,8 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_FUSED_SHADOWS")) ctx->fused_shadows = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SHADOW_COMPACT")) ctx->shadow_compact = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
-    if (const char *k = std::getenv("SVO_LAT_TILES")) ctx->lat_tiles = std::max(0, std::atoi(k));
+    if (const char *k = std::getenv("SVO_LAT")) ctx->lat_mode = std::atoi(k) != 0 ? 1 : 0;
+    if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
     if (e != hipSuccess) {
         destroy_single(ctx);
         return fail(SVO_ERR_HIP, std::string("svo_create: ") + hipGetErrorString(e));

@@ -116,8 +116,11 @@ struct AssembleParams {
 // beyond n_tiles is read, never used).
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream);
 size_t order_cost_capacity(int n_tiles);
-// The same per XCD strip (xcd_remap 2): order must hold n_tiles + 36 entries.
-hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream);
+// The same per XCD strip (xcd_remap 2): order must hold n_tiles + 36 entries.  stats
+// (nullable, 16 words, host-visible memory): per XCD x the max [2 x] and the sum [2 x + 1]
+// of its tiles' costs.
+hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
+                               uint32_t *stats = nullptr);
 
 // Progressive accumulation (AddShader blend) of an RGBA32F sample frame.
 hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32_t sample, int num_cus,

@@ -1,5 +1,5 @@
-"""A/B of the render loop's latency form (trace_lat, env SVO_LAT_TILES) against the lean
-loop on launches of decreasing size: the whole C3 frame, one rank's band of the strong
+"""A/B of the render loop's latency form (trace_lat, env SVO_LAT=1) against the lean loop
+(SVO_LAT=0) and the library's automatic choice (SVO_LAT unset) on launches of decreasing size: the whole C3 frame, one rank's band of the strong
 1920x1080 split at N = 2, 4, 8 (round-robin 8-row bands), and the tile row holding the
 frame's heaviest tile alone.  Kernel time = the library's HIP events around the render
 kernel (mean of K launches after warmup).  Both contexts render the same frame; their hit
@@ -34,13 +34,15 @@ def main():
     cam = CAMERAS[a.camera or cfg["camera"]]()
     svo = build_sampler_svo(cfg["sampler"], cfg["max_level"])
     ctx = {}
-    for name, tiles in (("lean", "0"), ("lat", "1000000000")):
-        os.environ["SVO_LAT_TILES"] = tiles
+    for name, lat in (("lean", "0"), ("lat", "1"), ("auto", None)):
+        if lat is None:
+            os.environ.pop("SVO_LAT", None)
+        else:
+            os.environ["SVO_LAT"] = lat
         rm = RaytracingMaster(capacity_nodes=len(svo))
         rm.SetSVOBuffer(svo)
         rm.UpdateShaderParameters(cam, W, H)
         ctx[name] = rm
-    del os.environ["SVO_LAT_TILES"]
     cases = [("frame", None), ("band N=2", (8, 1, 2)), ("band N=4", (8, 1, 4)), ("band N=8", (8, 1, 8)),
              (f"tile row {a.heavy_row}", (8, a.heavy_row, (H + 7) // 8))]
     s = torch.cuda.Stream()
@@ -63,10 +65,11 @@ def main():
             torch.cuda.synchronize()
             out[name] = ms
             hits[name] = h.cpu().numpy()
-        same = np.array_equal(hits["lean"], hits["lat"])
+        same = np.array_equal(hits["lean"], hits["lat"]) and np.array_equal(hits["lean"], hits["auto"])
         tiles = ((W + 7) // 8) * ((rows + 7) // 8)
         print(f"{label:>14}: {tiles:6d} tiles  lean {out['lean'] * 1e3:8.1f} us  lat {out['lat'] * 1e3:8.1f} us  "
-              f"lat/lean {out['lat'] / out['lean']:.3f}  hit records identical: {same}", flush=True)
+              f"lat/lean {out['lat'] / out['lean']:.3f}  auto {out['auto'] * 1e3:8.1f} us  "
+              f"hit records identical: {same}", flush=True)
         if not same:
             raise SystemExit("latency form and lean loop disagree")
     for rm in ctx.values():
