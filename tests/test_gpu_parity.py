@@ -197,7 +197,7 @@ def test_errors_are_loud(rm):
 @pytest.mark.parametrize("env", [
     {"SVO_XCD_REMAP": "0"}, {"SVO_TILE_ORDER": "0"}, {"SVO_PRIO": "0"}, {"SVO_FETCH_ALL": "0"},
     {"SVO_FETCH_ALL": "1"}, {"SVO_ORDER_EVERY": "1"}, {"SVO_SHADOW_ORDER": "0", "SVO_FUSED_SHADOWS": "0"},
-    {"SVO_SHADOW_COMPACT": "1"}])
+    {"SVO_SHADOW_COMPACT": "1"}, {"SVO_LAT": "1"}, {"SVO_LAT": "0"}, {"SVO_LAT_RATIO": "1000"}])
 def test_runtime_switches_identical(oracle_mod, monkeypatch, env):
     """Every surviving placement / loop-form switch (svo_rt.hip svo_create; the
     loop forms and block shapes measured slower in round 1 were removed) gives
@@ -405,3 +405,40 @@ def test_c1_golden_frames(rm, text_svo, mode, camera_name):
     rm.UpdateShaderParameters(main_camera() if camera_name == "main" else overview_camera(), 256, 256)
     rgba, hits = rm.Render(256, 256, stack_mode=mode)
     _compare(hits, rgba, ref_hits, z[camera_name + "_rgba"].reshape(-1, 4))
+
+
+@pytest.mark.parametrize("stack_mode", [0, 1])
+def test_loop_forms_identical_on_a_split_band(oracle_mod, monkeypatch, stack_mode):
+    """The two loop forms (lean; latency: the node kept in the stack entry, the next node
+    loaded mid-trip) and the automatic choice between them (the order kernel's cost stats,
+    svo_rt.hip launch) give the oracle's records on a strong-split band of a depth-9 terrain
+    pool -- the launch size where the automatic choice switches forms -- over repeated
+    launches, both stack modes."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    svo = build_sampler_svo(4, 10)
+    cam = overview_camera()
+    w, h = 1024, 576
+    band = (8, 1, 4)
+    ys = band_rows(h, band)
+    ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, svo, cam, w, h, stack_mode)
+    ref = ref_hits.reshape(h, w)[ys]
+    for lat in ("0", "1", None):
+        if lat is None:
+            monkeypatch.delenv("SVO_LAT", raising=False)
+        else:
+            monkeypatch.setenv("SVO_LAT", lat)
+        m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+        try:
+            m.SetSVOBuffer(svo)
+            m.UpdateShaderParameters(cam, w, h)
+            buf = torch.empty(len(ys) * w * 24, dtype=torch.uint8, device="cuda")
+            for _ in range(6):   # the order (and its stats) exist from the second launch on
+                m.render_device(w, h, hits_ptr=buf.data_ptr(), band=band, stack_mode=stack_mode)
+                m.synchronize()
+                got = buf.cpu().numpy().view(ref.dtype).reshape(len(ys), w)
+                assert got.tobytes() == ref.tobytes(), f"SVO_LAT={lat}"
+        finally:
+            m.close()
