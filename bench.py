@@ -72,8 +72,8 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=None, help="GPUs (default: WORLD_SIZE under torchrun, else 1)")
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--config", choices=sorted(CONFIGS), default="C3",
                    help="BASELINE.json workload; the flags below override its fields")
     p.add_argument("--width", type=int, default=None)

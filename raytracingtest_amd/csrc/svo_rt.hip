@@ -94,6 +94,16 @@ struct Sched {
     unsigned long long built_view = 0;   // the context's view generation the order was built under
     int built_mode = -1;                 // shadows | stack_mode << 2 of the costs it was built from
     uint32_t *stats = nullptr;           // host-visible: per XCD max / sum of the tile costs the order kernel saw
+    // loop-form choice (see launch): stats are read only once the order build that wrote
+    // them has completed (stats_ev); the decision they give is kept with the geometry and
+    // view they were measured at
+    hipEvent_t stats_ev = nullptr;       // recorded behind the last order build
+    bool stats_pending = false;
+    Geo stats_key;                       // geometry / view of the pending build
+    unsigned long long stats_view = 0;
+    int lat_cache = 0;                   // the decision of the last completed build ...
+    Geo lat_key;                         // ... made at this geometry / view (width -1: none)
+    unsigned long long lat_view = 0;
 };
 
 struct Peer {                       // one per member of a multi-device context (index 0: the display device)
@@ -238,6 +248,8 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         if (pick->done) HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
         pick->order_key = pick->shadow_key = Geo();   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
+        pick->stats_pending = false;
+        pick->lat_key = Geo();
     }
     if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
     pick->stream = s;
@@ -546,6 +558,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         if (!q->stats) {
             HIP_TRY(hipHostMalloc(&q->stats, 16 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
             std::memset(q->stats, 0, 16 * sizeof(uint32_t));
+            HIP_TRY(hipEventCreateWithFlags(&q->stats_ev, hipEventDisableTiming));
         }
         p.tile_order = q->order_key == key ? q->tile_order : nullptr;
         p.tile_cost = q->tile_cost;
@@ -559,25 +572,44 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // chain, and the latency form (svo_kernel.hip trace_lat: the node kept in the stack entry,
     // the next node loaded mid-trip, half the occupancy) runs it faster; a launch that fills
     // the chip's wave slots many times over is bound by issue, and the lean loop's full
-    // occupancy wins.  Measured: latency form faster when the last launch's
-    // wave trips T (sum over tiles) and heaviest tile M satisfy T < 0.3 * slots * M, slots =
-    // the lean loop's resident waves on the chip.  T and M come from the order kernel of the
-    // last order build at this geometry (host-visible, read without a sync: a stale value only
-    // picks the other, equally correct, form).
+    // occupancy wins.  Measured: latency form faster when the wave trips T
+    // (sum over tiles) and heaviest tile M satisfy T < 0.3 * slots * M, slots = the lean
+    // loop's resident waves on the chip.  T and M come from the order kernel of the last
+    // COMPLETED order build at this geometry (stats_ev; the host may be many launches ahead
+    // of the GPU).  Decisions of an earlier view are kept while the camera moves (one launch
+    // per view: the last frame's costs); once a build for the current view is in flight --
+    // the second launch after a move -- the host waits for it (once per view), so a jump to
+    // a different pose is never rendered with another pose's choice.
     p.lat = 0;
     if (!p.guard && p.shadows == 0 && !p.out.fetches && ctx->lat_mode != 0) {
         if (ctx->lat_mode == 1) {
             p.lat = 1;
         } else if (q && q->stats && p.tile_order) {
-            uint32_t m = 0;
-            uint64_t t = 0;
-            for (int x = 0; x < 8; ++x) {
-                m = std::max(m, (uint32_t)((volatile uint32_t *)q->stats)[2 * x]);
-                t += ((volatile uint32_t *)q->stats)[2 * x + 1];
+            if (q->stats_pending) {
+                const bool wait = q->stats_key == key && q->stats_view == ctx->view_gen &&
+                                  !(q->lat_key == key && q->lat_view == ctx->view_gen);
+                const hipError_t st = wait ? hipEventSynchronize(q->stats_ev) : hipEventQuery(q->stats_ev);
+                if (st == hipSuccess) {
+                    uint32_t m = 0;
+                    uint64_t t = 0;
+                    for (int x = 0; x < 8; ++x) {
+                        m = std::max(m, (uint32_t)((volatile uint32_t *)q->stats)[2 * x]);
+                        t += ((volatile uint32_t *)q->stats)[2 * x + 1];
+                    }
+                    const size_t lds = (size_t)(p.slots + 1) * svo::TILE * sizeof(uint2);
+                    const double slots = (double)ctx->num_cus * (double)std::min<size_t>(32, (160 * 1024) / lds);
+                    q->lat_cache = m > 0 && (double)t < ctx->lat_ratio * slots * (double)m ? 1 : 0;
+                    q->lat_key = q->stats_key;
+                    q->lat_view = q->stats_view;
+                    q->stats_pending = false;
+                    if (std::getenv("SVO_LAT_DEBUG"))   // diagnostics: the decision and its inputs
+                        std::fprintf(stderr, "svo lat: view %llu T %llu M %u slots %.0f -> %s\n", q->lat_view,
+                                     (unsigned long long)t, m, slots, q->lat_cache ? "latency" : "lean");
+                } else if (st != hipErrorNotReady) {
+                    return fail(SVO_ERR_HIP, std::string("order build event: ") + hipGetErrorString(st));
+                }
             }
-            const size_t lds = (size_t)(p.slots + 1) * svo::TILE * sizeof(uint2);
-            const double slots = (double)ctx->num_cus * (double)std::min<size_t>(32, (160 * 1024) / lds);
-            p.lat = m > 0 && (double)t < ctx->lat_ratio * slots * (double)m ? 1 : 0;
+            p.lat = q->lat_key == key ? q->lat_cache : 0;
         }
     }
     const char *log_path = std::getenv("SVO_WAVE_LOG");
@@ -609,7 +641,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                          (q->order_key != key || q->launches++ % ctx->order_every == 0 ||
                           q->built_view != ctx->view_gen || q->built_mode != mode_now);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
-        if (q->order_key != key) std::memset(q->stats, 0, 16 * sizeof(uint32_t));   // another geometry's
         e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s,
                                                         q->stats)
                              : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s);
@@ -617,6 +648,12 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         q->order_key = key;
         q->built_view = ctx->view_gen;
         q->built_mode = mode_now;
+        if (q->stats_ev && p.xcd_remap == 2) {
+            HIP_TRY(hipEventRecord(q->stats_ev, s));
+            q->stats_pending = true;
+            q->stats_key = key;
+            q->stats_view = ctx->view_gen;
+        }
     }
     if (q && p.shadow_cost && (q->shadow_key != key || q->shadow_launches++ % ctx->order_every == 0)) {
         e = p.xcd_remap == 2 ? svo::launch_order_strips(q->shadow_cost, q->shadow_order, n_tiles, (width + 7) / 8, s)
@@ -857,6 +894,7 @@ int destroy_single(svo_ctx *ctx) {
     for (Sched &q : ctx->sched) {
         free_sched(q);
         if (q.done) hipEventDestroy(q.done);
+        if (q.stats_ev) hipEventDestroy(q.stats_ev);
         if (q.stats) hipHostFree(q.stats);
     }
     for (auto &v : ctx->timing_events)

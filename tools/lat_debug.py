@@ -1,0 +1,52 @@
+"""The automatic loop-form choice across camera jumps, submitted the way bench.py's
+extra_poses does (10 + 20 launches per pose, no host sync between them): prints the
+library's decisions (SVO_LAT_DEBUG) and each pose's kernel time.  A pose must get the
+form its own costs call for, not the previous pose's.
+
+  python tools/lat_debug.py [--config C3]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["SVO_LAT_DEBUG"] = "1"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    a = ap.parse_args()
+    import torch
+    from bench import CONFIGS
+    from raytracingtest_amd import RaytracingMaster
+    from raytracingtest_amd.camera import CAMERAS
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    cfg = CONFIGS[a.config]
+    W, H, mode = cfg["width"], cfg["height"], cfg["stack_mode"]
+    svo = build_sampler_svo(cfg["sampler"], cfg["max_level"])
+    rm = RaytracingMaster(capacity_nodes=len(svo))
+    rm.SetSVOBuffer(svo)
+    h = torch.empty(W * H * 24, dtype=torch.uint8, device="cuda")
+    rg = torch.empty(W * H * 4, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    for pose in ("flyover", "overview", "main", "terrain", "overview", "flyover"):
+        rm.UpdateShaderParameters(CAMERAS[pose](), W, H)
+        print(f"== pose {pose}", file=sys.stderr, flush=True)
+        for _ in range(10):
+            rm.render_device(W, H, hits_ptr=h.data_ptr(), rgba_ptr=rg.data_ptr(), stack_mode=mode, stream=s.cuda_stream)
+        rm.set_kernel_timing(True)
+        rm.kernel_time()
+        for _ in range(20):
+            rm.render_device(W, H, hits_ptr=h.data_ptr(), rgba_ptr=rg.data_ptr(), stack_mode=mode, stream=s.cuda_stream)
+        ms, _ = rm.kernel_time()
+        rm.set_kernel_timing(False)
+        torch.cuda.synchronize()
+        print(f"   {pose}: kernel {ms * 1e3:.1f} us", file=sys.stderr, flush=True)
+    rm.close()
+
+
+if __name__ == "__main__":
+    main()
