@@ -4,6 +4,6 @@
 set -o pipefail
 OUT=gpurun_out/$1; mkdir -p $OUT
 for c in ${CONFIGS:-C1 C2 C4 C5}; do
-  timeout -k 10 300 python bench.py --config $c --steps 30 --warmup 3 --cpu-seconds ${CPU_SECONDS:-0} > $OUT/config_$c.json 2>> $OUT/configs.err || exit $?
+  timeout -k 10 300 python bench.py --config $c --steps ${STEPS:-300} --warmup 20 --cpu-seconds ${CPU_SECONDS:-0} > $OUT/config_$c.json 2>> $OUT/configs.err || exit $?
 done
 echo done

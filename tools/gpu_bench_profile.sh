@@ -8,9 +8,9 @@ TAG=${1:-r1}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 400 python bench.py --steps 50 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || exit $?
-timeout -k 10 300 python bench.py --steps 30 --warmup 5 --camera overview --cpu-seconds 0 > $OUT/bench_overview.json 2>> $OUT/bench.err || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 30 --warmup 5 --cpu-seconds 0 --no-extras > $OUT/bench_prof.json 2> $OUT/prof.err || exit $?
+timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?
+timeout -k 10 300 python bench.py --camera overview --cpu-seconds 0 > $OUT/bench_overview.json 2>> $OUT/bench.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --cpu-seconds 0 --no-extras > $OUT/bench_prof.json 2> $OUT/prof.err || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex render_tile_kernel -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-extras > /dev/null 2> $OUT/pmc1.err || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --kernel-include-regex render_tile_kernel -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-extras > /dev/null 2> $OUT/pmc2.err || exit $?
 timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --kernel-include-regex render_tile_kernel -d $OUT/pmc_l2 -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-extras > /dev/null 2> $OUT/pmc3.err || exit $?
