@@ -369,7 +369,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         const lmask pop = adv & LM_OF((mv & ~(sh ^ oct)) != 0);   // N:130-131: (idx ^ step) & step
         const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
         sh = (LM_ON(push) ? oct : sh) ^ mv;             // PUSH: idx = mv, else idx ^= mv
-        if (LM_ON(push)) {
+        if (LM_ON(push)) {   // an exec-masked block: 4 selects instead cost +1 % / +3.5 % (r03j)
             r.parent = child;
             r.h = tc_max;
             r.t_max = tv_max;
