@@ -442,3 +442,43 @@ def test_loop_forms_identical_on_a_split_band(oracle_mod, monkeypatch, stack_mod
                 assert got.tobytes() == ref.tobytes(), f"SVO_LAT={lat}"
         finally:
             m.close()
+
+
+def test_loop_form_choice_follows_the_pose(monkeypatch, capfd):
+    """The automatic loop form (svo_rt.hip launch) is decided from the dispatch-order build
+    of the CURRENT camera view: across jumps between unrelated poses of the C3 frame, each
+    submitted as a burst of launches with no host sync (the host runs ahead of the GPU),
+    every decision taken at a pose uses that pose's own costs -- the sky-heavy overview the
+    latency form, the flyover and Main poses the lean loop.  Reads the
+    library's SVO_LAT_DEBUG trace."""
+    import re
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from raytracingtest_amd.camera import CAMERAS
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    monkeypatch.setenv("SVO_LAT_DEBUG", "1")
+    monkeypatch.delenv("SVO_LAT", raising=False)
+    monkeypatch.delenv("SVO_LAT_RATIO", raising=False)
+    svo = build_sampler_svo(4, 11)   # config C3's pool
+    w, h = 1920, 1080
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        buf = torch.empty(w * h * 24, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        plan = [("flyover", "lean"), ("overview", "latency"), ("main", "lean"), ("overview", "latency")]
+        for view, (pose, form) in enumerate(plan, start=1):
+            capfd.readouterr()
+            m.UpdateShaderParameters(CAMERAS[pose](), w, h)
+            for _ in range(12):
+                m.render_device(w, h, hits_ptr=buf.data_ptr(), stack_mode=0)
+            m.synchronize()
+            err = capfd.readouterr().err
+            decisions = re.findall(r"svo lat: view (\d+) .*-> (\w+)", err)
+            mine = [f for v, f in decisions if int(v) == view]
+            assert mine, f"no decision from view {view} ({pose}): {decisions}"
+            assert all(f == form for f in mine), f"{pose}: {decisions}"
+            assert all(int(v) >= view - 1 for v, _ in decisions), f"{pose}: stale decisions {decisions}"
+    finally:
+        m.close()
