@@ -12,7 +12,7 @@ LIB_DIR = os.path.join(ROOT, "raytracingtest_amd")
 SRC = os.path.join(ROOT, "examples", "render_min.c")
 
 
-def _build(tmp_path, src=SRC, name="render_min", libs=("-lsvo_rt",)):
+def _build(tmp_path, src=SRC, name="render_min", libs=("-lsvo_rt",), extra=()):
     for lib in libs:
         if not os.path.exists(os.path.join(LIB_DIR, "lib" + lib[2:] + ".so")):
             pytest.skip(f"lib{lib[2:]}.so not built (run __graft_entry__.build())")
@@ -20,7 +20,7 @@ def _build(tmp_path, src=SRC, name="render_min", libs=("-lsvo_rt",)):
     if cc is None:
         pytest.skip("no C compiler")
     exe = str(tmp_path / name)
-    subprocess.run([cc, "-O2", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), src,
+    subprocess.run([cc, "-O2", "-std=c99", "-Wall", "-Werror", *extra, "-I", os.path.join(ROOT, "include"), src,
                     "-L", LIB_DIR, *libs, "-L/opt/rocm/lib", "-lamdhip64", "-lm",
                     "-Wl,-rpath," + LIB_DIR, "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
     return exe
@@ -29,6 +29,24 @@ def _build(tmp_path, src=SRC, name="render_min", libs=("-lsvo_rt",)):
 def _build_key_r(tmp_path):
     return _build(tmp_path, os.path.join(ROOT, "examples", "build_and_render.c"), "build_and_render",
                   ("-lsvo_rt", "-lsvo_build"))
+
+
+def _build_bench(tmp_path):
+    if not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
+        pytest.skip("no HIP headers")
+    return _build(tmp_path, os.path.join(ROOT, "examples", "bench_native.c"), "bench_native",
+                  ("-lsvo_rt", "-lsvo_build"), ("-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"))
+
+
+def _camera_blob(W, H, name="flyover"):
+    import numpy as np
+    from raytracingtest_amd.camera import CAMERAS, column_major, main_light
+    c2w, inv_proj = CAMERAS[name]().uniforms(W, H)
+    blob = np.concatenate([column_major(np.asarray(c2w, np.float32)).reshape(-1),
+                           column_major(np.asarray(inv_proj, np.float32)).reshape(-1),
+                           np.asarray(main_light(), np.float32)]).astype(np.float32)
+    assert blob.size == 36
+    return blob.tobytes()
 
 
 def test_c_host_compiles_and_links(tmp_path):
@@ -42,6 +60,26 @@ def test_c_host_renders(tmp_path):
     assert out.returncode == 0, out.stdout + out.stderr
     assert "render_min: ok" in out.stdout
     assert (tmp_path / "frame.ppm").stat().st_size == len("P6\n64 64\n255\n") + 64 * 64 * 3
+
+
+def test_c_bench_host_compiles_and_links(tmp_path):
+    assert os.path.exists(_build_bench(tmp_path))
+
+
+@pytest.mark.gpu
+def test_c_bench_host_runs(tmp_path):
+    """examples/bench_native.c: the metric's frame (C3 pool, 1920x1080, flyover) timed from a
+    plain C process through the C-ABIs alone; a short run here, the full one in profiles/."""
+    import json
+    exe = _build_bench(tmp_path)
+    (tmp_path / "cam.bin").write_bytes(_camera_blob(1920, 1080))
+    out = subprocess.run([exe, "4", "11", str(tmp_path / "cam.bin"), "1920", "1080", "20", "5"],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["nodes"] == 1569748 and r["stack_mode"] == "hlsl" and r["kernel_launches"] == 20
+    assert 0.0 < r["kernel_ms"] <= r["ms_per_step"] * 1.5
+    assert r["Mrays_per_s"] > 1000.0
 
 
 def test_c_host_key_r_compiles_and_links(tmp_path):

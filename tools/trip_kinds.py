@@ -122,6 +122,23 @@ def trace_kinds(nodes, o, d):
     return kinds
 
 
+def fold2(ks):
+    """Folded trips of one ray when a trip whose iteration is a same-node ADVANCE also
+    runs the next iteration (a second evaluation stage, no fetch in between), and
+    which of those trips carry the second stage."""
+    trips, two = [], []
+    i = 0
+    while i < len(ks):
+        if ks[i] == "ADV" and i + 1 < len(ks):
+            two.append(True)
+            i += 2
+        else:
+            two.append(False)
+            i += 1
+        trips.append(1)
+    return two
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("npz")
@@ -143,10 +160,12 @@ def main():
     cost = tiles.max(1)
     order = np.argsort(-cost)[:a.tiles]
     tot = collections.Counter()
+    fold2_rows = []
     nodes_l = nodes.tolist()
     for k in order:
         r0, c0 = divmod(int(k), tx)
         per_lane_fold = []
+        per_lane_two = []
         kc = collections.Counter()
         for j in range(64):
             y, x = r0 * 8 + j // 8, c0 * 8 + j % 8
@@ -156,10 +175,16 @@ def main():
                 raise SystemExit(f"restatement disagrees with the oracle at ({x}, {y}): {len(ks)} vs {it[y, x]}")
             kc.update(ks)
             per_lane_fold.append(len(ks) - ks.count("ADV"))
+            per_lane_two.append(fold2(ks))
         tot.update(kc)
+        f2 = max(len(t) for t in per_lane_two)
+        stage2 = sum(1 for j in range(f2) if any(j < len(t) and t[j] for t in per_lane_two))
+        fold2_rows.append((int(cost[k]), f2, stage2))
         n = sum(kc.values())
         print(f"tile {int(k):6d} (row {r0}): wave trips {cost[k]:4d}, folded {max(per_lane_fold):4d}   "
               + "  ".join(f"{kk} {100.0 * kc[kk] / n:4.1f}%" for kk in ("PUSH", "ADV", "POP", "HIT")), flush=True)
+    for c, f2, st in fold2_rows:
+        print(f"two-stage trip: wave trips {c:4d} -> {f2:4d} ({100.0 * f2 / c:5.1f} %), second stage on {st:4d} trips")
     n = sum(tot.values())
     pd = collections.Counter(kinds_pop_dist)
     npd = sum(pd.values())
