@@ -622,18 +622,30 @@ __device__ __forceinline__ void record(const LaunchParams &p, const Ray &r, int 
     }
 }
 
+// Output stores are non-temporal (global_store ... nt): the frame's 40-84 MB of records and
+// colours stream through L2 once, and with the default policy they evict the node pool's lines
+// there -- a trip whose node fetch misses L1 (most wave trips have one such lane) then waits on
+// the Infinity Cache instead of L2.  C3 flyover kernel 0.1066 -> 0.1030 ms, Main pose -0.8 %
+// (profiles/r03n_ab_nt_stores.txt).
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ void store_outputs(const Outputs &out, size_t i, const Record &o) {
     if (out.hits) {
-        uint2 *dst = reinterpret_cast<uint2 *>(out.hits + i);
-        dst[0] = make_uint2(o.w[0], o.w[1]);
-        dst[1] = make_uint2(o.w[2], o.w[3]);
-        dst[2] = make_uint2(o.w[4], o.w[5]);
+        u32x2 *dst = reinterpret_cast<u32x2 *>(out.hits + i);
+        __builtin_nontemporal_store(u32x2{o.w[0], o.w[1]}, dst + 0);
+        __builtin_nontemporal_store(u32x2{o.w[2], o.w[3]}, dst + 1);
+        __builtin_nontemporal_store(u32x2{o.w[4], o.w[5]}, dst + 2);
     }
-    if (out.compact) reinterpret_cast<uint3 *>(out.compact)[i] = make_uint3(o.w[0], o.w[1], o.w[2]);
-    if (out.rgba) out.rgba[i] = make_float4(o.rgb[0], o.rgb[1], o.rgb[2], 1.0f);
+    if (out.compact)
+        // a 3-vector is 16 bytes apart in arrays: address the 12-byte record explicitly
+        __builtin_nontemporal_store(u32x3{o.w[0], o.w[1], o.w[2]}, reinterpret_cast<u32x3 *>(out.compact + 3 * i));
+    if (out.rgba)
+        __builtin_nontemporal_store(f32x4{o.rgb[0], o.rgb[1], o.rgb[2], 1.0f}, reinterpret_cast<f32x4 *>(out.rgba + i));
     if (out.rgba8 || out.rgb8) {
         const uint32_t w = pack_rgba8(o.rgb[0], o.rgb[1], o.rgb[2]);
-        if (out.rgba8) out.rgba8[i] = w;
+        if (out.rgba8) __builtin_nontemporal_store(w, out.rgba8 + i);
         if (out.rgb8) {
             uint8_t *d = out.rgb8 + 3 * i;
             d[0] = (uint8_t)w;
@@ -641,8 +653,9 @@ __device__ __forceinline__ void store_outputs(const Outputs &out, size_t i, cons
             d[2] = (uint8_t)(w >> 16);
         }
     }
-    if (out.position) out.position[i] = make_float4(o.pos[0], o.pos[1], o.pos[2], 0.0f);
-    if (out.voxel) out.voxel[i] = o.key;
+    if (out.position)
+        __builtin_nontemporal_store(f32x4{o.pos[0], o.pos[1], o.pos[2], 0.0f}, reinterpret_cast<f32x4 *>(out.position + i));
+    if (out.voxel) __builtin_nontemporal_store(o.key, out.voxel + i);
 }
 
 // Shadow ray of a primary hit (the reference's test is commented
@@ -681,9 +694,18 @@ __device__ __forceinline__ size_t out_index(const LaunchParams &p, int lr, int g
 // through its own columns while every XCD samples the whole screen (sky and
 // terrain alike).  Needs the tile columns to be a multiple of 8 (the host
 // checks).  e = position within the XCD's share, column-major.
+#ifndef SVO_STRIP_K
+#define SVO_STRIP_K 1
+#endif
+// strips SVO_STRIP_K tile columns wide: XCD x owns columns c with (c / K) % 8 == x (K = 2, 3
+// within noise of 1, 5 and 6 +3 %: profiles/r03n_ab_strip_width.txt)
+__device__ __forceinline__ int strip_col(int x, int m) {
+    constexpr int K = SVO_STRIP_K;
+    return K == 1 ? m * 8 + x : (m / K) * (8 * K) + x * K + (m % K);
+}
 __device__ __forceinline__ int strip_tile(int x, int e, int tiles_x, int tiles_y) {
     const int m = e / tiles_y, row = e - m * tiles_y;
-    return row * tiles_x + m * 8 + x;
+    return row * tiles_x + strip_col(x, m);
 }
 
 // FA: the lean loop's unpredicated node loads (p.fetch_all) -- a separate
@@ -1169,7 +1191,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         w.e += ORDER_THREADS; w.c += dc; w.r += dr;
         if (w.r >= tiles_y) { w.r -= tiles_y; w.c += 1; }
     };
-    auto tile_of = [&](const Walk &w) { return w.r * tiles_x + w.c * 8 + x; };
+    auto tile_of = [&](const Walk &w) { return w.r * tiles_x + strip_col(x, w.c); };
     uint32_t mx = 0, sum = 0;
     for (Walk w = start(); w.e < len; next(w)) {
         const uint32_t k = cost[tile_of(w)];
