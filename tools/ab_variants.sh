@@ -10,7 +10,7 @@ for rep in 1 2; do
   for name in "$@"; do
     lib="$ROOT/build/ab/libsvo_rt_$name.so"
     line="$name"
-    for cam in flyover main; do
+    for cam in ${AB_CAMS:-flyover main}; do
       SVO_RT_LIB=$lib timeout -k 10 200 python bench.py --steps 300 --warmup 20 --cpu-seconds 0 --no-extras --camera $cam \
         > gpurun_out/ab/out.json 2>>gpurun_out/ab/err.log || exit $?
       line="$line $cam $(python3 -c "import json; d=json.load(open('gpurun_out/ab/out.json')); print(d['roofline']['kernel_ms'])")"
