@@ -694,13 +694,9 @@ __device__ __forceinline__ size_t out_index(const LaunchParams &p, int lr, int g
 // through its own columns while every XCD samples the whole screen (sky and
 // terrain alike).  Needs the tile columns to be a multiple of 8 (the host
 // checks).  e = position within the XCD's share, column-major.
-#ifndef SVO_STRIP_K
-#define SVO_STRIP_K 1
-#endif
-// strips SVO_STRIP_K tile columns wide: XCD x owns columns c with (c / K) % 8 == x (K = 2, 3
-// within noise of 1, 5 and 6 +3 %: profiles/r03n_ab_strip_width.txt)
+// strips STRIP_K tile columns wide: XCD x owns columns c with (c / K) % 8 == x
 __device__ __forceinline__ int strip_col(int x, int m) {
-    constexpr int K = SVO_STRIP_K;
+    constexpr int K = STRIP_K;
     return K == 1 ? m * 8 + x : (m / K) * (8 * K) + x * K + (m % K);
 }
 __device__ __forceinline__ int strip_tile(int x, int e, int tiles_x, int tiles_y) {

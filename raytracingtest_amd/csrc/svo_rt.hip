@@ -498,10 +498,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.out = out;
     if (b.count == 1) p.out.frame_layout = 0;   // the whole frame: both layouts coincide
     p.xcd_remap = ctx->xcd_remap;
-#ifndef SVO_STRIP_K
-#define SVO_STRIP_K 1
-#endif
-    if (p.xcd_remap == 2 && ((width + 7) / 8) % (8 * SVO_STRIP_K) != 0) p.xcd_remap = 0;
+    if (p.xcd_remap == 2 && ((width + 7) / 8) % (8 * svo::STRIP_K) != 0) p.xcd_remap = 0;
     p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? (ctx->shadow_compact ? 3 : ctx->fused_shadows ? 2 : 1) : 0;
     if (p.shadows == 3 && out.hitmask) p.shadows = 1;   // the caller's masks are not a list scratch
     if (p.local_rows == 0) return SVO_OK;

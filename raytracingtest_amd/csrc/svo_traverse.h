@@ -20,6 +20,13 @@ constexpr int MAX_ITERS = 65536;   // safety net, identical in oracle/svo_oracle
 constexpr int TILE = 64;           // one wave64 = one 8x8 pixel tile
 constexpr int MAX_PARTS = 64;      // band parts one assemble launch reads (devices / ranks)
 constexpr int MAX_CYCLE = 256;     // bands per cycle of a weighted band deal (svo_band.cycle)
+// XCD column strips are STRIP_K tile columns wide (svo_kernel.hip strip_col; compile-time knob
+// -DSVO_STRIP_K for A/Bs: 2 and 3 within noise of 1, 5 and 6 +3 %, profiles/r03n_ab_strip_width.txt)
+#ifdef SVO_STRIP_K
+constexpr int STRIP_K = SVO_STRIP_K;
+#else
+constexpr int STRIP_K = 1;
+#endif
 
 struct Camera {
     float c2w[16];        // Unity Matrix4x4, column-major
