@@ -258,9 +258,9 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     // index is the identity and node byte offsets fit 32 bits.
     constexpr int STRIDE = TILE;
     const int slots = p.slots;
-    // + the spare slot: a ray that leaves the root takes its parent from there, and
-    // (!GUARD) every lane, finished ones too, fetches nodes[parent] on every trip
-    for (int s = 0; s <= slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
+    // a ray that leaves the root pops the top slot (the root's entry: parent 0) -- every lane,
+    // finished ones too, fetches nodes[parent] on every trip (!GUARD), so it must hold a node
+    for (int s = 0; s < slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
     const int scale_lo = S_MAX - slots;
     const float sexp_lo = __int_as_float((scale_lo - S_MAX + 127) << 23);   // push below scale_lo overflows
     lmask act = LM_OF(true);
@@ -274,7 +274,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
     const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
     // POP: slot address from the exponent field e of float(differing), e = scale + 127
     const uint2 *stk_pop = stk - (127 + scale_lo) * STRIDE;   // indexed by e (never below slot 1)
-    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots);   // leaving the root: the spare slot
+    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots - 1);   // leaving the root: the top slot
     int it = 0;
     uint64_t tl0 = 0;
     if (DIAG) tl0 = __builtin_amdgcn_s_memtime();
@@ -446,8 +446,8 @@ template <int MODE>
 __device__ __forceinline__ void trace_lat(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk) {
     constexpr int STRIDE = TILE;
     const int slots = p.slots;
-    const int nodes_off = (slots + 1) * STRIDE;   // the node half of an entry, in uint2 units
-    for (int s = 0; s <= slots; ++s) {
+    const int nodes_off = slots * STRIDE;   // the node half of an entry, in uint2 units
+    for (int s = 0; s < slots; ++s) {
         stk[s * STRIDE] = make_uint2(0u, 0u);
         stk[nodes_off + s * STRIDE] = make_uint2(0u, 0u);
     }
@@ -461,7 +461,7 @@ __device__ __forceinline__ void trace_lat(const LaunchParams &p, FRay &r, uint2 
     const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
     const uint32_t node_bytes = (uint32_t)nodes_off * (uint32_t)sizeof(uint2);
     const uint2 *stk_pop = stk - (127 + scale_lo) * STRIDE;
-    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots);
+    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots - 1);
     int it = 0;
     asm volatile("" : "+v"(r.parent));
     // the root's node: every ray starts at node 0
@@ -714,9 +714,17 @@ __device__ __forceinline__ int strip_tile(int x, int e, int tiles_x, int tiles_y
 // LAT: the latency form of the loop (trace_lat) for launches that leave wave slots empty;
 // twice the LDS (the stack entries keep their node).
 template <int MODE, bool COUNT, bool FA = false, bool SH = false, bool LAT = false>
-__global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int tiles_x) {
-    extern __shared__ uint2 stk_base[];   // [p.slots + 1][64] (LAT: twice, the nodes behind)
+// SGPR budget: at .sgpr_count 80 (what the compiler chose unbounded) the hardware admitted only 7
+// of these one-wave workgroups per SIMD (wave ids 0-6, 28 per CU in the per-wave HW_ID log,
+// profiles/r03t_*), though the compiler's and the API's occupancy said 8; capped at 72 it needs 70,
+// spills nothing, and 8 waves per SIMD are resident (C3 frame -2 %, profiles/r03t_ab_sgpr_cap.txt).
+#ifndef SVO_NUM_SGPR
+#define SVO_NUM_SGPR 72
+#endif
+__global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))) void render_tile_kernel(LaunchParams p, int tiles_x) {
+    extern __shared__ uint2 stk_base[];   // [p.slots][64] (LAT: twice, the nodes behind)
     const int lane = threadIdx.x;
+    const uint32_t t_entry = !COUNT && p.wave_log ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     const int n_tiles = (int)gridDim.x;
     const int t = p.tile_order ? (int)p.tile_order[blockIdx.x]
                 : p.xcd_remap == 2 ? strip_tile((int)blockIdx.x % 8, (int)blockIdx.x / 8, tiles_x, n_tiles / tiles_x)
@@ -794,7 +802,9 @@ __global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int t
     }
     if (p.tile_cost && (!SH || lane == 0)) p.tile_cost[t] = (uint16_t)min(trips, 65535);
     if (p.wave_log && lane == 0) {   // 100 MHz constant clock, tile, XCC_ID
-        uint32_t *w = p.wave_log + 8 * (size_t)blockIdx.x;
+        uint32_t *w = p.wave_log + WAVE_LOG_WORDS * (size_t)blockIdx.x;
+        w[8] = t_entry;
+        w[10] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID: wave, SIMD, CU, SH, SE
         w[0] = t0;
         w[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         w[2] = (uint32_t)t;   // the tile (band-local, row-major)
@@ -805,6 +815,7 @@ __global__ __launch_bounds__(TILE) void render_tile_kernel(LaunchParams p, int t
         w[7] = dg.pop_trips;
     }
     store_outputs(p.out, out_index(p, lr, gy, x), o);
+    if (p.wave_log && lane == 0) p.wave_log[WAVE_LOG_WORDS * (size_t)blockIdx.x + 9] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------- shadow pass
@@ -1044,7 +1055,7 @@ static size_t lds_pad() {
 template <int MODE, bool COUNT>
 static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
     const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
-    const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2) + lds_pad();   // + the spare slot
+    const size_t lds = (size_t)p.slots * TILE * sizeof(uint2) + lds_pad();
     const dim3 grid((unsigned)(bx * by)), block(TILE);
     if (COUNT)
         hipLaunchKernelGGL((render_tile_kernel<MODE, true>), grid, block, lds, stream, p, bx);
@@ -1481,7 +1492,7 @@ hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
 template <int MODE>
 static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
     const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
-    const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2);
+    const size_t lds = (size_t)p.slots * TILE * sizeof(uint2);
     if (p.fetch_all && !p.guard)
         hipLaunchKernelGGL((shadow_tile_kernel<MODE, true>), dim3((unsigned)(bx * by)), dim3(TILE), lds, stream, p, bx);
     else
@@ -1511,7 +1522,7 @@ hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stre
         const uint8_t *base = reinterpret_cast<const uint8_t *>(p.out.hitmask);
         const uint32_t *list = reinterpret_cast<const uint32_t *>(base + L.rgb);
         const uint32_t *cnt = reinterpret_cast<const uint32_t *>(base + L.offsets) + n;
-        const size_t lds = (size_t)(p.slots + 1) * TILE * sizeof(uint2);
+        const size_t lds = (size_t)p.slots * TILE * sizeof(uint2);
         const dim3 grid((unsigned)(((size_t)p.width * (size_t)p.local_rows + TILE - 1) / TILE));
         LaunchParams q = p;
         q.out.hitmask = nullptr;

@@ -596,7 +596,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                         m = std::max(m, (uint32_t)((volatile uint32_t *)q->stats)[2 * x]);
                         t += ((volatile uint32_t *)q->stats)[2 * x + 1];
                     }
-                    const size_t lds = (size_t)(p.slots + 1) * svo::TILE * sizeof(uint2);
+                    const size_t lds = (size_t)p.slots * svo::TILE * sizeof(uint2);
                     const double slots = (double)ctx->num_cus * (double)std::min<size_t>(32, (160 * 1024) / lds);
                     q->lat_cache = m > 0 && (double)t < ctx->lat_ratio * slots * (double)m ? 1 : 0;
                     q->lat_key = q->stats_key;
@@ -620,10 +620,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
             ctx->d_wave_log = nullptr;
             ctx->wave_log_cap = 0;
-            HIP_TRY(hipMalloc(&ctx->d_wave_log, n_wave * 32));
+            HIP_TRY(hipMalloc(&ctx->d_wave_log, n_wave * 4 * svo::WAVE_LOG_WORDS));
             ctx->wave_log_cap = n_wave;
         }
-        HIP_TRY(hipMemsetAsync(ctx->d_wave_log, 0, n_wave * 32, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_wave_log, 0, n_wave * 4 * svo::WAVE_LOG_WORDS, s));
         p.wave_log = ctx->d_wave_log;
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -664,10 +664,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     if (q) HIP_TRY(hipEventRecord(q->done, s));
     if (p.wave_log) {   // blocking dump of the last launch's per-wave record
         HIP_TRY(hipStreamSynchronize(s));
-        std::vector<uint32_t> h(n_wave * 8);
-        HIP_TRY(hipMemcpy(h.data(), ctx->d_wave_log, n_wave * 32, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> h(n_wave * svo::WAVE_LOG_WORDS);
+        HIP_TRY(hipMemcpy(h.data(), ctx->d_wave_log, h.size() * 4, hipMemcpyDeviceToHost));
         if (FILE *f = std::fopen(log_path, "wb")) {
-            std::fwrite(h.data(), 32, n_wave, f);
+            std::fwrite(h.data(), 4 * svo::WAVE_LOG_WORDS, n_wave, f);
             std::fclose(f);
         }
     }

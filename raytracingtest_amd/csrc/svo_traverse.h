@@ -19,6 +19,7 @@ constexpr int S_MAX = 23;          // NVIDIASVO.compute:2
 constexpr int MAX_ITERS = 65536;   // safety net, identical in oracle/svo_oracle.c
 constexpr int TILE = 64;           // one wave64 = one 8x8 pixel tile
 constexpr int MAX_PARTS = 64;      // band parts one assemble launch reads (devices / ranks)
+constexpr int WAVE_LOG_WORDS = 12;   // per-wave record of the SVO_WAVE_LOG diagnostics
 constexpr int MAX_CYCLE = 256;     // bands per cycle of a weighted band deal (svo_band.cycle)
 // XCD column strips are STRIP_K tile columns wide (svo_kernel.hip strip_col; compile-time knob
 // -DSVO_STRIP_K for A/Bs: 2 and 3 within noise of 1, 5 and 6 +3 %, profiles/r03n_ab_strip_width.txt)
@@ -77,8 +78,9 @@ struct LaunchParams {
     int xcd_remap;        // 2: interleaved XCD column strips, 0: raster
     int shadows;          // one shadow ray per primary hit: 1 = second pass (needs hits), 2 = fused into the primary
                           // launch, 3 = second pass over the compacted hit list (needs hits + out.hitmask scratch)
-    uint32_t *wave_log;   // diagnostics (env SVO_WAVE_LOG): per wave {t0, t1, HW_ID, XCC_ID | trips << 8,
-                          //   loop cycles, fetch-wait cycles, fetch trips, pop trips} (instrumented loop)
+    uint32_t *wave_log;   // diagnostics (env SVO_WAVE_LOG): per wave {t0, t1, tile, XCC_ID | trips << 8,
+                          //   loop cycles, push-only | advance-only trips << 16, fetch trips, pop trips,
+                          //   wave entry, wave exit (after its stores), 2 spare} (WAVE_LOG_WORDS)
     // Cost-ordered dispatch: block b traces 8x8 tile tile_order[b] (null = b)
     // and records its wave trip count in tile_cost.
     const uint32_t *tile_order;   // n_tiles entries + 36 class boundaries

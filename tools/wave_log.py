@@ -14,6 +14,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORDS = 12   # svo_traverse.h WAVE_LOG_WORDS
 sys.path.insert(0, ROOT)
 
 
@@ -48,7 +49,7 @@ def main():
         for _ in range(3):
             rm.render_device(W, H, rgba.data_ptr(), hits.data_ptr(), stack_mode=mode)
         rm.synchronize()
-        full = np.fromfile(args.out, np.uint32).reshape(-1, 8)
+        full = np.fromfile(args.out, np.uint32).reshape(-1, WORDS)
         k = int(np.argmax(full[:, 3] >> 8))
         args.tile_row = int(full[k, 2]) // ((W + 7) // 8)
         print(f"heaviest tile {int(full[k, 2])}: {int(full[k, 3] >> 8)} trips, tile row {args.tile_row}")
@@ -66,7 +67,7 @@ def main():
         b.record(s)
     torch.cuda.synchronize()
     print(f"uninstrumented launch: {np.median([a.elapsed_time(b) for a, b in evs]) * 1e3:.1f} us (median of 10)")
-    log = np.fromfile(args.out, np.uint32).reshape(-1, 8)
+    log = np.fromfile(args.out, np.uint32).reshape(-1, WORDS)
     log = log[(log[:, 0] != 0) | (log[:, 1] != 0)]
     t0 = log[:, 0].astype(np.int64)
     t1 = log[:, 1].astype(np.int64)
@@ -115,6 +116,44 @@ def main():
         print(f"{name}: cycles/trip {loop_c[m].sum() / tr:.0f}, fetching trips {ft[m].sum() / tr:.2f},"
               f" popping trips {pt[m].sum() / tr:.2f}, push-only trips {push_only[m].sum() / tr:.2f},"
               f" advance-only trips {adv_only[m].sum() / tr:.2f}")
+    # the whole wave (entry .. its stores issued) against the traced loop
+    te = log[:, 8].astype(np.int64)
+    tx = log[:, 9].astype(np.int64)
+    ok = (te != 0) & (tx != 0)
+    if ok.any():
+        te = np.where(te > log[:, 0], te - (1 << 32), te) - base
+        tx = np.where(tx < log[:, 1], tx + (1 << 32), tx) - base
+        setup = (t0 - te)[ok] * 10e-3
+        rec = (tx - t1)[ok] * 10e-3
+        whole = (tx - te)[ok] * 10e-3
+        q = [0, 10, 50, 90, 99, 100]
+        print("setup us (entry -> loop)      min/p10/p50/p90/p99/max", np.round(np.percentile(setup, q), 2))
+        print("record us (loop -> stores)    min/p10/p50/p90/p99/max", np.round(np.percentile(rec, q), 2))
+        print(f"whole waves: sum {whole.sum():.0f} us -> mean resident {whole.sum() / ((tx.max() - te.min()) * 10e-3):.0f};"
+              f" setup {setup.sum() / whole.sum():.1%}, record {rec.sum() / whole.sum():.1%} of wave time;"
+              f" span {(tx.max() - te.min()) * 10e-3:.1f} us")
+        nb = 20
+        lo, hi = te[ok].min(), tx[ok].max()
+        edges = np.linspace(lo, hi, nb + 1)
+        res = [np.clip(np.minimum(tx[ok], b) - np.maximum(te[ok], a), 0, None).sum() / (b - a)
+               for a, b in zip(edges[:-1], edges[1:])]
+        print("resident whole waves per 5% of span:", " ".join(f"{int(v)}" for v in res))
+    hw = log[:, 10].astype(np.int64)
+    if hw.any():   # gfx9 HW_ID: wave_id [3:0], simd_id [5:4], cu_id [11:8], sh_id [12], se_id [15:13]
+        cu = ((log[:, 3] & 0xFF).astype(np.int64) << 8) | ((hw >> 13) & 7) << 5 | ((hw >> 12) & 1) << 4 | ((hw >> 8) & 15)
+        ucu, cnt = np.unique(cu, return_counts=True)
+        simd = (hw >> 4) & 3
+        print(f"distinct CUs used {len(ucu)}; waves per CU min/median/max {cnt.min()}/{int(np.median(cnt))}/{cnt.max()};"
+              f" SIMD ids seen {np.unique(simd).tolist()}; wave ids seen {np.unique(hw & 15).tolist()}")
+        if ok.any():   # peak concurrent whole waves on one CU
+            peak = 0
+            for c in ucu[:64]:
+                m = ok & (cu == c)
+                ev = np.concatenate([np.stack([te[m], np.ones(m.sum(), np.int64)], 1),
+                                     np.stack([tx[m], -np.ones(m.sum(), np.int64)], 1)])
+                ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+                peak = max(peak, int(np.cumsum(ev[:, 1]).max()))
+            print(f"peak concurrent waves on one CU (first 64 CUs): {peak}")
     xcc = log[:, 3] & 0xFF
     print("waves per XCC:", np.bincount(xcc, minlength=8)[:8])
     for x in range(8):
