@@ -225,6 +225,42 @@ def test_runtime_switches_identical(oracle_mod, monkeypatch, env):
         m.close()
 
 
+@pytest.mark.parametrize("lat", ["0", "1"])
+def test_degenerate_frame_sizes(oracle_mod, monkeypatch, lat):
+    """Frames far from the 8x8 tile grid (one pixel, one row, one column, partial
+    tiles on both edges) in both loop forms, with and without the fused shadow
+    rays, over repeated (cost-ordered) launches: every record equals the oracle's.
+    A zero-sized frame is an argument error, not an empty launch."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("SVO_LAT", lat)
+    svo = build_menger(7)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        for cam in (main_camera(), overview_camera()):
+            for w, h in ((1, 1), (1, 41), (41, 1), (7, 9), (9, 7), (8, 8), (17, 3), (257, 129)):
+                m.UpdateShaderParameters(cam, w, h)
+                for shadows in (False, True):
+                    ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, svo, cam, w, h, 0, shadows=shadows)
+                    m.SetShadowRays(shadows)
+                    for _ in range(2):
+                        rgba, hits = m.Render(w, h)
+                        _compare(hits, rgba, ref_hits, ref_rgba)
+        m.SetShadowRays(False)
+        for w, h in ((0, 8), (8, 0)):
+            with pytest.raises(SvoError):
+                m.Render(w, h)
+        buf = torch.zeros(64 * 24, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        for w, h in ((-1, 8), (8, -1)):
+            with pytest.raises(SvoError):
+                m.render_device(w, h, hits_ptr=buf.data_ptr())
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_shadow_rays_parity(rm, oracle_mod, mode):
     """C3's '+1 shadow ray' pass: occlusion flag and black
