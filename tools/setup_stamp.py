@@ -1,3 +1,8 @@
+"""Setup-phase breakdown of a wave log (tools/wave_log.py --out gpurun_out/wave_log.bin).
+Word 11 of each record is a stamp taken once the wave's tile index is in hand; the committed
+kernel leaves that word 0 -- r03y wrote it from a diagnostic patch of render_tile_kernel
+(an `s_memrealtime` after the tile index, behind p.wave_log), built with tools/ab_lib.sh and
+run through SVO_RT_LIB (profiles/r03y_setup_phase_breakdown.txt)."""
 import numpy as np
 L = np.fromfile("gpurun_out/wave_log.bin", np.uint32).reshape(-1, 12).astype(np.int64)
 entry, tile, loop0, loop1, exitt = L[:, 8], L[:, 11], L[:, 0], L[:, 1], L[:, 9]
