@@ -285,6 +285,8 @@ def main():
                           "whole step on the host clock between synchronizes, like value"}
     host_path = host_path_rates(rm, W, H, args) if world == 1 and args.steps > 0 and args.extras else None
     in_flight = frames_in_flight(rm, W, H, args, dev) if world == 1 and args.steps > 0 and args.extras else None
+    samples = (samples_in_flight(rm, W, H, args, dev, stream)
+               if world == 1 and args.steps > 0 and args.extras and not args.shadows else None)
     poses = None
     if world == 1 and args.extras and args.svo != "menger":
         poses = extra_poses(rm, args, W, H, hits, rgba, sptr, dev)
@@ -386,6 +388,8 @@ def main():
             out["host_path"] = host_path
         if in_flight:
             out["frames_in_flight"] = in_flight
+        if samples:
+            out["samples_in_flight"] = samples
         print(json.dumps(out), flush=True)
     rm.close()
     if world > 1:
@@ -1134,6 +1138,48 @@ def frames_in_flight(rm, W, H, args, dev, n_streams=3):
     torch.cuda.synchronize(dev)
     ms = (time.perf_counter() - t) / args.steps * 1e3
     return {"streams": n_streams, "ms_per_frame": round(ms, 4), "Mrays_per_s": round(W * H / (ms * 1e-3) / 1e6, 2)}
+
+
+def samples_in_flight(rm, W, H, args, dev, stream, sizes=(1, 2, 4, 8)):
+    """Samples in flight on one GPU (svo_render_samples): a step traces S jittered samples
+    of the frame in ONE launch (one wave per sample and 8x8 tile, cost-ordered) and blends
+    them into the accumulation in _currentSample order (RaytracingMaster.cs:35,70-73,
+    AddShader.shader:44-47).  Rate = S x W x H rays per step.  Reported beside `value`
+    (one sample per step, the metric); the N > 1 form is multi_gpu.samples_in_flight."""
+    import torch
+    from raytracingtest_amd.camera import jitter_offsets
+    offs = jitter_offsets(4096)
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+    frame8 = torch.empty(W * H, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    out = {}
+    n = 0
+    for S in sizes:
+        def step():
+            nonlocal n
+            rm.render_samples(W, H, offs[np.arange(n, n + S) % len(offs)], n,
+                              acc.data_ptr(), rgba8=frame8.data_ptr(), stack_mode=args.stack_mode,
+                              stream=stream.cuda_stream)
+            n += S
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t) / args.steps * 1e3
+        rm.set_kernel_timing(True)
+        rm.kernel_time()
+        for _ in range(args.steps):
+            step()
+        kern, _ = rm.kernel_time()
+        rm.set_kernel_timing(False)
+        out[str(S)] = {"ms_per_step": round(ms, 4), "kernel_ms": round(kern, 4),
+                       "Mrays_per_s": round(S * W * H / (ms * 1e-3) / 1e6, 2),
+                       "kernel_Mrays_per_s": round(S * W * H / (kern * 1e-3) / 1e6, 2)}
+    return {"per_samples": out, "outputs": "RGBA32F accumulation (read + written) + display RGBA8 of the blended frame",
+            "note": "S jittered samples per launch, rays = S x W x H per step; primary rays only"}
 
 
 def host_path_rates(rm, W, H, args, n=5):

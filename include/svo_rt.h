@@ -172,6 +172,22 @@ int svo_render_device(svo_ctx *ctx, int width, int height, int stack_mode,
 int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band,
                      const svo_frame *frame, void *stream);
 
+/* Samples in flight -- the reference's progressive frame loop (_PixelOffset = (Random.value,
+ * Random.value) per frame, RaytracingMaster.cs:35; the AddShader blend with _Sample =
+ * _currentSample, then _currentSample++, :70-73, AddShader.shader:44-47), several frames'
+ * samples in ONE launch: trace n_samples (1..8) jittered samples of the frame (or of `band`'s
+ * rows) -- sample k with _PixelOffset (px_offsets[2k], px_offsets[2k + 1]), the context's
+ * camera otherwise -- and blend them in order into d_accum (RGBA32F, band or frame layout as
+ * `layout`), sample k with _Sample = first_sample + k.  The blend is svo_accumulate's
+ * arithmetic: d_accum ends bit-identical to n_samples single-sample renders each followed by
+ * svo_accumulate.  d_rgba8 / d_rgb8 (nullable): the blended pixels' display RGBA8 words /
+ * 3-byte RGB (a split frame's band payload).  Primary rays only; one device (pass a member
+ * of a multi-device context).  Asynchronous.  One launch holds n_samples waves per 8x8 tile,
+ * so a small band's heaviest wave no longer drains alone. */
+int svo_render_samples(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band, int n_samples,
+                       const float *px_offsets, uint32_t first_sample, float *d_accum, uint32_t *d_rgba8,
+                       uint8_t *d_rgb8, int layout, void *stream);
+
 /* Rebuild a split frame on this context's device from its band parts: part m
  * holds the rows of rank m of the deal `deal` (band_count == n_parts; band_rank
  * ignored; round-robin: bands b with b % n_parts == m), band layout, as
@@ -237,6 +253,12 @@ int svo_kernel_time(svo_ctx *ctx, double *mean_ms, uint64_t *launches);
  * svo_get_member gives one device's own figure. */
 enum { SVO_STAGE_KERNEL = 0, SVO_STAGE_ASSEMBLE = 1 };
 int svo_stage_time(svo_ctx *ctx, int stage, double *mean_ms, uint64_t *launches);
+/* Every recorded launch's duration of a stage, in launch order (the first `cap`
+ * into ms_out; *launches = how many were recorded), then forgets them like
+ * svo_stage_time.  A multi-device context returns devices[0]'s launches and drops
+ * the other members' records.  For hosts that watch frame-to-frame variation
+ * (a moving camera renders every frame at a new view). */
+int svo_stage_times(svo_ctx *ctx, int stage, float *ms_out, size_t cap, size_t *launches);
 
 /* ~ Graphics.Blit(Result, destination, AddMaterial) with _Sample = `sample`
  * (RaytracingMaster.cs:70-73, AddShader.shader:10,44-47): progressive

@@ -27,14 +27,14 @@ assert HIT_DTYPE.itemsize == 24
 COMPACT_DTYPE = np.dtype([("parent", "<u4"), ("meta", "<u4"), ("t", "<f4")])   # svo_hit_compact
 assert COMPACT_DTYPE.itemsize == 12
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
            "svo_destroy", "svo_last_error", "svo_abi_version", "svo_set_options", "svo_accumulate",
            "svo_kernel_time", "svo_create_multi", "svo_num_devices", "svo_get_member", "svo_render_frame",
            "svo_assemble_frame", "svo_stage_time", "svo_render_progressive", "svo_set_band_deal",
-           "svo_pack_hits", "svo_get_member_link")
+           "svo_pack_hits", "svo_get_member_link", "svo_stage_times", "svo_render_samples")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
@@ -54,6 +54,7 @@ def sparse_part_bytes(n_tiles, n_px):
     the scan's scratch tail)."""
     return ((sparse_head_bytes(n_tiles) + 3 * n_px + 3) & ~3) + 4 * n_tiles + 4 * ((n_tiles + 1023) // 1024)
 STAGE_KERNEL, STAGE_ASSEMBLE = 0, 1
+MAX_SAMPLES = 8   # svo_render_samples: jittered samples per launch
 
 
 class SvoBand(ctypes.Structure):
@@ -125,6 +126,9 @@ def lib():
         "svo_assemble_frame": [vp, i, i, ctypes.POINTER(SvoBand), i, ctypes.POINTER(vp), i, i,
                                ctypes.POINTER(SvoFrame), vp],
         "svo_stage_time": [vp, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)],
+        "svo_stage_times": [vp, i, ctypes.POINTER(f), sz, ctypes.POINTER(sz)],
+        "svo_render_samples": [vp, i, i, i, ctypes.POINTER(SvoBand), i, ctypes.POINTER(f), ctypes.c_uint32, vp, vp, vp,
+                               i, vp],
         "svo_render_progressive": [vp, i, i, i, ctypes.c_uint32, vp, vp],
         "svo_set_band_deal": [vp, i, ctypes.POINTER(ctypes.c_uint8)],
         "svo_pack_hits": [vp, i, i, ctypes.POINTER(SvoBand), vp, vp, vp],

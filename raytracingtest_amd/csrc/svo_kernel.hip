@@ -818,6 +818,90 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
     if (p.wave_log && lane == 0) p.wave_log[WAVE_LOG_WORDS * (size_t)blockIdx.x + 9] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 }
 
+// ------------------------------------------------------------- samples in flight
+// svo_render_samples: the reference's frame loop is a stream of independent jittered samples,
+// each blended into the display target (_PixelOffset = (Random.value, Random.value) per frame,
+// RaytracingMaster.cs:35; _Sample blend and _currentSample++, :70-73, AddShader.shader:44-47).
+// One launch traces S of them: workgroup = 8x8 tile (cost-ordered like render_tile_kernel),
+// wave k = sample k.  A launch then holds S times the waves behind each heavy tile, so the
+// heaviest wave -- which bounds a one-sample launch of a small band -- is
+// overlapped by the other samples' work instead of draining alone.  After tracing, each wave
+// parks its colour in its own (dead) stack region, and wave 0 blends the S colours into the
+// accumulation in sample order with accumulate_kernel's arithmetic (bit-identical to S
+// consecutive svo_accumulate calls), then stores the display words.
+template <int MODE, bool FA>
+__global__ __launch_bounds__(TILE * MAX_SAMPLES) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR)))
+void render_samples_kernel(LaunchParams p, int tiles_x) {
+    extern __shared__ uint2 stk_base[];   // [sample][p.slots][64]
+    const int lane = threadIdx.x & (TILE - 1);
+    const int k = threadIdx.x / TILE;     // this wave's sample
+    const int n_tiles = (int)gridDim.x;
+    const int t = p.tile_order ? (int)p.tile_order[blockIdx.x]
+                : p.xcd_remap == 2 ? strip_tile((int)blockIdx.x % 8, (int)blockIdx.x / 8, tiles_x, n_tiles / tiles_x)
+                                   : (int)blockIdx.x;
+    const int bx = t % tiles_x, by = t / tiles_x;
+    const int x = bx * 8 + (lane & 7);
+    const int lr = by * 8 + (lane >> 3);
+    // every wave of the workgroup covers the same pixels: a lane out of the frame leaves in all
+    // of them, so the barrier below sees the same lanes from each wave
+    if (x >= p.width || lr >= p.local_rows) return;
+    if (p.tile_order && p.prio) {
+        const uint32_t n = gridDim.x;
+        const bool strips = p.xcd_remap == 2;
+        const uint32_t b = strips ? blockIdx.x / 8 : blockIdx.x;
+        const uint32_t *bound = strips ? p.tile_order + n + 4 + 4 * (blockIdx.x % 8) : p.tile_order + n;
+        if (b < bound[0]) __builtin_amdgcn_s_setprio(3);
+        else if (b < bound[1]) __builtin_amdgcn_s_setprio(2);
+        else if (b < bound[2]) __builtin_amdgcn_s_setprio(1);
+    }
+    const int gy = global_row(p, lr);
+    Ray r;
+    {
+        Camera cam = p.cam;
+        cam.px_off[0] = p.sample_off[k][0];
+        cam.px_off[1] = p.sample_off[k][1];
+        float org[3], dir[3];
+        camera_ray(cam, p.width, p.height, x, gy, org, dir);
+        setup_ray(org, dir, r);
+    }
+    const size_t region = (size_t)max(p.slots, 2) * TILE;   // >= 64 float4: the colours below
+    uint2 *stk = stk_base + (size_t)k * region + lane;
+    FRay f;
+    to_fray(r, f);
+    if (p.guard) trace_lean<MODE, true>(p, f, stk);
+    else trace_lean<MODE, false, false, FA>(p, f, stk);
+    from_fray(f, r);
+    Record o;
+    record(p, r, x, gy, o);   // p.out.rgba is set (the accumulation), so the hit is shaded
+    if (k == 0 && lane == 0 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);
+    // the colour into this wave's own stack region (dead now; 16 B per lane <= the stack's share)
+    float4 *col = reinterpret_cast<float4 *>(stk_base + (size_t)k * region);
+    col[lane] = make_float4(o.rgb[0], o.rgb[1], o.rgb[2], 1.0f);
+    __syncthreads();
+    if (k != 0) return;
+    const size_t i = out_index(p, lr, gy, x);
+    float4 d = p.accum[i];
+    for (int j = 0; j < p.samples; ++j) {   // accumulate_kernel's blend, sample j after sample j - 1
+        const float4 c = reinterpret_cast<const float4 *>(stk_base + (size_t)j * region)[lane];
+        const float a = p.blend_a[j], b = p.blend_b[j];
+        d.x = c.x * a + d.x * b;
+        d.y = c.y * a + d.y * b;
+        d.z = c.z * a + d.z * b;
+        d.w = a * a + d.w * b;
+    }
+    p.accum[i] = d;
+    if (p.accum8 || p.accum_rgb8) {
+        const uint32_t w = pack_rgba8(d.x, d.y, d.z);
+        if (p.accum8) __builtin_nontemporal_store(w, p.accum8 + i);
+        if (p.accum_rgb8) {
+            uint8_t *c = p.accum_rgb8 + 3 * i;
+            c[0] = (uint8_t)w;
+            c[1] = (uint8_t)(w >> 8);
+            c[2] = (uint8_t)(w >> 16);
+        }
+    }
+}
+
 // ------------------------------------------------------------- shadow pass
 // Two-pass form (env SVO_FUSED_SHADOWS=0): one shadow ray per primary hit, read
 // back from the primary pass's records (svo_hit or compact); an occluded pixel
@@ -1057,6 +1141,15 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
     const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
     const size_t lds = (size_t)p.slots * TILE * sizeof(uint2) + lds_pad();
     const dim3 grid((unsigned)(bx * by)), block(TILE);
+    if (!COUNT && p.samples > 0) {   // samples in flight: S waves per tile, S stacks (>= 1 KB each: the colours)
+        const size_t per = (size_t)std::max(p.slots, 2) * TILE * sizeof(uint2);
+        const dim3 sblock((unsigned)(TILE * p.samples));
+        if (p.fetch_all && !p.guard)
+            hipLaunchKernelGGL((render_samples_kernel<MODE, true>), grid, sblock, per * p.samples, stream, p, bx);
+        else
+            hipLaunchKernelGGL((render_samples_kernel<MODE, false>), grid, sblock, per * p.samples, stream, p, bx);
+        return hipGetLastError();
+    }
     if (COUNT)
         hipLaunchKernelGGL((render_tile_kernel<MODE, true>), grid, block, lds, stream, p, bx);
     else if (p.lat)   // latency form (svo_rt.hip launch decides): the stack entries keep their node
@@ -1094,31 +1187,50 @@ __device__ __forceinline__ void order_load(const uint16_t *cost, int chunk, int 
 }
 
 __global__ __launch_bounds__(ORDER_THREADS) void order_tiles_kernel(const uint16_t *__restrict__ cost,
-                                                                    uint32_t *__restrict__ order, int n) {
+                                                                    uint32_t *__restrict__ order, int n,
+                                                                    uint32_t *stats) {
     constexpr int NW = ORDER_THREADS / 64, NC = 4;
-    __shared__ uint32_t red[NW];
+    __shared__ uint32_t red[NW], red_sum[NW];
     __shared__ uint32_t cnt[NC][NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n_chunks = (n + ORDER_CHUNK - 1) / ORDER_CHUNK;
     uint32_t v[ORDER_PER / 2];   // two 16-bit costs per word
     // ---- max cost
-    uint32_t mx = 0;
+    uint32_t mx = 0, sum = 0;
     for (int c = 0; c < n_chunks; ++c) {
         order_load(cost, c, tid, v);
 #pragma unroll
         for (int e = 0; e < ORDER_PER; ++e) {
             const int i = c * ORDER_CHUNK + tid * ORDER_PER + e;
             const uint32_t k = (v[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu;
-            if (i < n) mx = max(mx, k);
+            if (i < n) {
+                mx = max(mx, k);
+                sum += k;
+            }
         }
     }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
-    if (lane == 0) red[wave] = mx;
+    for (int d = 32; d >= 1; d >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+        sum += (uint32_t)__shfl_xor((int)sum, d);
+    }
+    if (lane == 0) {
+        red[wave] = mx;
+        red_sum[wave] = sum;
+    }
     __syncthreads();
     mx = 0;
+    sum = 0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) mx = max(mx, red[w]);
+    for (int w = 0; w < NW; ++w) {
+        mx = max(mx, red[w]);
+        sum += red_sum[w];
+    }
+    // the loop-form statistics (as order_strips_kernel's, all of it under "XCD 0")
+    if (stats && tid < 8) {
+        stats[2 * tid] = tid == 0 ? mx : 0u;
+        stats[2 * tid + 1] = tid == 0 ? sum : 0u;
+    }
     // class of a cost (NC = invalid element)
     auto cls = [mx](uint32_t k) { return 2 * k >= mx ? 0 : 4 * k >= mx ? 1 : 8 * k >= mx ? 2 : 3; };
     // ---- per-wave class counts
@@ -1260,9 +1372,10 @@ hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tile
     return hipGetLastError();
 }
 
-hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream) {
+hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream,
+                              uint32_t *stats) {
     if (n_tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(order_tiles_kernel, dim3(1), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles);
+    hipLaunchKernelGGL(order_tiles_kernel, dim3(1), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, stats);
     return hipGetLastError();
 }
 

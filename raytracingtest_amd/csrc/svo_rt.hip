@@ -99,11 +99,13 @@ struct Sched {
     // view they were measured at
     hipEvent_t stats_ev = nullptr;       // recorded behind the last order build
     bool stats_pending = false;
-    Geo stats_key;                       // geometry / view of the pending build
+    Geo stats_key;                       // geometry / view / render mode of the pending build
     unsigned long long stats_view = 0;
+    int stats_mode = -1;
     int lat_cache = 0;                   // the decision of the last completed build ...
-    Geo lat_key;                         // ... made at this geometry / view (width -1: none)
+    Geo lat_key;                         // ... made at this geometry / view / mode (width -1: none)
     unsigned long long lat_view = 0;
+    int lat_mode = -1;
 };
 
 struct Peer {                       // one per member of a multi-device context (index 0: the display device)
@@ -250,6 +252,7 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         pick->launches = pick->shadow_launches = 0;
         pick->stats_pending = false;
         pick->lat_key = Geo();
+        pick->lat_mode = pick->stats_mode = -1;
     }
     if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
     pick->stream = s;
@@ -458,8 +461,19 @@ svo::Outputs outputs_of(const svo_frame *f) {
     return o;
 }
 
+// svo_render_samples' arguments (launch's optional last parameter)
+struct SampleArgs {
+    int n;
+    const float *offsets;   // 2 n floats
+    uint32_t first;
+    float4 *accum;
+    uint32_t *rgba8;
+    uint8_t *rgb8;
+    int layout;
+};
+
 int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band, svo::Outputs out,
-           hipStream_t stream) {
+           hipStream_t stream, const SampleArgs *sa = nullptr) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
     if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
     if ((size_t)width * (size_t)height > ((size_t)1 << 31)) return fail(SVO_ERR_ARG, "frame larger than 2^31 pixels");
@@ -500,6 +514,23 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.xcd_remap = ctx->xcd_remap;
     if (p.xcd_remap == 2 && ((width + 7) / 8) % (8 * svo::STRIP_K) != 0) p.xcd_remap = 0;
     p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? (ctx->shadow_compact ? 3 : ctx->fused_shadows ? 2 : 1) : 0;
+    if (sa) {   // samples in flight: primary rays only, the blend replaces every other output
+        p.samples = sa->n;
+        for (int k = 0; k < sa->n; ++k) {
+            p.sample_off[k][0] = sa->offsets[2 * k];
+            p.sample_off[k][1] = sa->offsets[2 * k + 1];
+            // launch_accumulate's a and b (host float arithmetic), _Sample = first + k
+            p.blend_a[k] = 1.0f / ((float)(sa->first + (uint32_t)k) + 1.0f);
+            p.blend_b[k] = 1.0f - p.blend_a[k];
+        }
+        p.accum = sa->accum;
+        p.accum8 = sa->rgba8;
+        p.accum_rgb8 = sa->rgb8;
+        std::memset(&p.out, 0, sizeof p.out);
+        p.out.rgba = sa->accum;   // only tells `record` to shade; the samples kernel stores the blend itself
+        p.out.frame_layout = sa->layout == SVO_LAYOUT_FRAME && b.count > 1 ? 1 : 0;
+        p.shadows = 0;
+    }
     if (p.shadows == 3 && out.hitmask) p.shadows = 1;   // the caller's masks are not a list scratch
     if (p.local_rows == 0) return SVO_OK;
     if (out.fetches) p.shadows = 0;
@@ -580,14 +611,19 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // per view: the last frame's costs); once a build for the current view is in flight --
     // the second launch after a move -- the host waits for it (once per view), so a jump to
     // a different pose is never rendered with another pose's choice.
+    // The costs (and so the decision) are keyed on the render mode too: a shadowed launch's
+    // tile costs include its shadow trips.  The wait can block the host for up to a frame,
+    // once per new view (svo_rt.h, svo_render_device).
+    const int mode_now = p.shadows | (stack_mode << 2);
     p.lat = 0;
-    if (!p.guard && p.shadows == 0 && !p.out.fetches && ctx->lat_mode != 0) {
+    if (!p.guard && p.shadows == 0 && !p.out.fetches && !p.samples && ctx->lat_mode != 0) {
         if (ctx->lat_mode == 1) {
             p.lat = 1;
         } else if (q && q->stats && p.tile_order) {
             if (q->stats_pending) {
                 const bool wait = q->stats_key == key && q->stats_view == ctx->view_gen &&
-                                  !(q->lat_key == key && q->lat_view == ctx->view_gen);
+                                  q->stats_mode == mode_now &&
+                                  !(q->lat_key == key && q->lat_view == ctx->view_gen && q->lat_mode == mode_now);
                 const hipError_t st = wait ? hipEventSynchronize(q->stats_ev) : hipEventQuery(q->stats_ev);
                 if (st == hipSuccess) {
                     uint32_t m = 0;
@@ -601,6 +637,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                     q->lat_cache = m > 0 && (double)t < ctx->lat_ratio * slots * (double)m ? 1 : 0;
                     q->lat_key = q->stats_key;
                     q->lat_view = q->stats_view;
+                    q->lat_mode = q->stats_mode;
                     q->stats_pending = false;
                     if (std::getenv("SVO_LAT_DEBUG"))   // diagnostics: the decision and its inputs
                         std::fprintf(stderr, "svo lat: view %llu T %llu M %u slots %.0f -> %s\n", q->lat_view,
@@ -609,7 +646,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                     return fail(SVO_ERR_HIP, std::string("order build event: ") + hipGetErrorString(st));
                 }
             }
-            p.lat = q->lat_key == key ? q->lat_cache : 0;
+            p.lat = q->lat_key == key && q->lat_mode == mode_now ? q->lat_cache : 0;
         }
     }
     const char *log_path = std::getenv("SVO_WAVE_LOG");
@@ -636,23 +673,23 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // refresh: a new geometry, every order_every-th launch, and right after the first launch
     // following a camera move or a change of render mode (that launch still uses the old
     // order -- a permutation of the same tiles, placement only -- and records fresh costs)
-    const int mode_now = p.shadows | (stack_mode << 2);
     const bool refresh = q && p.tile_cost &&
                          (q->order_key != key || q->launches++ % ctx->order_every == 0 ||
                           q->built_view != ctx->view_gen || q->built_mode != mode_now);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
         e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s,
                                                         q->stats)
-                             : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s);
+                             : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s, q->stats);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         q->order_key = key;
         q->built_view = ctx->view_gen;
         q->built_mode = mode_now;
-        if (q->stats_ev && p.xcd_remap == 2) {
+        if (q->stats_ev) {
             HIP_TRY(hipEventRecord(q->stats_ev, s));
             q->stats_pending = true;
             q->stats_key = key;
             q->stats_view = ctx->view_gen;
+            q->stats_mode = mode_now;
         }
     }
     if (q && p.shadow_cost && (q->shadow_key != key || q->shadow_launches++ % ctx->order_every == 0)) {
@@ -911,7 +948,7 @@ int destroy_single(svo_ctx *ctx) {
 
 extern "C" {
 
-int svo_abi_version(void) { return 7; }
+int svo_abi_version(void) { return 8; }
 
 const char *svo_last_error(void) { return g_last_error.c_str(); }
 
@@ -1167,6 +1204,19 @@ int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const 
     return launch(ctx, width, height, stack_mode, band, outputs_of(frame), reinterpret_cast<hipStream_t>(stream));
 }
 
+int svo_render_samples(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band, int n_samples,
+                       const float *px_offsets, uint32_t first_sample, float *d_accum, uint32_t *d_rgba8,
+                       uint8_t *d_rgb8, int layout, void *stream) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (is_multi(ctx)) return fail(SVO_ERR_ARG, "svo_render_samples renders on one device: pass a member (svo_get_member)");
+    if (n_samples < 1 || n_samples > svo::MAX_SAMPLES) return fail(SVO_ERR_ARG, "n_samples must be in [1, 8]");
+    if (!px_offsets || !d_accum) return fail(SVO_ERR_ARG, "null px_offsets or d_accum");
+    if ((uintptr_t)d_accum & 15u) return fail(SVO_ERR_ARG, "d_accum must be 16-byte aligned");
+    if (layout != SVO_LAYOUT_BAND && layout != SVO_LAYOUT_FRAME) return fail(SVO_ERR_ARG, "unknown layout");
+    SampleArgs sa{n_samples, px_offsets, first_sample, reinterpret_cast<float4 *>(d_accum), d_rgba8, d_rgb8, layout};
+    return launch(ctx, width, height, stack_mode, band, svo::Outputs{}, reinterpret_cast<hipStream_t>(stream), &sa);
+}
+
 int svo_assemble_frame(svo_ctx *ctx, int width, int height, const svo_band *deal, int n_parts,
                        const void *const *parts, int part_format, int skip_part, const svo_frame *frame,
                        void *stream) {
@@ -1345,6 +1395,35 @@ int svo_stage_time(svo_ctx *ctx, int stage, double *mean_ms, uint64_t *launches)
 
 int svo_kernel_time(svo_ctx *ctx, double *mean_ms, uint64_t *launches) {
     return svo_stage_time(ctx, STAGE_KERNEL, mean_ms, launches);
+}
+
+int svo_stage_times(svo_ctx *ctx, int stage, float *ms_out, size_t cap, size_t *launches) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (stage < 0 || stage >= N_STAGES) return fail(SVO_ERR_ARG, "unknown stage");
+    if (cap && !ms_out) return fail(SVO_ERR_ARG, "ms_out is null");
+    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    if (is_multi(ctx))   // the other members' records are dropped, so none accumulates
+        for (size_t i = 1; i < ctx->members.size(); ++i) {
+            int rc = svo_stage_time(ctx->members[i], stage, nullptr, nullptr);
+            if (rc) return rc;
+        }
+    HIP_TRY(hipSetDevice(c->device));
+    size_t n = 0;
+    hipError_t err = hipSuccess;
+    for (auto &ev : c->timing_events[stage]) {
+        float ms = 0.0f;
+        if (err == hipSuccess) err = hipEventSynchronize(ev.second);
+        if (err == hipSuccess) err = hipEventElapsedTime(&ms, ev.first, ev.second);
+        if (err == hipSuccess) {
+            if (n < cap) ms_out[n] = ms;
+            ++n;
+        }
+        c->timing_free.push_back(ev);
+    }
+    c->timing_events[stage].clear();
+    if (err != hipSuccess) return fail(SVO_ERR_HIP, std::string("svo_stage_times: ") + hipGetErrorString(err));
+    if (launches) *launches = n;
+    return SVO_OK;
 }
 
 int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device) {

@@ -21,6 +21,7 @@ constexpr int TILE = 64;           // one wave64 = one 8x8 pixel tile
 constexpr int MAX_PARTS = 64;      // band parts one assemble launch reads (devices / ranks)
 constexpr int WAVE_LOG_WORDS = 12;   // per-wave record of the SVO_WAVE_LOG diagnostics
 constexpr int MAX_CYCLE = 256;     // bands per cycle of a weighted band deal (svo_band.cycle)
+constexpr int MAX_SAMPLES = 8;     // jittered samples one svo_render_samples launch traces per tile
 // XCD column strips are STRIP_K tile columns wide (svo_kernel.hip strip_col; compile-time knob
 // -DSVO_STRIP_K for A/Bs: 2 and 3 within noise of 1, 5 and 6 +3 %, profiles/r03n_ab_strip_width.txt)
 #ifdef SVO_STRIP_K
@@ -92,6 +93,16 @@ struct LaunchParams {
     // The same cost-ordered dispatch for the two-pass shadow form (its own costs and order).
     const uint32_t *shadow_order;
     uint16_t *shadow_cost;
+    // Samples in flight (svo_render_samples): samples > 0 traces that many jittered samples of
+    // every tile in ONE launch -- a workgroup per tile, wave k = sample k with pixel offset
+    // sample_off[k] -- and blends them in order into accum (AddShader, _Sample = first + k:
+    // dst = src * blend_a[k] + dst * blend_b[k]), then writes the blended frame's display words.
+    int samples;
+    float sample_off[MAX_SAMPLES][2];
+    float blend_a[MAX_SAMPLES], blend_b[MAX_SAMPLES];
+    float4 *accum;             // RGBA32F accumulation (out_index layout), read and written
+    uint32_t *accum8;          // display RGBA8 of the blended pixels (nullable)
+    uint8_t *accum_rgb8;       // the same as 3-byte RGB, the band payload (nullable)
 };
 
 // Re-interleave the band parts of a split frame on the display device
@@ -122,8 +133,10 @@ struct AssembleParams {
 // (one workgroup, no atomics), followed by the 4 cumulative class sizes
 // (order must hold n_tiles + 4 entries).  Placement only: any order gives
 // identical results.  `cost` must hold order_cost_capacity(n_tiles) entries (the tail
-// beyond n_tiles is read, never used).
-hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream);
+// beyond n_tiles is read, never used).  stats (nullable, 16 words, host-visible): the
+// max [0] and sum [1] of the tiles' costs, [2..15] zero (launch_order_strips' layout).
+hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream,
+                              uint32_t *stats = nullptr);
 size_t order_cost_capacity(int n_tiles);
 // The same per XCD strip (xcd_remap 2): order must hold n_tiles + 36 entries.  stats
 // (nullable, 16 words, host-visible memory): per XCD x the max [2 x] and the sum [2 x + 1]

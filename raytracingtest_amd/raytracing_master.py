@@ -139,6 +139,15 @@ class RaytracingMaster:
         check(_lib.lib().svo_stage_time(self._ctx, int(stage), ctypes.byref(ms), ctypes.byref(n)), "svo_stage_time")
         return ms.value, n.value
 
+    def stage_times(self, stage=_lib.STAGE_KERNEL, cap=1 << 16):
+        """Every timed launch's duration (ms, float32 array in launch order) of a stage
+        since the last read (svo_stage_times)."""
+        out = np.zeros(cap, np.float32)
+        n = ctypes.c_size_t()
+        check(_lib.lib().svo_stage_times(self._ctx, int(stage), out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                         cap, ctypes.byref(n)), "svo_stage_times")
+        return out[:min(n.value, cap)].copy()
+
     def set_band_deal(self, owner=None):
         """Multi-device context: deal band b to member owner[b % len(owner)]
         (distributed.weighted_owner gives fewer bands to devices[0]); None =
@@ -220,6 +229,18 @@ class RaytracingMaster:
         f = _frame(hits, rgba, rgba8, compact, position, voxel, layout, rgb8, hitmask)
         check(_lib.lib().svo_render_frame(self._ctx, width, height, stack_mode, b, ctypes.byref(f), stream),
               "svo_render_frame")
+
+    def render_samples(self, width, height, offsets, first_sample, accum, rgba8=None, rgb8=None, layout=LAYOUT_BAND,
+                       stack_mode=STACK_HLSL, band=None, stream=None):
+        """Samples in flight (svo_render_samples): trace len(offsets) jittered samples
+        (offsets: [S, 2] pixel offsets, S <= 8) in one launch and blend them in order into
+        the device RGBA32F frame `accum` as _Sample = first_sample + k; rgba8 / rgb8 (device
+        pointers, nullable): the blended frame's display words / 3-byte RGB."""
+        off = np.ascontiguousarray(offsets, np.float32).reshape(-1, 2)
+        b = None if band is None else ctypes.byref(band if isinstance(band, _lib.SvoBand) else make_band(band))
+        check(_lib.lib().svo_render_samples(self._ctx, width, height, stack_mode, b, len(off),
+                                            off.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), int(first_sample),
+                                            accum, rgba8, rgb8, layout, stream), "svo_render_samples")
 
     def assemble_frame(self, width, height, parts, part_format, band_rows=None, hits=None, rgba=None, rgba8=None,
                        compact=None, skip_part=-1, stream=None, owner=None, deal=None):

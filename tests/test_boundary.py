@@ -40,7 +40,8 @@ def test_exports_every_declared_symbol(native):
 
 
 def test_abi_version_and_error_text(native):
-    assert native.svo_abi_version() == 7
+    from raytracingtest_amd import _lib
+    assert native.svo_abi_version() == _lib.ABI_VERSION == 8
     assert isinstance(native.svo_last_error(), bytes)
 
 

@@ -881,3 +881,111 @@ def test_render_progressive_resize_restarts(torch, oracle_mod, text_svo):
         assert out.tobytes() == oracle_sample(96, 70).tobytes()
     finally:
         rm.close()
+
+
+def _oracle_accumulated(oracle_mod, svo, cam, w, h, offs, acc=None, first=0):
+    """The oracle's progressive frame: one render per jittered offset, blended in order
+    with orc_accumulate as _Sample = first + k (AddShader.shader:44-47)."""
+    c2w, inv_proj = cam.uniforms(w, h)
+    osvo = oracle_mod.OracleSVO(nodes=svo.to_v2(), attachments=svo.attachments)
+    acc = np.zeros((w * h, 4), np.float32) if acc is None else acc
+    for k, off in enumerate(offs):
+        _, smp, _ = oracle_mod.render(osvo, oracle_mod.make_camera(c2w, inv_proj, tuple(float(v) for v in off),
+                                                                  main_light()), w, h)
+        oracle_mod.accumulate(acc, np.ascontiguousarray(smp, np.float32), first + k)
+    return acc
+
+
+@pytest.mark.parametrize("n_samples", [1, 3, 8])
+def test_render_samples_matches_oracle_accumulate(torch, oracle_mod, n_samples):
+    """Samples in flight (svo_render_samples): S jittered samples traced in one launch
+    (one wave per sample) and blended in order into the accumulation equal the oracle's S
+    renders + orc_accumulate, bit for bit -- also continued from an existing accumulation
+    (_Sample = first + k), with the display words and 3-byte RGB of the blended frame."""
+    from raytracingtest_amd.camera import jitter_offsets
+    svo = build_menger(7)
+    cam = overview_camera()
+    w, h = 203, 150   # neither a multiple of 8: partial tiles
+    offs = jitter_offsets(2 * n_samples)
+    want = _oracle_accumulated(oracle_mod, svo, cam, w, h, offs[:n_samples])
+    rm = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        rm.SetSVOBuffer(svo)
+        rm.UpdateShaderParameters(cam, w, h)
+        acc = torch.zeros(w * h * 4, dtype=torch.float32, device="cuda")
+        b = _bufs(torch, w * h)
+        torch.cuda.synchronize()
+        rm.render_samples(w, h, offs[:n_samples], 0, acc.data_ptr(), rgba8=b["rgba8"].data_ptr(),
+                          rgb8=b["rgb8"].data_ptr())
+        rm.synchronize()
+        assert acc.cpu().numpy().tobytes() == want.tobytes(), "accumulation differs"
+        assert np.array_equal(b["rgba8"].cpu().numpy().view(np.uint32), oracle_mod.pack_rgba8(want))
+        assert np.array_equal(b["rgb8"].cpu().numpy().reshape(-1, 3),
+                              oracle_mod.pack_rgba8(want).view(np.uint8).reshape(-1, 4)[:, :3])
+        # the next S samples continue the accumulation
+        want2 = _oracle_accumulated(oracle_mod, svo, cam, w, h, offs[n_samples:], acc=want.copy(), first=n_samples)
+        rm.render_samples(w, h, offs[n_samples:], n_samples, acc.data_ptr())
+        rm.synchronize()
+        assert acc.cpu().numpy().tobytes() == want2.tobytes(), "continued accumulation differs"
+    finally:
+        rm.close()
+
+
+@pytest.mark.parametrize("world,share", [(2, None), (4, 0.75)])
+def test_render_samples_rank_parts_assemble(torch, oracle_mod, world, share):
+    """The N > 1 samples-in-flight step on one GPU: every 'rank' traces S = 4 samples of
+    its bands into its band accumulation (band layout; the display rank straight into the
+    frame-layout accumulation) and sends the blended 3-byte RGB; svo_assemble_frame
+    rebuilds the display frame, equal to orc_accumulate over the oracle's 4 whole-frame
+    samples, then packed -- bit for bit, twice in a row (the second step continues)."""
+    from raytracingtest_amd.camera import jitter_offsets
+    from raytracingtest_amd.distributed import weighted_owner
+    svo = build_menger(7)
+    cam = overview_camera()
+    w, h = 264, 203
+    S = 4
+    offs = jitter_offsets(2 * S, seed=7)
+    owner = None if share is None else weighted_owner(world, share)
+    deal = (lambda r: (8, r, world)) if owner is None else (lambda r: (8, r, world, owner))
+    rm = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        rm.SetSVOBuffer(svo)
+        rm.UpdateShaderParameters(cam, w, h)
+        acc0 = torch.zeros(w * h * 4, dtype=torch.float32, device="cuda")   # display rank: frame layout
+        frame8 = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+        accs, parts = [None], [None]
+        for r in range(1, world):
+            n = len(band_rows(h, deal(r))) * w
+            accs.append(torch.zeros(max(n, 1) * 4, dtype=torch.float32, device="cuda"))
+            parts.append(torch.zeros(max(n, 1) * 3, dtype=torch.uint8, device="cuda"))
+        torch.cuda.synchronize()
+        want = None
+        for step in range(2):
+            o = offs[step * S:(step + 1) * S]
+            rm.render_samples(w, h, o, step * S, acc0.data_ptr(), rgba8=frame8.data_ptr(), layout=_lib.LAYOUT_FRAME,
+                              band=deal(0))
+            for r in range(1, world):
+                rm.render_samples(w, h, o, step * S, accs[r].data_ptr(), rgb8=parts[r].data_ptr(), band=deal(r))
+            rm.assemble_frame(w, h, [None] + [p.data_ptr() for p in parts[1:]], _lib.PART_RGB8,
+                              rgba8=frame8.data_ptr(), skip_part=0, owner=owner)
+            rm.synchronize()
+            want = _oracle_accumulated(oracle_mod, svo, cam, w, h, o, acc=want, first=step * S)
+            assert np.array_equal(frame8.cpu().numpy().view(np.uint32), oracle_mod.pack_rgba8(want)), f"step {step}"
+    finally:
+        rm.close()
+
+
+def test_render_samples_errors(torch, text_svo):
+    rm = RaytracingMaster(capacity_nodes=1 << 16)
+    try:
+        rm.SetSVOBuffer(text_svo)
+        rm.UpdateShaderParameters(overview_camera(), 64, 64)
+        acc = torch.zeros(64 * 64 * 4, dtype=torch.float32, device="cuda")
+        with pytest.raises(SvoError):
+            rm.render_samples(64, 64, np.zeros((9, 2), np.float32), 0, acc.data_ptr())   # > 8 samples
+        with pytest.raises(SvoError):
+            rm.render_samples(64, 64, np.zeros((0, 2), np.float32), 0, acc.data_ptr())
+        with pytest.raises(SvoError):
+            rm.render_samples(64, 64, np.zeros((2, 2), np.float32), 0, acc.data_ptr() + 4)   # misaligned
+    finally:
+        rm.close()

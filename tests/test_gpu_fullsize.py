@@ -94,8 +94,9 @@ def _self_consistent(hits, rgba, depth):
     assert np.all(rgba[:, 3] == 1.0)
 
 
+# C3: the bench's flyover pose and both SURVEY.md 8(d) poses (overview, Main.unity)
 @pytest.mark.parametrize("name,camera", [("C2", "overview"), ("C3", "flyover"), ("C3", "overview"),
-                                         ("C4", "overview")])
+                                         ("C3", "main"), ("C4", "overview")])
 def test_full_frame_parity(gpu, oracle_mod, name, camera):
     cfg = CONFIGS[name]
     svo = _svo(cfg)
