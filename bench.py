@@ -264,6 +264,21 @@ def main():
         gather = m["gather"] = None
         torch.cuda.synchronize(dev)
 
+    # samples in flight across the ranks: S jittered samples of the same
+    # frame per step, reported beside value (which stays the one-sample strong split)
+    samples_n = None
+    if world > 1 and args.extras and not args.shadows and args.steps > 0:
+        if m["gather"] is not None:
+            m["gather"].release()
+            gather = m["gather"] = None
+        rm.UpdateShaderParameters(cam, W, H)
+        samples_n = {"frame": f"{W}x{H}", "per_samples": [measure_samples(args, rm, W, H, rank, world, dev, stream,
+                                                                          dist, S) for S in (1, 2, 4, 8)],
+                     "outputs": "every rank: RGBA32F accumulation of its rows + the blended band's display words "
+                                "(rank 0) or 3-byte RGB payload (ranks 1..N-1, gathered once per S samples)",
+                     "note": "value is the one-sample strong split; this line traces S jittered samples of the same "
+                             "frame per step (svo_render_samples), rays = S x W x H per step"}
+
     # C3's '+1 shadow ray' (BASELINE.json configs[2]): the same frame with the
     # shadow pass, timed separately on one GPU (reported beside, not as `value`)
     shadow = None
@@ -379,6 +394,7 @@ def main():
                 "display_rank_deal": deal_info,
                 "payload_choice": payload_choice,
                 "assembled_frame_check": frame_check,
+                "samples_in_flight": samples_n,
                 "note": "value overlaps the gather of frame k with the render of frame k+1; render_only_Mrays is "
                         "the frame's rays over the slowest rank's render kernel alone; gather/assemble from a "
                         "serialized pass (events on the gather stream)"}
@@ -865,6 +881,114 @@ class SparseGather(Gather):
                 "payload_bytes": self.payload_bytes}
 
 
+class SamplesGather(Gather):
+    """N > 1 samples in flight: every rank traces S jittered samples of its
+    bands in ONE launch (svo_render_samples, one wave per sample and tile) and blends them
+    into its own band accumulation in _currentSample order (RaytracingMaster.cs:35,70-73,
+    AddShader.shader:44-47).  Rank 0 blends straight into the frame-layout accumulation and
+    the display frame's words; every other rank into its band accumulation plus the 3-byte
+    RGB of the blended band, which moves to rank 0 once per S samples through the Gather
+    pipeline (payload k gathered while step k + 1 renders, assembled behind it).  The
+    display frame after a step = RGBA8 of the frame accumulated over S more samples.  S is
+    a class attribute (samples_gather_class) so weigh_display_rank can rebuild it."""
+    S = 4
+
+    def __init__(self, rm, W, H, rank, world, dev, payload, stream, no_rgba, owner=None):
+        super().__init__(rm, W, H, rank, world, dev, "rgb8", stream, True, owner)
+        from raytracingtest_amd.camera import jitter_offsets
+        torch = self.torch
+        self.offs = jitter_offsets(4096)
+        self.n = 0               # samples blended so far (_currentSample)
+        self.count_at = [0, 0]   # samples in display frame k
+        self.fhits = self.frgba = self.hits = self.rgba = None   # one-sample outputs, unused here
+        px = W * H if rank == 0 else max(self.n_local, 1)
+        self.acc = torch.zeros(px * 4, dtype=torch.float32, device=dev)
+        torch.cuda.synchronize(dev)
+
+    def local_hits(self):
+        raise NotImplementedError("samples in flight write no hit records")
+
+    def render(self, k, stack_mode):
+        offs = self.offs[np.arange(self.n, self.n + self.S) % len(self.offs)]
+        first = self.n
+        self.n += self.S
+        self.count_at[k] = self.n
+        s = self.R.cuda_stream
+        if self.rank == 0:
+            self.rm.render_samples(self.W, self.H, offs, first, self.acc.data_ptr(), rgba8=self.frame8[k].data_ptr(),
+                                   layout=self._lib.LAYOUT_FRAME, stack_mode=stack_mode, band=self.band_c, stream=s)
+        else:
+            if self.used[k]:
+                self.R.wait_event(self.ev_g[k])   # payload k sent
+            self.rm.render_samples(self.W, self.H, offs, first, self.acc.data_ptr(), rgb8=self.send[k].data_ptr(),
+                                   stack_mode=stack_mode, band=self.band_c, stream=s)
+        self.ev_r[k].record(self.R)
+
+    def check_frame(self, stack_mode):
+        """The assembled display frame vs ONE device replaying the same sample sequence
+        over the whole frame (one launch per S samples, no split): RGBA8 words identical."""
+        torch = self.torch
+        self.drain()
+        torch.cuda.synchronize(self.dev)
+        k = self.last
+        n = self.count_at[k]
+        acc = torch.zeros(self.W * self.H * 4, dtype=torch.float32, device=self.dev)
+        whole8 = torch.empty_like(self.frame8[k])
+        torch.cuda.synchronize(self.dev)
+        for j in range(0, n, self.S):
+            self.rm.render_samples(self.W, self.H, self.offs[np.arange(j, j + self.S) % len(self.offs)], j,
+                                   acc.data_ptr(), rgba8=whole8.data_ptr(), stack_mode=stack_mode,
+                                   stream=self.R.cuda_stream)
+        torch.cuda.synchronize(self.dev)
+        return {"pixels": self.W * self.H, "samples_accumulated": n,
+                "rgba8_mismatches": int((whole8 != self.frame8[k]).sum().item())}
+
+
+def samples_gather_class(S):
+    return type(f"SamplesGather{S}", (SamplesGather,), {"S": S})
+
+
+def measure_samples(args, rm, W, H, rank, world, dev, stream, dist, S):
+    """The N > 1 samples-in-flight line for one S: weighted deal calibrated as for the
+    one-sample line, K pipelined steps between barriers (max over ranks), the render
+    kernel's mean (library events, max over ranks) and the assembled-frame check."""
+    import torch
+    g = samples_gather_class(S)(rm, W, H, rank, world, dev, "rgb8", stream, True)
+    g, info = weigh_display_rank(g, args, rm, dist, dev)
+    for _ in range(max(1, args.warmup)):
+        g.step(args.stack_mode)
+    g.drain()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.step(args.stack_mode)
+    g.drain()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    rm.set_kernel_timing(True)
+    rm.kernel_time()
+    for _ in range(args.steps):
+        g.step(args.stack_mode)
+    g.drain()
+    kern, _ = rm.kernel_time()
+    rm.set_kernel_timing(False)
+    torch.cuda.synchronize(dev)
+    check = g.check_frame(args.stack_mode) if rank == 0 else None
+    t = torch.tensor([elapsed, kern], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per_rank = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+    dist.all_gather(per_rank, torch.tensor([kern], dtype=torch.float64, device=dev))
+    g.release()
+    ms = float(t[0]) / args.steps * 1e3
+    return {"S": S, "ms_per_step": round(ms, 4), "Mrays_per_s": round(S * W * H / (ms * 1e-3) / 1e6, 2),
+            "rays_per_step": S * W * H, "kernel_ms_max_rank": round(float(t[1]), 4),
+            "per_rank_kernel_ms": [round(float(x[0]), 4) for x in per_rank],
+            "display_rank_deal": info, "assembled_frame_check": check}
+
+
 def choose_payload(args, rm, W, H, rank, world, dev, stream, dist, steps=20):
     """The N > 1 gather of the run: the payload --payload names, or with `auto`
     the faster of rgb8 and sparse.  Each candidate gets its own weighted deal
@@ -1188,15 +1312,23 @@ def host_path_rates(rm, W, H, args, n=5):
     and svo_render_progressive (sample rendered and accumulated on the GPU, the
     display RGBA8 frame to the host, 4 B/px) -- what the Unity host pays per frame."""
     out = {}
-    for name, fn in (("svo_render_rgba32f_hits", lambda: rm.Render(W, H, stack_mode=args.stack_mode)),
-                     ("svo_render_progressive_rgba8", lambda: rm.RenderProgressive(W, H, stack_mode=args.stack_mode))):
+    for name, fn, k in (("svo_render_rgba32f_hits", lambda: rm.Render(W, H, stack_mode=args.stack_mode), n),
+                        ("svo_render_progressive_rgba8", lambda: rm.RenderProgressive(W, H, stack_mode=args.stack_mode),
+                         n),
+                        # the pipelined entry point: a pointer to the previous frame in pinned memory
+                        # (copy=False: what LoadRawTextureData receives), D2H overlapping the next render
+                        ("svo_render_progressive_async_rgba8",
+                         lambda: rm.RenderProgressiveAsync(W, H, stack_mode=args.stack_mode, copy=False), 50)):
+        fn()
         fn()
         t = time.perf_counter()
-        for _ in range(n):
+        for _ in range(k):
             fn()
-        ms = (time.perf_counter() - t) / n * 1e3
+        ms = (time.perf_counter() - t) / k * 1e3
         out[name] = {"ms_per_frame": round(ms, 3), "Mrays_per_s": round(W * H / (ms * 1e-3) / 1e6, 1),
-                     "host_bytes_per_frame": W * H * (40 if name.startswith("svo_render_rgba") else 4)}
+                     "host_bytes_per_frame": W * H * (40 if name.startswith("svo_render_rgba") else 4), "frames": k}
+    out["svo_render_progressive_async_rgba8"]["note"] = ("each call returns the previous frame's pinned RGBA8 words; "
+                                                         "the caller's own copy of them is not included")
     return out
 
 

@@ -163,7 +163,13 @@ int svo_render(svo_ctx *ctx, int width, int height, int stack_mode,
 /* Device-resident variant for hosts that keep the frame in HBM: d_rgba /
  * d_hits are device pointers on this context's device (either may be NULL),
  * `band` selects this rank's rows (NULL = all), `stream` is a hipStream_t
- * (NULL = the context's own stream).  Asynchronous: returns after enqueue. */
+ * (NULL = the context's own stream).  Asynchronous: returns after enqueue --
+ * with one exception: the automatic loop-form choice (SVO_LAT
+ * unset) waits, once per new static view (the second render after a camera move),
+ * for the dispatch-order build of the first one, i.e. for up to one frame of
+ * already-enqueued work on that stream.  A caller whose stream waits on something
+ * the host signals only after this call returns must set SVO_LAT=0 or 1.  The same
+ * holds for svo_render_frame and the renders of svo_render. */
 int svo_render_device(svo_ctx *ctx, int width, int height, int stack_mode,
                       const svo_band *band, void *d_rgba, void *d_hits, void *stream);
 
@@ -284,6 +290,21 @@ int svo_accumulate(svo_ctx *ctx, void *d_accum, const void *d_sample, size_t n_p
  * accumulates on devices[0].  Blocking. */
 int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, uint32_t sample,
                            uint32_t *rgba8_out, float *rgba_out);
+
+/* svo_render_progressive for a host that displays every frame (Unity:
+ * Texture2D.LoadRawTextureData(IntPtr, int) on the returned pointer, then Apply):
+ * enqueue one sample -- render, blend with _Sample = `sample`, pack the accumulated
+ * frame to display RGBA8 (the same words as svo_render_progressive's rgba8_out) --
+ * and its copy into plugin-owned pinned host memory on a copy stream, then return in
+ * *frame_out the PREVIOUS call's frame (NULL on the first call after creation or a
+ * size change), waiting only for that frame's copy.  So the D2H of frame k overlaps
+ * the render of frame k + 1, and the host never waits for the frame it just asked for.
+ * A returned pointer (W * H uint32 words) stays valid until the call after next; the
+ * plugin owns it.  svo_progressive_last returns the most recent frame, waiting for its
+ * copy (the end of a sequence).  The blocking svo_render_progressive stays available. */
+int svo_render_progressive_async(svo_ctx *ctx, int width, int height, int stack_mode, uint32_t sample,
+                                 const uint32_t **frame_out);
+int svo_progressive_last(svo_ctx *ctx, const uint32_t **frame_out);
 
 /* Information about the uploaded pool. */
 int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device);

@@ -34,7 +34,8 @@ EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera"
            "svo_destroy", "svo_last_error", "svo_abi_version", "svo_set_options", "svo_accumulate",
            "svo_kernel_time", "svo_create_multi", "svo_num_devices", "svo_get_member", "svo_render_frame",
            "svo_assemble_frame", "svo_stage_time", "svo_render_progressive", "svo_set_band_deal",
-           "svo_pack_hits", "svo_get_member_link", "svo_stage_times", "svo_render_samples")
+           "svo_pack_hits", "svo_get_member_link", "svo_stage_times", "svo_render_samples",
+           "svo_render_progressive_async", "svo_progressive_last")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
@@ -130,6 +131,8 @@ def lib():
         "svo_render_samples": [vp, i, i, i, ctypes.POINTER(SvoBand), i, ctypes.POINTER(f), ctypes.c_uint32, vp, vp, vp,
                                i, vp],
         "svo_render_progressive": [vp, i, i, i, ctypes.c_uint32, vp, vp],
+        "svo_render_progressive_async": [vp, i, i, i, ctypes.c_uint32, ctypes.POINTER(vp)],
+        "svo_progressive_last": [vp, ctypes.POINTER(vp)],
         "svo_set_band_deal": [vp, i, ctypes.POINTER(ctypes.c_uint8)],
         "svo_pack_hits": [vp, i, i, ctypes.POINTER(SvoBand), vp, vp, vp],
         "svo_synchronize": [vp],

@@ -296,7 +296,7 @@ __device__ __forceinline__ void trace_lean(const LaunchParams &p, FRay &r, uint2
         // sky-heavy overview pose).  On the 25 M / 100 M-node pools of C4 / C5 the
         // extra loads cost 6-12 %, so those fetch only the lanes that need a node.
         // Every lane's parent is a valid index: a pool proven to be one tree, and
-        // a ray that left the root holds the cleared spare slot's 0.
+        // a ray that left the root popped the top (root) slot, whose parent is 0.
         constexpr bool ALWAYS = !GUARD && FETCH_ALL && !COUNT;
         const lmask need = ALWAYS ? ~(lmask)0 : act & ~cached;
         if (ALWAYS || LM_ON(need)) {

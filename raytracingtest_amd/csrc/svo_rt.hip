@@ -147,6 +147,17 @@ struct svo_ctx {
     float4 *d_accum = nullptr;
     uint32_t *d_accum8 = nullptr;
     int accum_w = 0, accum_h = 0;
+    // svo_render_progressive_async: the accumulated frame's RGBA8 words packed into one of
+    // PIN_SLOTS device slots and copied on copy_stream into plugin-owned pinned host memory
+    // (the D2H of frame k overlaps the render of frame k + 1)
+    static constexpr int PIN_SLOTS = 3;
+    uint32_t *h_pin[PIN_SLOTS] = {};
+    uint32_t *d_pin[PIN_SLOTS] = {};
+    hipEvent_t pin_packed[PIN_SLOTS] = {}, pin_copied[PIN_SLOTS] = {};
+    bool pin_used[PIN_SLOTS] = {};
+    hipStream_t copy_stream = nullptr;
+    int pin_w = 0, pin_h = 0, pin_next = 0;
+    unsigned long long pin_frames = 0;   // frames enqueued since the slots were (re)allocated
     int num_cus = 256;
     int xcd_remap = 2;               // env SVO_XCD_REMAP: 2 interleaved column strips (default), 0 raster
     uint32_t options = 0;            // svo_set_options
@@ -375,6 +386,42 @@ int ensure_accum(svo_ctx *ctx, int width, int height, bool *fresh) {
     HIP_TRY(hipMemset(ctx->d_accum, 0, px * sizeof(float4)));   // a fresh render target
     ctx->accum_w = width;
     ctx->accum_h = height;
+    return SVO_OK;
+}
+
+void free_pinned(svo_ctx *ctx) {
+    for (int i = 0; i < svo_ctx::PIN_SLOTS; ++i) {
+        if (ctx->h_pin[i]) hipHostFree(ctx->h_pin[i]);
+        if (ctx->d_pin[i]) hipFree(ctx->d_pin[i]);
+        if (ctx->pin_packed[i]) hipEventDestroy(ctx->pin_packed[i]);
+        if (ctx->pin_copied[i]) hipEventDestroy(ctx->pin_copied[i]);
+        ctx->h_pin[i] = nullptr;
+        ctx->d_pin[i] = nullptr;
+        ctx->pin_packed[i] = ctx->pin_copied[i] = nullptr;
+        ctx->pin_used[i] = false;
+    }
+    ctx->pin_w = ctx->pin_h = 0;
+    ctx->pin_next = 0;
+    ctx->pin_frames = 0;
+}
+
+// The pinned readback slots for a width x height frame (reallocated on a size change: the
+// previous frames' pointers die with them).
+int ensure_pinned(svo_ctx *ctx, int width, int height) {
+    if (ctx->h_pin[0] && ctx->pin_w == width && ctx->pin_h == height) return SVO_OK;
+    if (ctx->copy_stream) HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    free_pinned(ctx);
+    if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    const size_t bytes = (size_t)width * (size_t)height * sizeof(uint32_t);
+    for (int i = 0; i < svo_ctx::PIN_SLOTS; ++i) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_pin[i]), bytes, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&ctx->d_pin[i], bytes));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->pin_packed[i], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->pin_copied[i], hipEventDisableTiming));
+    }
+    ctx->pin_w = width;
+    ctx->pin_h = height;
     return SVO_OK;
 }
 
@@ -928,6 +975,9 @@ int destroy_single(svo_ctx *ctx) {
     if (ctx->d_out_rgba) hipFree(ctx->d_out_rgba);
     if (ctx->d_accum) hipFree(ctx->d_accum);
     if (ctx->d_accum8) hipFree(ctx->d_accum8);
+    if (ctx->copy_stream) hipStreamSynchronize(ctx->copy_stream);
+    free_pinned(ctx);
+    if (ctx->copy_stream) hipStreamDestroy(ctx->copy_stream);
     for (Sched &q : ctx->sched) {
         free_sched(q);
         if (q.done) hipEventDestroy(q.done);
@@ -1306,6 +1356,66 @@ int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, 
     if (rgba_out)
         HIP_TRY(hipMemcpyAsync(rgba_out, c->d_accum, px * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return SVO_OK;
+}
+
+int svo_render_progressive_async(svo_ctx *ctx, int width, int height, int stack_mode, uint32_t sample,
+                                 const uint32_t **frame_out) {
+    if (!ctx || !frame_out) return fail(SVO_ERR_ARG, "null argument");
+    *frame_out = nullptr;
+    if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
+    const size_t px = (size_t)width * (size_t)height;
+    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = ensure_out(c, px);
+    if (rc) return rc;
+    bool fresh = false;
+    rc = ensure_accum(c, width, height, &fresh);
+    if (rc) return rc;
+    if (fresh) sample = 0;   // as svo_render_progressive: a resized target restarts the accumulation
+    rc = ensure_pinned(c, width, height);
+    if (rc) return rc;
+    rc = order_scratch(c, c->stream);
+    if (rc) return rc;
+    svo_frame f{};
+    f.rgba = reinterpret_cast<float *>(c->d_out_rgba);   // this sample's Result
+    f.layout = SVO_LAYOUT_FRAME;
+    rc = is_multi(ctx) ? multi_render(ctx, width, height, stack_mode, &f, c->stream)
+                       : launch(c, width, height, stack_mode, nullptr, outputs_of(&f), c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = svo::launch_accumulate(c->d_accum, reinterpret_cast<const float4 *>(c->d_out_rgba), px, sample,
+                                          c->num_cus, c->stream);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("accumulate launch: ") + hipGetErrorString(e));
+    const int k = c->pin_next;
+    // slot k's previous copy (PIN_SLOTS frames ago) must have read d_pin[k] before the pack overwrites it
+    if (c->pin_used[k]) HIP_TRY(hipStreamWaitEvent(c->stream, c->pin_copied[k], 0));
+    e = svo::launch_pack_rgba8(c->d_accum, c->d_pin[k], px, c->num_cus, c->stream);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("pack launch: ") + hipGetErrorString(e));
+    HIP_TRY(hipEventRecord(c->pin_packed[k], c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->copy_stream, c->pin_packed[k], 0));
+    HIP_TRY(hipMemcpyAsync(c->h_pin[k], c->d_pin[k], px * sizeof(uint32_t), hipMemcpyDeviceToHost, c->copy_stream));
+    HIP_TRY(hipEventRecord(c->pin_copied[k], c->copy_stream));
+    c->pin_used[k] = true;
+    c->pin_next = (k + 1) % svo_ctx::PIN_SLOTS;
+    ++c->pin_frames;
+    if (c->pin_frames >= 2) {   // the previous call's frame: wait for its copy only
+        const int prev = (k + svo_ctx::PIN_SLOTS - 1) % svo_ctx::PIN_SLOTS;
+        HIP_TRY(hipEventSynchronize(c->pin_copied[prev]));
+        *frame_out = c->h_pin[prev];
+    }
+    return SVO_OK;
+}
+
+int svo_progressive_last(svo_ctx *ctx, const uint32_t **frame_out) {
+    if (!ctx || !frame_out) return fail(SVO_ERR_ARG, "null argument");
+    *frame_out = nullptr;
+    svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
+    if (c->pin_frames == 0) return SVO_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const int last = (c->pin_next + svo_ctx::PIN_SLOTS - 1) % svo_ctx::PIN_SLOTS;
+    HIP_TRY(hipEventSynchronize(c->pin_copied[last]));
+    *frame_out = c->h_pin[last];
     return SVO_OK;
 }
 

@@ -989,3 +989,51 @@ def test_render_samples_errors(torch, text_svo):
             rm.render_samples(64, 64, np.zeros((2, 2), np.float32), 0, acc.data_ptr() + 4)   # misaligned
     finally:
         rm.close()
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_render_progressive_async_pipelined_frames(torch, oracle_mod, text_svo, devices):
+    """svo_render_progressive_async returns the previous call's frame from the plugin's
+    pinned slots (None first), equal to svo_render_progressive's display words for the
+    same sample sequence; svo_progressive_last gives the newest; a returned view stays
+    valid until the call after next; a size change restarts (None, sample 0)."""
+    from raytracingtest_amd.camera import jitter_offsets
+    W, H = 96, 70
+    cam = overview_camera()
+    offs = jitter_offsets(5, seed=11)
+    c2w, inv_proj = cam.uniforms(W, H)
+    osvo = oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments)
+    acc = np.zeros((W * H, 4), np.float32)
+    want = []
+    for k, off in enumerate(offs):
+        _, smp, _ = oracle_mod.render(osvo, oracle_mod.make_camera(c2w, inv_proj, tuple(float(v) for v in off),
+                                                                  main_light()), W, H)
+        oracle_mod.accumulate(acc, np.ascontiguousarray(smp, np.float32), k)
+        want.append(oracle_mod.pack_rgba8(acc).copy())
+    rm = RaytracingMaster(capacity_nodes=1 << 16, devices=devices)
+    try:
+        rm.SetSVOBuffer(text_svo)
+        views = []
+        for k, off in enumerate(offs):
+            rm.UpdateShaderParameters(cam, W, H, pixel_offset=tuple(float(v) for v in off))
+            if k == 0:
+                assert rm.currentSample == 0
+            got = rm.RenderProgressiveAsync(W, H, copy=False)
+            if k == 0:
+                assert got is None
+            else:
+                views.append((k - 1, got))
+                assert np.array_equal(got.reshape(-1), want[k - 1]), f"frame {k - 1}"
+            if len(views) >= 2:   # the view returned by the previous call is still intact
+                j, v = views[-2]
+                assert np.array_equal(v.reshape(-1), want[j]), f"frame {j} overwritten too early"
+        last = rm.ProgressiveLast(W, H)
+        assert np.array_equal(last.reshape(-1), want[-1])
+        rm.UpdateShaderParameters(cam, 64, 48)   # a new size: fresh accumulation and slots
+        assert rm.RenderProgressiveAsync(64, 48) is None
+        c2, i2 = cam.uniforms(64, 48)
+        _, smp, _ = oracle_mod.render(osvo, oracle_mod.make_camera(c2, i2, (0.5, 0.5), main_light()), 64, 48)
+        assert np.array_equal(rm.ProgressiveLast(64, 48).reshape(-1),
+                              oracle_mod.pack_rgba8(np.ascontiguousarray(smp, np.float32)))
+    finally:
+        rm.close()

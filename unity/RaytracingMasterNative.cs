@@ -33,6 +33,11 @@ public static class SvoNative {
     [DllImport(Lib)] public static extern int svo_render_progressive(IntPtr ctx, int width, int height, int stackMode,
                                                                      uint sample, [Out] uint[] rgba8Out,
                                                                      [Out] float[] rgbaOut);
+    // pipelined readback: returns the previous frame's RGBA8 words in plugin-owned pinned memory
+    // (valid until the call after next), the D2H of this frame overlapping the next render
+    [DllImport(Lib)] public static extern int svo_render_progressive_async(IntPtr ctx, int width, int height,
+                                                                           int stackMode, uint sample,
+                                                                           out IntPtr frame);
     [DllImport(Lib)] public static extern int svo_destroy(IntPtr ctx);
     [DllImport(Lib)] public static extern IntPtr svo_last_error();
 
@@ -103,13 +108,15 @@ public class RaytracingMasterNative : MonoBehaviour {
     }
 
     void CreateContext(UIntPtr capacity) {
+        IntPtr ctx;
         if (gpus <= 1) {
-            SvoNative.Check(SvoNative.svo_create(0, capacity, out _ctx), "svo_create");
+            SvoNative.Check(SvoNative.svo_create(0, capacity, out ctx), "svo_create");
         } else {   // one SVO replica per GPU, bands gathered to GPU 0 over xGMI; every other call is unchanged
             var devices = new int[gpus];
             for (int i = 0; i < gpus; i++) devices[i] = i;
-            SvoNative.Check(SvoNative.svo_create_multi(devices, gpus, capacity, 8, out _ctx), "svo_create_multi");
+            SvoNative.Check(SvoNative.svo_create_multi(devices, gpus, capacity, 8, out ctx), "svo_create_multi");
         }
+        _ctx = ctx;
     }
 
     // RaytracingMaster.cs:90-109 (key R): NaiveCreator.Create(SampleFunctions.functions[sampleType], maxLevel)
@@ -117,12 +124,19 @@ public class RaytracingMasterNative : MonoBehaviour {
     // 256^3 up has child pointers beyond the reference's 16 bits.  The pool replaces the old one (the
     // capacity is the 1 GiB of InitializeSVOBuffer; a bigger pool gets a context of its size).
     void SetSVOBuffer() {
+        // SampleFunctions.functions[5] (Custom2) is null in the reference (SampleFunctions.cs:13-48):
+        // its key R would throw there too; say so instead of calling the builder
+        if ((int)sampleType > (int)SampleFunctions.Type.Custom1) {
+            Debug.LogError("sampleType " + sampleType + " has no sampler in the reference (SampleFunctions.functions)");
+            return;
+        }
         SvoNative.CheckBuild(SvoNative.svob_build_sampler(0, (int)sampleType, maxLevel, out var r), "svob_build_sampler");
         try {
             ulong n = (ulong)r.nNodes;
             if (n > (ulong)(1073741824 / 8)) {   // beyond InitializeSVOBuffer's capacity
                 SvoNative.svo_destroy(_ctx);
-                CreateContext((UIntPtr)n);
+                _ctx = IntPtr.Zero;                // never left pointing at the freed context
+                CreateContext((UIntPtr)n);         // assigns _ctx only once the new context exists
             }
             SvoNative.Check(SvoNative.svo_set_buffer_v2(_ctx, r.nodes, r.nNodes, r.attachments, (UIntPtr)(2 * n),
                                                         UIntPtr.Zero), "svo_set_buffer_v2");
@@ -144,7 +158,12 @@ public class RaytracingMasterNative : MonoBehaviour {
 
     // RaytracingMaster.cs:32-41 + 55-74: the sample is rendered, blended into the plugin's
     // device-resident accumulation frame with _Sample = _currentSample (AddShader.shader:44-47),
-    // and only the accumulated display frame (RGBA8, 4 B/px) crosses PCIe.
+    // and only the accumulated display frame (RGBA8, 4 B/px) crosses PCIe -- into the plugin's
+    // pinned buffer, on a copy stream, while the next frame renders: the call returns the
+    // PREVIOUS frame's words, which LoadRawTextureData copies straight from that pointer (no
+    // managed array).  One frame of display latency; pipelined = false uses the blocking call.
+    public bool pipelined = true;
+
     void OnRenderImage(RenderTexture source, RenderTexture destination) {
         Vector3 l = DirectionalLight.transform.forward;
         SvoNative.Check(SvoNative.svo_set_camera(_ctx, SvoNative.ToArray(_camera.cameraToWorldMatrix),
@@ -157,10 +176,19 @@ public class RaytracingMasterNative : MonoBehaviour {
             _rgba8 = new uint[w * h];
             _currentSample = 0;   // a new render target: the plugin starts a fresh accumulation frame
         }
-        SvoNative.Check(SvoNative.svo_render_progressive(_ctx, w, h, _stackMode, _currentSample, _rgba8, null),
-                        "svo_render_progressive");
-        _frame.SetPixelData(_rgba8, 0);
-        _frame.Apply(false);
+        if (pipelined) {
+            SvoNative.Check(SvoNative.svo_render_progressive_async(_ctx, w, h, _stackMode, _currentSample,
+                                                                   out IntPtr prev), "svo_render_progressive_async");
+            if (prev != IntPtr.Zero) {   // NULL only on the first frame at this size
+                _frame.LoadRawTextureData(prev, w * h * 4);
+                _frame.Apply(false);
+            }
+        } else {
+            SvoNative.Check(SvoNative.svo_render_progressive(_ctx, w, h, _stackMode, _currentSample, _rgba8, null),
+                            "svo_render_progressive");
+            _frame.SetPixelData(_rgba8, 0);
+            _frame.Apply(false);
+        }
         Graphics.Blit(_frame, destination);   // already accumulated: a plain copy, no AddMaterial
         _currentSample++;
     }
