@@ -1195,7 +1195,55 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
         return {"ms": ms, "kern": kern, "asm_ms": asm_ms, "deal": deal, "check": check, "bytes0": bytes0,
                 "F0": F, "rows0": rows0}
 
+    def measure_samples_md(S):
+        """Samples in flight through the multi-device context (svo_render_samples): every
+        member blends S samples of its bands on its own device, the display device
+        assembles the blended frame's words; checked against one device replaying the
+        same sample sequence over the whole frame."""
+        from raytracingtest_amd.camera import jitter_offsets
+        rm.UpdateShaderParameters(cam, W, H)
+        rm.set_band_deal(None)
+        offs = jitter_offsets(4096)
+        acc = torch.zeros(W * H * 4, dtype=torch.float32, device=dev0)
+        frame8 = torch.zeros(W * H, dtype=torch.int32, device=dev0)
+        sync_all()
+        cnt = [0]
+
+        def step():
+            j = cnt[0]
+            rm.render_samples(W, H, offs[np.arange(j, j + S) % len(offs)], j, acc.data_ptr(), rgba8=frame8.data_ptr(),
+                              layout=_lib.LAYOUT_FRAME, stack_mode=args.stack_mode, stream=s.cuda_stream)
+            cnt[0] += S
+
+        for _ in range(max(1, args.warmup)):
+            step()
+        sync_all()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        sync_all()
+        ms = (time.perf_counter() - t) / args.steps * 1e3
+        one = RaytracingMaster(device=dev0.index, capacity_nodes=len(svo))
+        one.SetSVOBuffer(svo)
+        one.UpdateShaderParameters(cam, W, H)
+        acc1 = torch.zeros_like(acc)
+        w8 = torch.zeros_like(frame8)
+        torch.cuda.synchronize(dev0)
+        for j in range(0, cnt[0], S):
+            one.render_samples(W, H, offs[np.arange(j, j + S) % len(offs)], j, acc1.data_ptr(), rgba8=w8.data_ptr(),
+                               stack_mode=args.stack_mode, stream=s.cuda_stream)
+        torch.cuda.synchronize(dev0)
+        bad = int((w8 != frame8).sum().item())
+        one.close()
+        return {"S": S, "ms_per_step": round(ms, 4), "Mrays_per_s": round(S * W * H / (ms * 1e-3) / 1e6, 2),
+                "assembled_frame_check": {"pixels": W * H, "samples_accumulated": cnt[0], "rgba8_mismatches": bad}}
+
     r = measure(W, H)
+    samples_md = None
+    if args.extras:
+        samples_md = {"frame": f"{W}x{H}", "per_samples": [measure_samples_md(S) for S in (1, 2, 4, 8)],
+                      "note": "S jittered samples of the frame per step through the multi-device context "
+                              "(svo_render_samples), rays = S x W x H per step; value is one sample per step"}
     other = None
     if args.extras and args.cfg_gpus == 1:
         other_scaling = "weak" if scaling == "strong" else "strong"
@@ -1231,7 +1279,8 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
                                            "records",
                       "per_device_kernel_ms": [round(k, 4) for k in r["kern"]],
                       "assemble_ms": round(r["asm_ms"], 4), "display_device_deal": r["deal"],
-                      "assembled_frame_check": r["check"], "other_frame": other},
+                      "assembled_frame_check": r["check"], "other_frame": other,
+                      "samples_in_flight": samples_md},
     }), flush=True)
 
 

@@ -187,9 +187,13 @@ int svo_render_frame(svo_ctx *ctx, int width, int height, int stack_mode, const 
  * `layout`), sample k with _Sample = first_sample + k.  The blend is svo_accumulate's
  * arithmetic: d_accum ends bit-identical to n_samples single-sample renders each followed by
  * svo_accumulate.  d_rgba8 / d_rgb8 (nullable): the blended pixels' display RGBA8 words /
- * 3-byte RGB (a split frame's band payload).  Primary rays only; one device (pass a member
- * of a multi-device context).  Asynchronous.  One launch holds n_samples waves per 8x8 tile,
- * so a small band's heaviest wave no longer drains alone. */
+ * 3-byte RGB (a split frame's band payload).  Primary rays only.  Asynchronous.  One launch
+ * holds n_samples waves per 8x8 tile, so a small band's heaviest wave no longer drains alone
+ * (DESIGN.md 6.1).  A multi-device context (band NULL, frame layout) splits the frame over
+ * its devices: each member blends its own rows into a band accumulation it keeps on its own
+ * device (zeroed when the frame size changes), the display device into d_accum's rows of its
+ * bands; the members' blended rows travel as 3-byte RGB and d_rgba8 (required; d_rgb8 must be
+ * NULL) receives the whole frame's display words. */
 int svo_render_samples(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band, int n_samples,
                        const float *px_offsets, uint32_t first_sample, float *d_accum, uint32_t *d_rgba8,
                        uint8_t *d_rgb8, int layout, void *stream);

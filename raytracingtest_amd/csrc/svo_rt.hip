@@ -93,15 +93,20 @@ struct Sched {
     unsigned long long launches = 0, shadow_launches = 0;
     unsigned long long built_view = 0;   // the context's view generation the order was built under
     int built_mode = -1;                 // shadows | stack_mode << 2 of the costs it was built from
-    uint32_t *stats = nullptr;           // host-visible: per XCD max / sum of the tile costs the order kernel saw
-    // loop-form choice (see launch): stats are read only once the order build that wrote
-    // them has completed (stats_ev); the decision they give is kept with the geometry and
-    // view they were measured at
-    hipEvent_t stats_ev = nullptr;       // recorded behind the last order build
-    bool stats_pending = false;
-    Geo stats_key;                       // geometry / view / render mode of the pending build
-    unsigned long long stats_view = 0;
-    int stats_mode = -1;
+    // loop-form choice (see launch): a ring of the last STATS_RING order builds' statistics
+    // (host-visible: per XCD max / sum of the tile costs the order kernel saw, 16 words each),
+    // each read only once its build has completed (its event); the decision it gives is kept
+    // with the geometry, view and render mode it was measured at.  A ring rather than one slot:
+    // while the camera moves every launch rebuilds the order, and one slot would be re-recorded
+    // before the host ever found it complete.
+    static constexpr int STATS_RING = 4;
+    uint32_t *stats = nullptr;           // STATS_RING x 16 words
+    hipEvent_t stats_ev[STATS_RING] = {};
+    bool stats_pending[STATS_RING] = {};
+    Geo stats_key[STATS_RING];
+    unsigned long long stats_view[STATS_RING] = {};
+    int stats_mode[STATS_RING] = {};
+    int stats_head = 0;                  // the slot the next build writes
     int lat_cache = 0;                   // the decision of the last completed build ...
     Geo lat_key;                         // ... made at this geometry / view / mode (width -1: none)
     unsigned long long lat_view = 0;
@@ -114,6 +119,8 @@ struct Peer {                       // one per member of a multi-device context 
     hipEvent_t rendered[2] = {nullptr, nullptr};
     void *dense = nullptr;               // sparse payload: the band's dense RGB before the pack
     size_t dense_cap = 0;
+    float4 *accum = nullptr;             // svo_render_samples: this member's band accumulation (band layout)
+    int accum_w = 0, accum_rows = -1;
     int link = SVO_LINK_SELF;            // how the payload reaches the display device (svo_get_member_link)
     void *local[2] = {nullptr, nullptr}; // SVO_LINK_COPY: the payload's copy on the display device
     size_t local_cap = 0;
@@ -261,9 +268,9 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         if (pick->done) HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
         pick->order_key = pick->shadow_key = Geo();   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
-        pick->stats_pending = false;
+        for (int r = 0; r < Sched::STATS_RING; ++r) pick->stats_pending[r] = false;
         pick->lat_key = Geo();
-        pick->lat_mode = pick->stats_mode = -1;
+        pick->lat_mode = -1;
     }
     if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
     pick->stream = s;
@@ -634,9 +641,11 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             q->cap = (size_t)n_tiles;
         }
         if (!q->stats) {
-            HIP_TRY(hipHostMalloc(&q->stats, 16 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
-            std::memset(q->stats, 0, 16 * sizeof(uint32_t));
-            HIP_TRY(hipEventCreateWithFlags(&q->stats_ev, hipEventDisableTiming));
+            const size_t words = 16 * Sched::STATS_RING;
+            HIP_TRY(hipHostMalloc(&q->stats, words * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+            std::memset(q->stats, 0, words * sizeof(uint32_t));
+            for (int r = 0; r < Sched::STATS_RING; ++r)
+                HIP_TRY(hipEventCreateWithFlags(&q->stats_ev[r], hipEventDisableTiming));
         }
         p.tile_order = q->order_key == key ? q->tile_order : nullptr;
         p.tile_cost = q->tile_cost;
@@ -667,31 +676,38 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         if (ctx->lat_mode == 1) {
             p.lat = 1;
         } else if (q && q->stats && p.tile_order) {
-            if (q->stats_pending) {
-                const bool wait = q->stats_key == key && q->stats_view == ctx->view_gen &&
-                                  q->stats_mode == mode_now &&
-                                  !(q->lat_key == key && q->lat_view == ctx->view_gen && q->lat_mode == mode_now);
-                const hipError_t st = wait ? hipEventSynchronize(q->stats_ev) : hipEventQuery(q->stats_ev);
-                if (st == hipSuccess) {
+            // the newest pending build first: wait for it if it is this view's and this view has
+            // no decision yet (once per view), else take the newest build that has completed
+            // (stream order: then every older one has too) and drop the older ones
+            const bool decided = q->lat_key == key && q->lat_view == ctx->view_gen && q->lat_mode == mode_now;
+            for (int i = 1; i <= Sched::STATS_RING; ++i) {
+                const int r = (q->stats_head + Sched::STATS_RING - i) % Sched::STATS_RING;
+                if (!q->stats_pending[r]) continue;
+                const bool wait = i == 1 && !decided && q->stats_key[r] == key && q->stats_view[r] == ctx->view_gen &&
+                                  q->stats_mode[r] == mode_now;
+                const hipError_t st = wait ? hipEventSynchronize(q->stats_ev[r]) : hipEventQuery(q->stats_ev[r]);
+                if (st == hipErrorNotReady) continue;
+                if (st != hipSuccess) return fail(SVO_ERR_HIP, std::string("order build event: ") + hipGetErrorString(st));
+                for (int j = 0; j < Sched::STATS_RING; ++j) q->stats_pending[j] = false;   // r and everything older
+                if (q->stats_key[r] == key && q->stats_mode[r] == mode_now) {
+                    const volatile uint32_t *st16 = q->stats + 16 * r;
                     uint32_t m = 0;
                     uint64_t t = 0;
                     for (int x = 0; x < 8; ++x) {
-                        m = std::max(m, (uint32_t)((volatile uint32_t *)q->stats)[2 * x]);
-                        t += ((volatile uint32_t *)q->stats)[2 * x + 1];
+                        m = std::max(m, (uint32_t)st16[2 * x]);
+                        t += st16[2 * x + 1];
                     }
                     const size_t lds = (size_t)p.slots * svo::TILE * sizeof(uint2);
                     const double slots = (double)ctx->num_cus * (double)std::min<size_t>(32, (160 * 1024) / lds);
                     q->lat_cache = m > 0 && (double)t < ctx->lat_ratio * slots * (double)m ? 1 : 0;
-                    q->lat_key = q->stats_key;
-                    q->lat_view = q->stats_view;
-                    q->lat_mode = q->stats_mode;
-                    q->stats_pending = false;
+                    q->lat_key = q->stats_key[r];
+                    q->lat_view = q->stats_view[r];
+                    q->lat_mode = q->stats_mode[r];
                     if (std::getenv("SVO_LAT_DEBUG"))   // diagnostics: the decision and its inputs
                         std::fprintf(stderr, "svo lat: view %llu T %llu M %u slots %.0f -> %s\n", q->lat_view,
                                      (unsigned long long)t, m, slots, q->lat_cache ? "latency" : "lean");
-                } else if (st != hipErrorNotReady) {
-                    return fail(SVO_ERR_HIP, std::string("order build event: ") + hipGetErrorString(st));
                 }
+                break;
             }
             p.lat = q->lat_key == key && q->lat_mode == mode_now ? q->lat_cache : 0;
         }
@@ -724,19 +740,21 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                          (q->order_key != key || q->launches++ % ctx->order_every == 0 ||
                           q->built_view != ctx->view_gen || q->built_mode != mode_now);
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
-        e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s,
-                                                        q->stats)
-                             : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s, q->stats);
+        const int r = q->stats_head;
+        uint32_t *st16 = q->stats ? q->stats + 16 * r : nullptr;
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s, st16)
+                             : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s, st16);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         q->order_key = key;
         q->built_view = ctx->view_gen;
         q->built_mode = mode_now;
-        if (q->stats_ev) {
-            HIP_TRY(hipEventRecord(q->stats_ev, s));
-            q->stats_pending = true;
-            q->stats_key = key;
-            q->stats_view = ctx->view_gen;
-            q->stats_mode = mode_now;
+        if (st16) {   // slot r: a build still pending there (ring full) is simply superseded
+            HIP_TRY(hipEventRecord(q->stats_ev[r], s));
+            q->stats_pending[r] = true;
+            q->stats_key[r] = key;
+            q->stats_view[r] = ctx->view_gen;
+            q->stats_mode[r] = mode_now;
+            q->stats_head = (r + 1) % Sched::STATS_RING;
         }
     }
     if (q && p.shadow_cost && (q->shadow_key != key || q->shadow_launches++ % ctx->order_every == 0)) {
@@ -823,7 +841,11 @@ int check_assemble_args(svo_ctx *ctx, int width, int height, int n_parts, int pa
 }
 
 // ------------------------------------------------------ multi-device frame
-int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_frame *frame, hipStream_t stream) {
+// sa (svo_render_samples): every member traces S samples of its bands and blends them into its
+// own band accumulation (the display member into the caller's frame-layout accum); the members'
+// payloads are the blended bands' 3-byte RGB, assembled into the caller's rgba8 frame.
+int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_frame *frame, hipStream_t stream,
+                 const SampleArgs *sa = nullptr) {
     const int n = (int)ctx->members.size();
     svo::Outputs out = outputs_of(frame);
     out.frame_layout = 1;
@@ -833,7 +855,8 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
     // display-only frames travel as 3-byte RGB (the RGBA8 word without its constant alpha), or
     // (SVO_SPARSE_PAYLOAD=1) as sparse parts: tile hit masks + offsets + the hits' RGB, pulled by the
     // assemble kernel with no host round trip (the offsets travel in the part)
-    const int fmt = (out.hits || out.rgba || out.compact) ? SVO_PART_COMPACT
+    const int fmt = sa ? SVO_PART_RGB8
+                    : (out.hits || out.rgba || out.compact) ? SVO_PART_COMPACT
                     : ctx->sparse_payload ? SVO_PART_SPARSE_RGB8 : SVO_PART_RGB8;
     const size_t elem = fmt == SVO_PART_COMPACT ? 12 : 3;
     const int k = ctx->parity;
@@ -842,7 +865,7 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
     hipStream_t s0 = stream ? stream : m0->stream;
     // the display device renders its own bands straight into the caller's frame
     svo_band b0{ctx->band_rows, 0, n, ctx->deal_cycle, ctx->deal_cycle ? ctx->deal_owner : nullptr};
-    int rc = launch(m0, width, height, stack_mode, &b0, out, s0);
+    int rc = launch(m0, width, height, stack_mode, &b0, out, s0, sa);
     if (rc) return rc;
     std::vector<const void *> parts(n, nullptr);
     for (int i = 1; i < n; ++i) {
@@ -881,6 +904,18 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
             HIP_TRY(hipMalloc(&pr.dense, std::max<size_t>((size_t)rows_i * width * 3, 16)));
             pr.dense_cap = (size_t)rows_i * width * 3;
         }
+        if (sa && (pr.accum_w != width || pr.accum_rows != rows_i)) {   // this member's band accumulation
+            HIP_TRY(hipStreamSynchronize(m->stream));
+            if (pr.accum) hipFree(pr.accum);
+            pr.accum = nullptr;
+            pr.accum_w = 0;
+            pr.accum_rows = -1;
+            const size_t abytes = std::max<size_t>((size_t)rows_i * (size_t)width * sizeof(float4), 16);
+            HIP_TRY(hipMalloc(&pr.accum, abytes));
+            HIP_TRY(hipMemsetAsync(pr.accum, 0, abytes, m->stream));   // a fresh render target
+            pr.accum_w = width;
+            pr.accum_rows = rows_i;
+        }
         if (ctx->gathered_used[k]) HIP_TRY(hipStreamWaitEvent(m->stream, ctx->gathered[k], 0));   // payload k is free
         svo::Outputs oi{};
         if (fmt == SVO_PART_COMPACT) {
@@ -891,7 +926,15 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
         } else {
             oi.rgb8 = reinterpret_cast<uint8_t *>(pr.buf[k]);
         }
-        rc = launch(m, width, height, stack_mode, &bi, oi, m->stream);
+        SampleArgs sai{};
+        if (sa) {
+            sai = *sa;
+            sai.accum = pr.accum;
+            sai.rgba8 = nullptr;
+            sai.rgb8 = reinterpret_cast<uint8_t *>(pr.buf[k]);
+            sai.layout = SVO_LAYOUT_BAND;
+        }
+        rc = launch(m, width, height, stack_mode, &bi, oi, m->stream, sa ? &sai : nullptr);
         if (rc) return rc;
         if (fmt == SVO_PART_SPARSE_RGB8) {
             hipError_t e = svo::launch_pack_hits(reinterpret_cast<const uint8_t *>(pr.dense), width, rows_i, pr.buf[k],
@@ -981,7 +1024,8 @@ int destroy_single(svo_ctx *ctx) {
     for (Sched &q : ctx->sched) {
         free_sched(q);
         if (q.done) hipEventDestroy(q.done);
-        if (q.stats_ev) hipEventDestroy(q.stats_ev);
+        for (int r = 0; r < Sched::STATS_RING; ++r)
+            if (q.stats_ev[r]) hipEventDestroy(q.stats_ev[r]);
         if (q.stats) hipHostFree(q.stats);
     }
     for (auto &v : ctx->timing_events)
@@ -1258,12 +1302,21 @@ int svo_render_samples(svo_ctx *ctx, int width, int height, int stack_mode, cons
                        const float *px_offsets, uint32_t first_sample, float *d_accum, uint32_t *d_rgba8,
                        uint8_t *d_rgb8, int layout, void *stream) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
-    if (is_multi(ctx)) return fail(SVO_ERR_ARG, "svo_render_samples renders on one device: pass a member (svo_get_member)");
     if (n_samples < 1 || n_samples > svo::MAX_SAMPLES) return fail(SVO_ERR_ARG, "n_samples must be in [1, 8]");
     if (!px_offsets || !d_accum) return fail(SVO_ERR_ARG, "null px_offsets or d_accum");
     if ((uintptr_t)d_accum & 15u) return fail(SVO_ERR_ARG, "d_accum must be 16-byte aligned");
     if (layout != SVO_LAYOUT_BAND && layout != SVO_LAYOUT_FRAME) return fail(SVO_ERR_ARG, "unknown layout");
     SampleArgs sa{n_samples, px_offsets, first_sample, reinterpret_cast<float4 *>(d_accum), d_rgba8, d_rgb8, layout};
+    if (is_multi(ctx)) {   // the frame split over the members, each blending its own rows on its own device
+        if (band && band->band_count != 1) return fail(SVO_ERR_ARG, "a multi-device context splits the frame itself");
+        if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
+        if (!d_rgba8 || d_rgb8) return fail(SVO_ERR_ARG, "a multi-device context assembles d_rgba8 (d_rgb8 must be NULL)");
+        svo_frame f{};
+        f.rgba8 = d_rgba8;
+        f.layout = SVO_LAYOUT_FRAME;
+        sa.layout = SVO_LAYOUT_FRAME;
+        return multi_render(ctx, width, height, stack_mode, &f, reinterpret_cast<hipStream_t>(stream), &sa);
+    }
     return launch(ctx, width, height, stack_mode, band, svo::Outputs{}, reinterpret_cast<hipStream_t>(stream), &sa);
 }
 
@@ -1590,6 +1643,7 @@ int svo_destroy(svo_ctx *ctx) {
             if (pr.rendered[j]) hipEventDestroy(pr.rendered[j]);
         }
         if (pr.dense) hipFree(pr.dense);
+        if (pr.accum) hipFree(pr.accum);
     }
     if (!ctx->members.empty()) hipSetDevice(ctx->members[0]->device);
     for (size_t i = 1; i < ctx->peers.size(); ++i)

@@ -1037,3 +1037,37 @@ def test_render_progressive_async_pipelined_frames(torch, oracle_mod, text_svo, 
                               oracle_mod.pack_rgba8(np.ascontiguousarray(smp, np.float32)))
     finally:
         rm.close()
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_render_samples_multi_device(torch, oracle_mod, devices):
+    """Samples in flight on a multi-device context (the Unity host driving N GPUs): every
+    member blends S = 4 samples of its bands into its own band accumulation, the display
+    member into the caller's frame, and the assembled display words equal the oracle's
+    accumulation -- over two steps (the members' accumulations persist) and after a size
+    change (fresh, zeroed accumulations)."""
+    from raytracingtest_amd.camera import jitter_offsets
+    svo = build_menger(7)
+    cam = overview_camera()
+    S = 4
+    offs = jitter_offsets(2 * S, seed=3)
+    rm = RaytracingMaster(devices=devices, capacity_nodes=len(svo))
+    try:
+        rm.SetSVOBuffer(svo)
+        for (w, h) in ((200, 136), (96, 64)):
+            rm.UpdateShaderParameters(cam, w, h)
+            acc = torch.zeros(w * h * 4, dtype=torch.float32, device="cuda")
+            frame8 = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            want = None
+            for step in range(2):
+                o = offs[step * S:(step + 1) * S]
+                rm.render_samples(w, h, o, step * S, acc.data_ptr(), rgba8=frame8.data_ptr(), layout=_lib.LAYOUT_FRAME)
+                rm.synchronize()
+                want = _oracle_accumulated(oracle_mod, svo, cam, w, h, o, acc=want, first=step * S)
+                assert np.array_equal(frame8.cpu().numpy().view(np.uint32), oracle_mod.pack_rgba8(want)), \
+                    f"{w}x{h} step {step}"
+        with pytest.raises(SvoError):   # the display words are the multi-device output
+            rm.render_samples(96, 64, offs[:2], 0, acc.data_ptr(), layout=_lib.LAYOUT_FRAME)
+    finally:
+        rm.close()

@@ -9,6 +9,8 @@ import argparse
 import os
 import sys
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ["SVO_LAT_DEBUG"] = "1"
@@ -45,6 +47,21 @@ def main():
         rm.set_kernel_timing(False)
         torch.cuda.synchronize()
         print(f"   {pose}: kernel {ms * 1e3:.1f} us", file=sys.stderr, flush=True)
+    # a moving camera: a new view every launch (the interactive case), submitted without host
+    # syncs; the decisions must keep arriving (a few frames late) instead of freezing
+    from raytracingtest_amd.camera import OVERVIEW_EYE, OVERVIEW_TARGET, overview_camera
+    print("== moving camera: overview eye orbiting, 120 launches, one view each", file=sys.stderr, flush=True)
+    rm.set_kernel_timing(True)
+    rm.kernel_time()
+    for i in range(120):
+        a_ = 0.01 * i
+        eye = (OVERVIEW_EYE[0] + 5.0 * np.sin(a_), OVERVIEW_EYE[1], OVERVIEW_EYE[2] + 5.0 * (1.0 - np.cos(a_)))
+        rm.UpdateShaderParameters(overview_camera(eye, OVERVIEW_TARGET), W, H)
+        rm.render_device(W, H, hits_ptr=h.data_ptr(), rgba_ptr=rg.data_ptr(), stack_mode=mode, stream=s.cuda_stream)
+    t = rm.stage_times()
+    rm.set_kernel_timing(False)
+    print(f"   moving: kernel mean {np.mean(t) * 1e3:.1f} us, first 10 {np.mean(t[:10]) * 1e3:.1f} us, "
+          f"last 60 {np.mean(t[60:]) * 1e3:.1f} us", file=sys.stderr, flush=True)
     rm.close()
 
 
