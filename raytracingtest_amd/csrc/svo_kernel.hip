@@ -880,7 +880,11 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
     __syncthreads();
     if (k != 0) return;
     const size_t i = out_index(p, lr, gy, x);
-    float4 d = p.accum[i];
+    // the accumulation streams through once per launch (33 MB at 1080p): non-temporal both ways,
+    // so it does not evict the node pool from L2 (as the render's output stores, store_outputs)
+    f32x4 *acc = reinterpret_cast<f32x4 *>(p.accum + i);
+    const f32x4 a4 = __builtin_nontemporal_load(acc);
+    float4 d = make_float4(a4[0], a4[1], a4[2], a4[3]);
     for (int j = 0; j < p.samples; ++j) {   // accumulate_kernel's blend, sample j after sample j - 1
         const float4 c = reinterpret_cast<const float4 *>(stk_base + (size_t)j * region)[lane];
         const float a = p.blend_a[j], b = p.blend_b[j];
@@ -889,7 +893,7 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
         d.z = c.z * a + d.z * b;
         d.w = a * a + d.w * b;
     }
-    p.accum[i] = d;
+    __builtin_nontemporal_store(f32x4{d.x, d.y, d.z, d.w}, acc);
     if (p.accum8 || p.accum_rgb8) {
         const uint32_t w = pack_rgba8(d.x, d.y, d.z);
         if (p.accum8) __builtin_nontemporal_store(w, p.accum8 + i);
@@ -1407,6 +1411,29 @@ hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32
     const size_t want = (n_px + 255) / 256;
     const unsigned blocks = (unsigned)std::min<size_t>(want, (size_t)num_cus * 16);
     hipLaunchKernelGGL(accumulate_kernel, dim3(blocks), dim3(256), 0, stream, dst, src, n_px, a, b);
+    return hipGetLastError();
+}
+
+// svo_render_progressive_async (env SVO_PIN_PUSH=1): the packed display words pushed into the
+// plugin's mapped pinned host buffer by a kernel (PCIe writes from every workgroup) instead of
+// one DMA copy; 16 B per lane, grid-stride, non-temporal stores.
+__global__ __launch_bounds__(256) void push_host_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                        size_t n16) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        const uint4 v = src[i];
+        __builtin_nontemporal_store(v.x, &dst[i].x);
+        __builtin_nontemporal_store(v.y, &dst[i].y);
+        __builtin_nontemporal_store(v.z, &dst[i].z);
+        __builtin_nontemporal_store(v.w, &dst[i].w);
+    }
+}
+
+hipError_t launch_push_host(const void *src, void *dst_mapped, size_t bytes, int blocks, hipStream_t stream) {
+    if (bytes == 0) return hipSuccess;
+    const size_t n16 = bytes / 16;   // callers pass multiples of 16 bytes (whole frames of 4-byte words, padded)
+    hipLaunchKernelGGL(push_host_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       reinterpret_cast<const uint4 *>(src), reinterpret_cast<uint4 *>(dst_mapped), n16);
     return hipGetLastError();
 }
 

@@ -164,6 +164,10 @@ struct svo_ctx {
     bool pin_used[PIN_SLOTS] = {};
     hipStream_t copy_stream = nullptr;
     int pin_w = 0, pin_h = 0, pin_next = 0;
+    int pin_push = 0;                    // env SVO_PIN_PUSH: 0 hipMemcpyAsync (DMA), 1 a kernel writes the
+                                         // mapped pinned buffer, 2 the DMA split over two copy streams
+    hipStream_t copy_stream2 = nullptr;
+    hipEvent_t pin_copied2[PIN_SLOTS] = {};
     unsigned long long pin_frames = 0;   // frames enqueued since the slots were (re)allocated
     int num_cus = 256;
     int xcd_remap = 2;               // env SVO_XCD_REMAP: 2 interleaved column strips (default), 0 raster
@@ -402,6 +406,8 @@ void free_pinned(svo_ctx *ctx) {
         if (ctx->d_pin[i]) hipFree(ctx->d_pin[i]);
         if (ctx->pin_packed[i]) hipEventDestroy(ctx->pin_packed[i]);
         if (ctx->pin_copied[i]) hipEventDestroy(ctx->pin_copied[i]);
+        if (ctx->pin_copied2[i]) hipEventDestroy(ctx->pin_copied2[i]);
+        ctx->pin_copied2[i] = nullptr;
         ctx->h_pin[i] = nullptr;
         ctx->d_pin[i] = nullptr;
         ctx->pin_packed[i] = ctx->pin_copied[i] = nullptr;
@@ -417,15 +423,22 @@ void free_pinned(svo_ctx *ctx) {
 int ensure_pinned(svo_ctx *ctx, int width, int height) {
     if (ctx->h_pin[0] && ctx->pin_w == width && ctx->pin_h == height) return SVO_OK;
     if (ctx->copy_stream) HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
+    if (ctx->copy_stream2) HIP_TRY(hipStreamSynchronize(ctx->copy_stream2));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     free_pinned(ctx);
+    if (const char *v = std::getenv("SVO_PIN_PUSH")) ctx->pin_push = std::atoi(v);
     if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
-    const size_t bytes = (size_t)width * (size_t)height * sizeof(uint32_t);
+    if (ctx->pin_push == 2 && !ctx->copy_stream2)
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream2, hipStreamNonBlocking));
+    // 16-byte multiple (the push kernel moves 16 B per lane); the frame is the first W * H words
+    const size_t bytes = ((size_t)width * (size_t)height * sizeof(uint32_t) + 15) & ~(size_t)15;
+    const unsigned host_flags = ctx->pin_push == 1 ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault;
     for (int i = 0; i < svo_ctx::PIN_SLOTS; ++i) {
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_pin[i]), bytes, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_pin[i]), bytes, host_flags));
         HIP_TRY(hipMalloc(&ctx->d_pin[i], bytes));
         HIP_TRY(hipEventCreateWithFlags(&ctx->pin_packed[i], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&ctx->pin_copied[i], hipEventDisableTiming));
+        if (ctx->pin_push == 2) HIP_TRY(hipEventCreateWithFlags(&ctx->pin_copied2[i], hipEventDisableTiming));
     }
     ctx->pin_w = width;
     ctx->pin_h = height;
@@ -1019,8 +1032,10 @@ int destroy_single(svo_ctx *ctx) {
     if (ctx->d_accum) hipFree(ctx->d_accum);
     if (ctx->d_accum8) hipFree(ctx->d_accum8);
     if (ctx->copy_stream) hipStreamSynchronize(ctx->copy_stream);
+    if (ctx->copy_stream2) hipStreamSynchronize(ctx->copy_stream2);
     free_pinned(ctx);
     if (ctx->copy_stream) hipStreamDestroy(ctx->copy_stream);
+    if (ctx->copy_stream2) hipStreamDestroy(ctx->copy_stream2);
     for (Sched &q : ctx->sched) {
         free_sched(q);
         if (q.done) hipEventDestroy(q.done);
@@ -1447,8 +1462,27 @@ int svo_render_progressive_async(svo_ctx *ctx, int width, int height, int stack_
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("pack launch: ") + hipGetErrorString(e));
     HIP_TRY(hipEventRecord(c->pin_packed[k], c->stream));
     HIP_TRY(hipStreamWaitEvent(c->copy_stream, c->pin_packed[k], 0));
-    HIP_TRY(hipMemcpyAsync(c->h_pin[k], c->d_pin[k], px * sizeof(uint32_t), hipMemcpyDeviceToHost, c->copy_stream));
-    HIP_TRY(hipEventRecord(c->pin_copied[k], c->copy_stream));
+    const size_t fbytes = px * sizeof(uint32_t);
+    if (c->pin_push == 1) {   // a kernel writes the mapped pinned buffer over PCIe
+        void *dst = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&dst, c->h_pin[k], 0));
+        e = svo::launch_push_host(c->d_pin[k], dst, (fbytes + 15) & ~(size_t)15, c->num_cus, c->copy_stream);
+        if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("push launch: ") + hipGetErrorString(e));
+        HIP_TRY(hipEventRecord(c->pin_copied[k], c->copy_stream));
+    } else if (c->pin_push == 2) {   // two DMA copies of half the frame each, on two copy streams
+        const size_t half = (fbytes / 2) & ~(size_t)4095;
+        HIP_TRY(hipStreamWaitEvent(c->copy_stream2, c->pin_packed[k], 0));
+        HIP_TRY(hipMemcpyAsync(c->h_pin[k], c->d_pin[k], half, hipMemcpyDeviceToHost, c->copy_stream));
+        HIP_TRY(hipMemcpyAsync(reinterpret_cast<uint8_t *>(c->h_pin[k]) + half,
+                               reinterpret_cast<uint8_t *>(c->d_pin[k]) + half, fbytes - half, hipMemcpyDeviceToHost,
+                               c->copy_stream2));
+        HIP_TRY(hipEventRecord(c->pin_copied2[k], c->copy_stream2));
+        HIP_TRY(hipStreamWaitEvent(c->copy_stream, c->pin_copied2[k], 0));
+        HIP_TRY(hipEventRecord(c->pin_copied[k], c->copy_stream));
+    } else {
+        HIP_TRY(hipMemcpyAsync(c->h_pin[k], c->d_pin[k], fbytes, hipMemcpyDeviceToHost, c->copy_stream));
+        HIP_TRY(hipEventRecord(c->pin_copied[k], c->copy_stream));
+    }
     c->pin_used[k] = true;
     c->pin_next = (k + 1) % svo_ctx::PIN_SLOTS;
     ++c->pin_frames;
