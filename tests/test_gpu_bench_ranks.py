@@ -64,6 +64,13 @@ def test_two_ranks_assemble_the_whole_frame(gpu, payload):
         o = mg["other_frame"]
         assert o["scaling"] == "weak" and o["frame"] != "1920x1080" and o["value"] > 0
         assert o["assembled_frame_check"]["rgba8_mismatches"] == 0
+        # samples in flight across the ranks: S jittered samples per launch and rank, the
+        # assembled accumulation equal to one device replaying the same samples
+        sif = mg["samples_in_flight"]["per_samples"]
+        assert [e["S"] for e in sif] == [1, 2, 4, 8]
+        for e in sif:
+            assert e["rays_per_step"] == e["S"] * 1920 * 1080 and e["Mrays_per_s"] > 0
+            assert e["assembled_frame_check"]["rgba8_mismatches"] == 0, e
     else:
         assert mg["payload"] == payload and mg["other_frame"] is None
     assert d["config"]["parallelism"].endswith(f"rccl_gather({mg['payload']})")
