@@ -866,6 +866,10 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
     }
     const size_t region = (size_t)max(p.slots, 2) * TILE;   // >= 64 float4: the colours below
     uint2 *stk = stk_base + (size_t)k * region + lane;
+    // wave 0 loads its pixels' accumulation before tracing, so the load's latency is hidden by
+    // the trace instead of holding the wave's slot at its end
+    float4 dprev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (k == 0) dprev = p.accum[out_index(p, lr, gy, x)];
     FRay f;
     to_fray(r, f);
     if (p.guard) trace_lean<MODE, true>(p, f, stk);
@@ -880,11 +884,7 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
     __syncthreads();
     if (k != 0) return;
     const size_t i = out_index(p, lr, gy, x);
-    // the accumulation streams through once per launch (33 MB at 1080p): non-temporal both ways,
-    // so it does not evict the node pool from L2 (as the render's output stores, store_outputs)
-    f32x4 *acc = reinterpret_cast<f32x4 *>(p.accum + i);
-    const f32x4 a4 = __builtin_nontemporal_load(acc);
-    float4 d = make_float4(a4[0], a4[1], a4[2], a4[3]);
+    float4 d = dprev;
     for (int j = 0; j < p.samples; ++j) {   // accumulate_kernel's blend, sample j after sample j - 1
         const float4 c = reinterpret_cast<const float4 *>(stk_base + (size_t)j * region)[lane];
         const float a = p.blend_a[j], b = p.blend_b[j];
@@ -893,7 +893,7 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
         d.z = c.z * a + d.z * b;
         d.w = a * a + d.w * b;
     }
-    __builtin_nontemporal_store(f32x4{d.x, d.y, d.z, d.w}, acc);
+    p.accum[i] = d;
     if (p.accum8 || p.accum_rgb8) {
         const uint32_t w = pack_rgba8(d.x, d.y, d.z);
         if (p.accum8) __builtin_nontemporal_store(w, p.accum8 + i);

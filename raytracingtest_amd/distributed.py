@@ -220,7 +220,11 @@ def assemble(parts, height, width, dtype, rows=DEFAULT_BAND_ROWS):
 
 def accumulate_samples(rgba, world, dist=None):
     """Running mean of the ranks' jittered RGBA samples (AddShader's
-    alpha = 1/(n+1) blend over n = 0..world-1 equals the mean): in place."""
+    alpha = 1/(n+1) blend over n = 0..world-1 equals the mean in exact
+    arithmetic; in float32 the all-reduce's summation order differs from the
+    sequential blend, so this is the sample-parallel replica form, not bit-exact
+    with the reference's order -- svo_render_samples keeps that order bit for bit,
+    DESIGN.md 6.1b): in place."""
     if dist is None:
         import torch.distributed as dist
     dist.all_reduce(rgba)
