@@ -6,12 +6,13 @@
  * Texture2D.LoadRawTextureData(IntPtr, int).  Writes every displayed frame, in order, so a
  * test can compare them with the oracle's accumulation; prints the host time per frame.
  *
- *   progressive_async POOL CAM OFFS W H N OUT
+ *   progressive_async POOL CAM OFFS W H N OUT [rgb]
  *     POOL: uint32 n_desc, uint32 n_att, int32 desc[n_desc] (NaiveCreator.cs:184-187 words),
  *           uint32 att[n_att]
  *     CAM:  36 floats: c2w[16], inv_proj[16] (Unity column-major), light[4]
  *     OFFS: 2 N floats: _PixelOffset of frame k
- *     OUT:  N frames of W * H uint32 display words (frame k = the accumulation of samples 0..k)
+ *     OUT:  N frames of W * H uint32 display words (frame k = the accumulation of samples 0..k),
+ *           or with `rgb` W * H 3-byte pixels (SVO_PIXELS_RGB8 = TextureFormat.RGB24)
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -47,8 +48,8 @@ static double now_ms(void) {
 }
 
 int main(int argc, char **argv) {
-    if (argc != 8) {
-        fprintf(stderr, "usage: %s POOL CAM OFFS W H N OUT\n", argv[0]);
+    if (argc != 8 && argc != 9) {
+        fprintf(stderr, "usage: %s POOL CAM OFFS W H N OUT [rgb]\n", argv[0]);
         return 2;
     }
     size_t pool_size, cam_size, offs_size;
@@ -70,14 +71,15 @@ int main(int argc, char **argv) {
     svo_ctx *ctx = NULL;
     check(svo_create(0, n_desc, &ctx), "svo_create");
     check(svo_set_buffer(ctx, desc, n_desc, att, n_att, 0), "svo_set_buffer");
-    const size_t frame_bytes = (size_t)w * h * sizeof(uint32_t);
+    const int fmt = argc == 9 && strcmp(argv[8], "rgb") == 0 ? SVO_PIXELS_RGB8 : SVO_PIXELS_RGBA8;
+    const size_t frame_bytes = (size_t)w * h * (fmt == SVO_PIXELS_RGB8 ? 3 : 4);
     double t0 = 0.0;
     int written = 0;
     for (int k = 0; k < n; ++k) {
         if (k == 1) t0 = now_ms();   /* frame 0 allocates the accumulation and the pinned slots */
         check(svo_set_camera(ctx, cam, cam + 16, offs[2 * k], offs[2 * k + 1], cam + 32), "svo_set_camera");
-        const uint32_t *frame = NULL;
-        check(svo_render_progressive_async(ctx, w, h, SVO_STACK_HLSL, (uint32_t)k, &frame),
+        const void *frame = NULL;
+        check(svo_render_progressive_async(ctx, w, h, SVO_STACK_HLSL, (uint32_t)k, fmt, &frame),
               "svo_render_progressive_async");
         if ((k == 0) != (frame == NULL)) { fprintf(stderr, "frame %d: unexpected pointer\n", k); return 1; }
         if (frame) {   /* the previous frame (k - 1): consume it as LoadRawTextureData would */
@@ -86,7 +88,7 @@ int main(int argc, char **argv) {
         }
     }
     const double ms = n > 1 ? (now_ms() - t0) / (n - 1) : 0.0;
-    const uint32_t *last = NULL;
+    const void *last = NULL;
     check(svo_progressive_last(ctx, &last), "svo_progressive_last");
     if (!last) { fprintf(stderr, "no last frame\n"); return 1; }
     fwrite(last, 1, frame_bytes, out);

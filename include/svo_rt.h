@@ -298,17 +298,21 @@ int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, 
 /* svo_render_progressive for a host that displays every frame (Unity:
  * Texture2D.LoadRawTextureData(IntPtr, int) on the returned pointer, then Apply):
  * enqueue one sample -- render, blend with _Sample = `sample`, pack the accumulated
- * frame to display RGBA8 (the same words as svo_render_progressive's rgba8_out) --
- * and its copy into plugin-owned pinned host memory on a copy stream, then return in
- * *frame_out the PREVIOUS call's frame (NULL on the first call after creation or a
- * size change), waiting only for that frame's copy.  So the D2H of frame k overlaps
- * the render of frame k + 1, and the host never waits for the frame it just asked for.
- * A returned pointer (W * H uint32 words) stays valid until the call after next; the
- * plugin owns it.  svo_progressive_last returns the most recent frame, waiting for its
- * copy (the end of a sequence).  The blocking svo_render_progressive stays available. */
+ * frame to display pixels -- and their copy into plugin-owned pinned host memory on a
+ * copy stream, then return in *frame_out the PREVIOUS call's frame (NULL on the first
+ * call after creation, a size change or a pixel-format change), waiting only for that
+ * frame's copy.  So the D2H of frame k overlaps the render of frame k + 1, and the host
+ * never waits for the frame it just asked for.  pixel_format: SVO_PIXELS_RGBA8 (4 B/px,
+ * the words of svo_render_progressive's rgba8_out = TextureFormat.RGBA32) or
+ * SVO_PIXELS_RGB8 (3 B/px, the same words without their constant alpha =
+ * TextureFormat.RGB24: a quarter fewer bytes over PCIe).  A returned pointer (W * H
+ * pixels) stays valid until the call after next; the plugin owns it.
+ * svo_progressive_last returns the most recent frame, waiting for its copy (the end of a
+ * sequence).  The blocking svo_render_progressive stays available. */
+enum { SVO_PIXELS_RGBA8 = 0, SVO_PIXELS_RGB8 = 1 };
 int svo_render_progressive_async(svo_ctx *ctx, int width, int height, int stack_mode, uint32_t sample,
-                                 const uint32_t **frame_out);
-int svo_progressive_last(svo_ctx *ctx, const uint32_t **frame_out);
+                                 int pixel_format, const void **frame_out);
+int svo_progressive_last(svo_ctx *ctx, const void **frame_out);
 
 /* Information about the uploaded pool. */
 int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device);

@@ -56,6 +56,7 @@ def sparse_part_bytes(n_tiles, n_px):
     return ((sparse_head_bytes(n_tiles) + 3 * n_px + 3) & ~3) + 4 * n_tiles + 4 * ((n_tiles + 1023) // 1024)
 STAGE_KERNEL, STAGE_ASSEMBLE = 0, 1
 MAX_SAMPLES = 8   # svo_render_samples: jittered samples per launch
+PIXELS_RGBA8, PIXELS_RGB8 = 0, 1   # svo_render_progressive_async pixel formats
 
 
 class SvoBand(ctypes.Structure):
@@ -131,7 +132,7 @@ def lib():
         "svo_render_samples": [vp, i, i, i, ctypes.POINTER(SvoBand), i, ctypes.POINTER(f), ctypes.c_uint32, vp, vp, vp,
                                i, vp],
         "svo_render_progressive": [vp, i, i, i, ctypes.c_uint32, vp, vp],
-        "svo_render_progressive_async": [vp, i, i, i, ctypes.c_uint32, ctypes.POINTER(vp)],
+        "svo_render_progressive_async": [vp, i, i, i, ctypes.c_uint32, i, ctypes.POINTER(vp)],
         "svo_progressive_last": [vp, ctypes.POINTER(vp)],
         "svo_set_band_deal": [vp, i, ctypes.POINTER(ctypes.c_uint8)],
         "svo_pack_hits": [vp, i, i, ctypes.POINTER(SvoBand), vp, vp, vp],

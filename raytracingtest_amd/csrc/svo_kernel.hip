@@ -1453,6 +1453,46 @@ __global__ __launch_bounds__(256) void pack_rgba8_kernel(const float4 *__restric
     }
 }
 
+// The same words without their constant alpha, 3 bytes per pixel (Unity TextureFormat.RGB24):
+// 4 pixels per lane -> 3 dwords, so the stores stay whole and aligned; a tail of < 4 pixels
+// is written bytewise by the last lane.
+__global__ __launch_bounds__(256) void pack_rgb8_kernel(const float4 *__restrict__ src, uint8_t *__restrict__ dst,
+                                                        size_t n) {
+    auto q = [](float v) {
+        v = fminf(fmaxf(v, 0.0f), 1.0f);
+        v = v * 255.0f;
+        return (uint32_t)(v + 0.5f);
+    };
+    const size_t groups = n / 4, stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride) {
+        uint32_t b[12];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 c = src[4 * g + j];
+            b[3 * j] = q(c.x);
+            b[3 * j + 1] = q(c.y);
+            b[3 * j + 2] = q(c.z);
+        }
+        uint32_t *d = reinterpret_cast<uint32_t *>(dst + 12 * g);
+#pragma unroll
+        for (int w = 0; w < 3; ++w) d[w] = b[4 * w] | (b[4 * w + 1] << 8) | (b[4 * w + 2] << 16) | (b[4 * w + 3] << 24);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (size_t i = 4 * groups; i < n; ++i) {
+            const float4 c = src[i];
+            dst[3 * i] = (uint8_t)q(c.x);
+            dst[3 * i + 1] = (uint8_t)q(c.y);
+            dst[3 * i + 2] = (uint8_t)q(c.z);
+        }
+}
+
+hipError_t launch_pack_rgb8(const float4 *src, uint8_t *dst, size_t n_px, int num_cus, hipStream_t stream) {
+    if (n_px == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>((n_px / 4 + 255) / 256, (size_t)num_cus * 16));
+    hipLaunchKernelGGL(pack_rgb8_kernel, dim3(blocks), dim3(256), 0, stream, src, dst, n_px);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int num_cus, hipStream_t stream) {
     if (n_px == 0) return hipSuccess;
     const unsigned blocks = (unsigned)std::min<size_t>((n_px + 255) / 256, (size_t)num_cus * 16);

@@ -164,6 +164,7 @@ struct svo_ctx {
     bool pin_used[PIN_SLOTS] = {};
     hipStream_t copy_stream = nullptr;
     int pin_w = 0, pin_h = 0, pin_next = 0;
+    int pin_format = SVO_PIXELS_RGBA8;   // the slots' pixel format (svo_render_progressive_async)
     int pin_push = 0;                    // env SVO_PIN_PUSH: 0 hipMemcpyAsync (DMA), 1 a kernel writes the
                                          // mapped pinned buffer, 2 the DMA split over two copy streams
     hipStream_t copy_stream2 = nullptr;
@@ -1428,10 +1429,12 @@ int svo_render_progressive(svo_ctx *ctx, int width, int height, int stack_mode, 
 }
 
 int svo_render_progressive_async(svo_ctx *ctx, int width, int height, int stack_mode, uint32_t sample,
-                                 const uint32_t **frame_out) {
+                                 int pixel_format, const void **frame_out) {
     if (!ctx || !frame_out) return fail(SVO_ERR_ARG, "null argument");
     *frame_out = nullptr;
     if (width <= 0 || height <= 0) return fail(SVO_ERR_ARG, "width/height must be positive");
+    if (pixel_format != SVO_PIXELS_RGBA8 && pixel_format != SVO_PIXELS_RGB8)
+        return fail(SVO_ERR_ARG, "unknown pixel format");
     const size_t px = (size_t)width * (size_t)height;
     svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;
     HIP_TRY(hipSetDevice(c->device));
@@ -1441,6 +1444,13 @@ int svo_render_progressive_async(svo_ctx *ctx, int width, int height, int stack_
     rc = ensure_accum(c, width, height, &fresh);
     if (rc) return rc;
     if (fresh) sample = 0;   // as svo_render_progressive: a resized target restarts the accumulation
+    if (c->pin_format != pixel_format) {   // the slots' previous frames are in another format
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->copy_stream) HIP_TRY(hipStreamSynchronize(c->copy_stream));
+        if (c->copy_stream2) HIP_TRY(hipStreamSynchronize(c->copy_stream2));
+        free_pinned(c);
+        c->pin_format = pixel_format;
+    }
     rc = ensure_pinned(c, width, height);
     if (rc) return rc;
     rc = order_scratch(c, c->stream);
@@ -1458,11 +1468,13 @@ int svo_render_progressive_async(svo_ctx *ctx, int width, int height, int stack_
     const int k = c->pin_next;
     // slot k's previous copy (PIN_SLOTS frames ago) must have read d_pin[k] before the pack overwrites it
     if (c->pin_used[k]) HIP_TRY(hipStreamWaitEvent(c->stream, c->pin_copied[k], 0));
-    e = svo::launch_pack_rgba8(c->d_accum, c->d_pin[k], px, c->num_cus, c->stream);
+    e = pixel_format == SVO_PIXELS_RGB8
+            ? svo::launch_pack_rgb8(c->d_accum, reinterpret_cast<uint8_t *>(c->d_pin[k]), px, c->num_cus, c->stream)
+            : svo::launch_pack_rgba8(c->d_accum, c->d_pin[k], px, c->num_cus, c->stream);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("pack launch: ") + hipGetErrorString(e));
     HIP_TRY(hipEventRecord(c->pin_packed[k], c->stream));
     HIP_TRY(hipStreamWaitEvent(c->copy_stream, c->pin_packed[k], 0));
-    const size_t fbytes = px * sizeof(uint32_t);
+    const size_t fbytes = px * (pixel_format == SVO_PIXELS_RGB8 ? 3 : 4);
     if (c->pin_push == 1) {   // a kernel writes the mapped pinned buffer over PCIe
         void *dst = nullptr;
         HIP_TRY(hipHostGetDevicePointer(&dst, c->h_pin[k], 0));
@@ -1494,7 +1506,7 @@ int svo_render_progressive_async(svo_ctx *ctx, int width, int height, int stack_
     return SVO_OK;
 }
 
-int svo_progressive_last(svo_ctx *ctx, const uint32_t **frame_out) {
+int svo_progressive_last(svo_ctx *ctx, const void **frame_out) {
     if (!ctx || !frame_out) return fail(SVO_ERR_ARG, "null argument");
     *frame_out = nullptr;
     svo_ctx *c = is_multi(ctx) ? ctx->members[0] : ctx;

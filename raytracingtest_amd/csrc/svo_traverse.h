@@ -161,6 +161,9 @@ size_t shadow_list_bytes(int width, int local_rows);
 // Copy `bytes` (a multiple of 16) of device memory into mapped pinned host memory with a kernel.
 hipError_t launch_push_host(const void *src, void *dst_mapped, size_t bytes, int blocks, hipStream_t stream);
 
+// Display RGB, 3 bytes per pixel, of an RGBA32F frame (svo_render_progressive_async, RGB8).
+hipError_t launch_pack_rgb8(const float4 *src, uint8_t *dst, size_t n_px, int num_cus, hipStream_t stream);
+
 // Display RGBA8 words of an RGBA32F frame (svo_render_progressive).
 hipError_t launch_pack_rgba8(const float4 *src, uint32_t *dst, size_t n_px, int num_cus, hipStream_t stream);
 

@@ -208,31 +208,37 @@ class RaytracingMaster:
         self.currentSample += 1
         return rgba8, rgba
 
-    def RenderProgressiveAsync(self, width, height, stack_mode=STACK_HLSL, copy=True):
+    def RenderProgressiveAsync(self, width, height, stack_mode=STACK_HLSL, copy=True, rgb=False):
         """OnRenderImage through the pipelined readback (svo_render_progressive_async):
-        enqueue this sample and return the PREVIOUS frame's display words (rgba8[H, W]
-        uint32; None on the first call at a size).  copy=False returns a view of the
-        plugin's pinned buffer, valid until the call after next."""
+        enqueue this sample and return the PREVIOUS frame's display pixels (rgba8[H, W]
+        uint32 words, or with rgb=True uint8[H, W, 3]; None on the first call at a size or
+        format).  copy=False returns a view of the plugin's pinned buffer, valid until the
+        call after next."""
         if getattr(self, "_accum_size", None) != (width, height):
             self._accum_size = (width, height)
             self.currentSample = 0
         ptr = ctypes.c_void_p()
-        check(_lib.lib().svo_render_progressive_async(self._ctx, width, height, stack_mode, self.currentSample,
+        fmt = _lib.PIXELS_RGB8 if rgb else _lib.PIXELS_RGBA8
+        check(_lib.lib().svo_render_progressive_async(self._ctx, width, height, stack_mode, self.currentSample, fmt,
                                                       ctypes.byref(ptr)), "svo_render_progressive_async")
         self.currentSample += 1
-        return self._pinned_frame(ptr, width, height, copy)
+        self._pin_rgb = rgb
+        return self._pinned_frame(ptr, width, height, copy, rgb)
 
     def ProgressiveLast(self, width, height, copy=True):
         """The most recent frame of RenderProgressiveAsync (waits for its copy)."""
         ptr = ctypes.c_void_p()
         check(_lib.lib().svo_progressive_last(self._ctx, ctypes.byref(ptr)), "svo_progressive_last")
-        return self._pinned_frame(ptr, width, height, copy)
+        return self._pinned_frame(ptr, width, height, copy, getattr(self, "_pin_rgb", False))
 
     @staticmethod
-    def _pinned_frame(ptr, width, height, copy):
+    def _pinned_frame(ptr, width, height, copy, rgb=False):
         if not ptr.value:
             return None
-        a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint32)), shape=(height, width))
+        if rgb:
+            a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), shape=(height, width, 3))
+        else:
+            a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint32)), shape=(height, width))
         return a.copy() if copy else a
 
     def render_device(self, width, height, rgba_ptr=None, hits_ptr=None, stack_mode=STACK_HLSL,

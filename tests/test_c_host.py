@@ -132,7 +132,8 @@ def test_c_host_progressive_async_compiles_and_links(tmp_path):
 
 
 @pytest.mark.gpu
-def test_c_host_progressive_async_frames_match_oracle(tmp_path, oracle_mod, text_svo):
+@pytest.mark.parametrize("rgb", [False, True])
+def test_c_host_progressive_async_frames_match_oracle(tmp_path, oracle_mod, text_svo, rgb):
     """the Unity loop through svo_render_progressive_async from plain C --
     a new jittered _PixelOffset per frame, each call returning the previous frame from the
     plugin's pinned slots -- displays exactly the oracle's accumulation (per-sample render
@@ -151,11 +152,15 @@ def test_c_host_progressive_async_frames_match_oracle(tmp_path, oracle_mod, text
     offs = jitter_offsets(N)
     (tmp_path / "offs.bin").write_bytes(offs.astype(np.float32).tobytes())
     out = subprocess.run([exe, str(tmp_path / "pool.bin"), str(tmp_path / "cam.bin"), str(tmp_path / "offs.bin"),
-                          str(W), str(H), str(N), str(tmp_path / "frames.bin")], capture_output=True, text=True,
-                         timeout=120)
+                          str(W), str(H), str(N), str(tmp_path / "frames.bin")] + (["rgb"] if rgb else []),
+                         capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert json.loads(out.stdout.strip().splitlines()[-1])["frames"] == N
-    got = np.fromfile(tmp_path / "frames.bin", np.uint32).reshape(N, W * H)
+    if rgb:   # SVO_PIXELS_RGB8: the display words without their alpha byte
+        px = np.fromfile(tmp_path / "frames.bin", np.uint8).reshape(N, W * H, 3).astype(np.uint32)
+        got = px[..., 0] | (px[..., 1] << 8) | (px[..., 2] << 16) | np.uint32(255 << 24)
+    else:
+        got = np.fromfile(tmp_path / "frames.bin", np.uint32).reshape(N, W * H)
     c2w, inv_proj = CAMERAS["overview"]().uniforms(W, H)
     osvo = oracle_mod.OracleSVO(text_svo.childDescriptors, text_svo.attachments)
     acc = np.zeros((W * H, 4), np.float32)

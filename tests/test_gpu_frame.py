@@ -1029,6 +1029,14 @@ def test_render_progressive_async_pipelined_frames(torch, oracle_mod, text_svo, 
                 assert np.array_equal(v.reshape(-1), want[j]), f"frame {j} overwritten too early"
         last = rm.ProgressiveLast(W, H)
         assert np.array_equal(last.reshape(-1), want[-1])
+        # the 3-byte format (TextureFormat.RGB24): a format change restarts the slots (None), then
+        # each frame is the display words without their alpha; 203 x 70 leaves a 2-pixel tail
+        rm.UpdateShaderParameters(cam, W, H, pixel_offset=tuple(float(v) for v in offs[0]))
+        rm.currentSample = 0
+        assert rm.RenderProgressiveAsync(W, H, rgb=True) is None
+        rgb = rm.ProgressiveLast(W, H)
+        assert rgb.shape == (H, W, 3)
+        assert np.array_equal(rgb.reshape(-1, 3), want[0].view(np.uint8).reshape(-1, 4)[:, :3])
         rm.UpdateShaderParameters(cam, 64, 48)   # a new size: fresh accumulation and slots
         assert rm.RenderProgressiveAsync(64, 48) is None
         c2, i2 = cam.uniforms(64, 48)

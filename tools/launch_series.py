@@ -111,7 +111,7 @@ def main():
                 e.record(stream)
                 evs.append((first + i, e))
             launch()
-        torch.cuda.synchronize()
+        stream.synchronize()   # the render stream only: a device-wide sync would wait for the sampler
         marks.extend((i, sampler.ev.elapsed_time(e) * 1e3) for i, e in evs)
 
     def clock_at(marks, t_us, mhz, n):
@@ -131,8 +131,7 @@ def main():
     marks = []
     rm.count_fetches_device(W, H, fetch.data_ptr(), stack_mode=0, stream=sptr)
     run(5, marks)
-    _ = hits.cpu()          # bench.py's host copy of the records after the warmup
-    torch.cuda.synchronize()
+    _ = hits.cpu()          # bench.py's host copy of the records after the warmup (render stream)
     run(a.launches - 5, marks, first=5)
     seq = rm.stage_times()
     t_us, mhz = sampler.read()

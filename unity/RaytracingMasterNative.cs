@@ -35,8 +35,9 @@ public static class SvoNative {
                                                                      [Out] float[] rgbaOut);
     // pipelined readback: returns the previous frame's RGBA8 words in plugin-owned pinned memory
     // (valid until the call after next), the D2H of this frame overlapping the next render
+    public const int PixelsRgba8 = 0, PixelsRgb8 = 1;   // TextureFormat.RGBA32 / RGB24
     [DllImport(Lib)] public static extern int svo_render_progressive_async(IntPtr ctx, int width, int height,
-                                                                           int stackMode, uint sample,
+                                                                           int stackMode, uint sample, int pixelFormat,
                                                                            out IntPtr frame);
     [DllImport(Lib)] public static extern int svo_destroy(IntPtr ctx);
     [DllImport(Lib)] public static extern IntPtr svo_last_error();
@@ -172,15 +173,17 @@ public class RaytracingMasterNative : MonoBehaviour {
                                                  new[] { l.x, l.y, l.z, DirectionalLight.intensity }), "svo_set_camera");
         int w = Screen.width, h = Screen.height;
         if (_frame == null || _frame.width != w || _frame.height != h) {
-            _frame = new Texture2D(w, h, TextureFormat.RGBA32, false, true);
+            // the pipelined path moves 3-byte pixels (RGB24: a quarter fewer bytes over PCIe)
+            _frame = new Texture2D(w, h, pipelined ? TextureFormat.RGB24 : TextureFormat.RGBA32, false, true);
             _rgba8 = new uint[w * h];
             _currentSample = 0;   // a new render target: the plugin starts a fresh accumulation frame
         }
         if (pipelined) {
             SvoNative.Check(SvoNative.svo_render_progressive_async(_ctx, w, h, _stackMode, _currentSample,
-                                                                   out IntPtr prev), "svo_render_progressive_async");
+                                                                   SvoNative.PixelsRgb8, out IntPtr prev),
+                            "svo_render_progressive_async");
             if (prev != IntPtr.Zero) {   // NULL only on the first frame at this size
-                _frame.LoadRawTextureData(prev, w * h * 4);
+                _frame.LoadRawTextureData(prev, w * h * 3);
                 _frame.Apply(false);
             }
         } else {
