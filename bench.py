@@ -1367,17 +1367,21 @@ def host_path_rates(rm, W, H, args, n=5):
                         # the pipelined entry point: a pointer to the previous frame in pinned memory
                         # (copy=False: what LoadRawTextureData receives), D2H overlapping the next render
                         ("svo_render_progressive_async_rgba8",
-                         lambda: rm.RenderProgressiveAsync(W, H, stack_mode=args.stack_mode, copy=False), 50)):
+                         lambda: rm.RenderProgressiveAsync(W, H, stack_mode=args.stack_mode, copy=False), 50),
+                        ("svo_render_progressive_async_rgb24",
+                         lambda: rm.RenderProgressiveAsync(W, H, stack_mode=args.stack_mode, copy=False, rgb=True), 50)):
         fn()
         fn()
         t = time.perf_counter()
         for _ in range(k):
             fn()
         ms = (time.perf_counter() - t) / k * 1e3
+        bpp = 40 if name.startswith("svo_render_rgba") else 3 if name.endswith("rgb24") else 4
         out[name] = {"ms_per_frame": round(ms, 3), "Mrays_per_s": round(W * H / (ms * 1e-3) / 1e6, 1),
-                     "host_bytes_per_frame": W * H * (40 if name.startswith("svo_render_rgba") else 4), "frames": k}
-    out["svo_render_progressive_async_rgba8"]["note"] = ("each call returns the previous frame's pinned RGBA8 words; "
-                                                         "the caller's own copy of them is not included")
+                     "host_bytes_per_frame": W * H * bpp, "frames": k}
+    for name in ("svo_render_progressive_async_rgba8", "svo_render_progressive_async_rgb24"):
+        out[name]["note"] = ("each call returns the previous frame's pinned pixels (D2H overlapping the next "
+                             "render); the caller's own copy of them is not included")
     return out
 
 

@@ -1,7 +1,8 @@
 """A/B of svo_render_progressive_async's readback: per-frame host time of
 the C3 1080p progressive loop through the pipelined entry point, with the frame's RGBA8 words
 moved to the pinned slot by one DMA copy (SVO_PIN_PUSH=0), a kernel writing the mapped pinned
-buffer (1) or two DMA copies on two streams (2); the blocking svo_render_progressive beside.
+buffer (1) or two DMA copies on two streams (2), and one DMA copy of 3-byte pixels (RGB24); the
+blocking svo_render_progressive beside.
 Every mode's displayed frames are compared with the blocking path's for the same samples.
 Also times a plain pinned D2H of the same 8.3 MB (torch) for the link's rate.
 
@@ -58,27 +59,31 @@ def main():
             f, _ = rm.RenderProgressive(W, H)
             ref.append(f.copy())
         out["blocking_svo_render_progressive_ms"] = round((time.perf_counter() - t) / 20 * 1e3, 4)
-    for mode in (0, 1, 2):
+    for mode, rgb in ((0, False), (1, False), (2, False), (0, True)):
         os.environ["SVO_PIN_PUSH"] = str(mode)
+        key = f"async_push{mode}" + ("_rgb24" if rgb else "")
         with RaytracingMaster(device=0, capacity_nodes=len(svo)) as rm:
             rm.SetSVOBuffer(svo)
             rm.UpdateShaderParameters(cam, W, H)
             got = []
             for i in range(21):   # the same 20 samples as the blocking run (+1 call to get the 20th back)
-                f = rm.RenderProgressiveAsync(W, H)
+                f = rm.RenderProgressiveAsync(W, H, rgb=rgb)
                 if f is not None:
+                    if rgb:   # back to display words for the comparison
+                        f = f.astype(np.uint32)
+                        f = f[..., 0] | (f[..., 1] << 8) | (f[..., 2] << 16) | np.uint32(255 << 24)
                     got.append(f)
             bad = sum(int(not np.array_equal(g, r)) for g, r in zip(got, ref))
             rm.currentSample = 0
             for _ in range(10):
-                rm.RenderProgressiveAsync(W, H, copy=False)
+                rm.RenderProgressiveAsync(W, H, copy=False, rgb=rgb)
             t = time.perf_counter()
             for _ in range(a.frames):
-                rm.RenderProgressiveAsync(W, H, copy=False)
+                rm.RenderProgressiveAsync(W, H, copy=False, rgb=rgb)
             ms = (time.perf_counter() - t) / a.frames * 1e3
-        out[f"async_push{mode}"] = {"ms_per_frame": round(ms, 4), "frames_compared": len(got),
-                                    "frames_differing_from_blocking": bad}
-        print(json.dumps({f"async_push{mode}": out[f"async_push{mode}"]}), file=sys.stderr, flush=True)
+        out[key] = {"ms_per_frame": round(ms, 4), "frames_compared": len(got), "frames_differing_from_blocking": bad,
+                    "bytes_per_frame": W * H * (3 if rgb else 4)}
+        print(json.dumps({key: out[key]}), file=sys.stderr, flush=True)
     os.environ.pop("SVO_PIN_PUSH", None)
     print(json.dumps(out))
 
