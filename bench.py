@@ -452,19 +452,11 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     for _ in range(max(1, args.warmup)):
         step()
     drain()
-    torch.cuda.synchronize(dev)
-    host_hits = (hits if gather is None else gather.local_hits()).cpu().numpy().view(_lib.HIT_DTYPE)
-    n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
-    F = int(fetch[:n_px].to(torch.int64).sum().item())
-    bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if args.no_rgba else 16 * n_px)
-    if gather is not None:
-        # the RGBA8 display words (rank 0, in the frame) or band payload (3 B RGB / 4 B RGBA8 /
-        # 12-B compact records) the kernel also writes
-        bytes_per_launch += (4 if rank == 0 else {"rgb8": 3, "rgba8": 4, "compact": 12, "sparse": 3}[args.payload]) * n_px
 
-    # timed region: K steps between barrier + synchronize.  HIP events around each
-    # step only with SVO_STEP_EVENTS=1 (diagnostics): their stream markers add
-    # ~8 us to every step they bracket
+    # timed region: K steps between barrier + synchronize, right behind the warmup (the host
+    # reads of the hit records and fetch counts come after it, so the GPU does not idle between
+    # warmup and timing).  HIP events around each step only with SVO_STEP_EVENTS=1
+    # (diagnostics): their stream markers add ~8 us to every step they bracket
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -498,6 +490,14 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     torch.cuda.synchronize(dev)
     if n_timed != args.steps:
         raise RuntimeError(f"kernel timing: {n_timed} launches recorded, {args.steps} expected")
+    host_hits = (hits if gather is None else gather.local_hits()).cpu().numpy().view(_lib.HIT_DTYPE)
+    n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
+    F = int(fetch[:n_px].to(torch.int64).sum().item())
+    bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if args.no_rgba else 16 * n_px)
+    if gather is not None:
+        # the RGBA8 display words (rank 0, in the frame) or band payload (3 B RGB / 4 B RGBA8 /
+        # 12-B compact records) the kernel also writes
+        bytes_per_launch += (4 if rank == 0 else {"rgb8": 3, "rgba8": 4, "compact": 12, "sparse": 3}[args.payload]) * n_px
     stages = gather.stage_times(args.stack_mode, max(3, args.steps // 2)) if gather else None
     frame_check = gather.check_frame(args.stack_mode) if gather is not None and rank == 0 else None
     if world > 1:

@@ -82,7 +82,7 @@ struct Sched {
     hipStream_t stream = nullptr;
     bool used = false;
     unsigned long long last_use = 0;
-    hipEvent_t done = nullptr;       // recorded behind this stream's last render (eviction)
+    hipEvent_t done = nullptr;       // eviction: recorded on this stream when another takes the set over
     uint16_t *tile_cost = nullptr;
     uint32_t *tile_order = nullptr;
     uint16_t *shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
@@ -270,14 +270,23 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         pick = &ctx->sched[0];
         for (Sched &q : ctx->sched)
             if (q.last_use < pick->last_use) pick = &q;
-        if (pick->done) HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
+        // s takes over the set only after the renders the evicted stream was given: an event
+        // recorded on that stream NOW stands behind all of them (host order = stream order).
+        // Recorded here, at the rare eviction, not behind every launch: a marker packet
+        // between two renders of one stream cost ~2-3 us of GPU time per frame.
+        if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
+        if (hipEventRecord(pick->done, pick->stream) == hipSuccess) {
+            HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
+        } else {   // that stream is gone (destroyed by its owner): wait for the whole device
+            (void)hipGetLastError();
+            HIP_TRY(hipDeviceSynchronize());
+        }
         pick->order_key = pick->shadow_key = Geo();   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
         for (int r = 0; r < Sched::STATS_RING; ++r) pick->stats_pending[r] = false;
         pick->lat_key = Geo();
         pick->lat_mode = -1;
     }
-    if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
     pick->stream = s;
     pick->used = true;
     pick->last_use = ++ctx->sched_clock;
@@ -777,7 +786,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("shadow order launch: ") + hipGetErrorString(e));
         q->shadow_key = key;
     }
-    if (q) HIP_TRY(hipEventRecord(q->done, s));
     if (p.wave_log) {   // blocking dump of the last launch's per-wave record
         HIP_TRY(hipStreamSynchronize(s));
         std::vector<uint32_t> h(n_wave * svo::WAVE_LOG_WORDS);
