@@ -92,6 +92,8 @@ struct Sched {
     Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
     unsigned long long built_view = 0;   // the context's view generation the order was built under
+    unsigned long long view_prev = ~0ull;   // the view generation of this stream's last launch
+    unsigned long long last_build = 0;      // the launch count at the last order build
     int built_mode = -1;                 // shadows | stack_mode << 2 of the costs it was built from
     // loop-form choice (see launch): a ring of the last STATS_RING order builds' statistics
     // (host-visible: per XCD max / sum of the tile costs the order kernel saw, 16 words each),
@@ -187,6 +189,9 @@ struct svo_ctx {
     int shadow_compact = 0;          // env SVO_SHADOW_COMPACT=1: that launch over the compacted hit list
     int lat_mode = -1;               // env SVO_LAT: 0 never, 1 always, unset: by the last launch's costs (see launch)
     double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold
+    int move_every = 4;              // env SVO_MOVE_EVERY: while the camera moves every launch, rebuild the
+                                     // order only every k-th launch (see launch; 1 = at every new view).
+                                     // C3 pan: 118.8 us per frame at 1, 110.7 at 4, 111.9 at 8
     int order_every = 32;            // env SVO_ORDER_EVERY: rebuild the order every k-th launch (and after
                                      // every camera move or change of render mode)
     unsigned long long view_gen = 0; // bumped when svo_set_camera changes the matrices
@@ -283,6 +288,8 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         }
         pick->order_key = pick->shadow_key = Geo();   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
+        pick->view_prev = ~0ull;
+        pick->last_build = 0;
         for (int r = 0; r < Sched::STATS_RING; ++r) pick->stats_pending[r] = false;
         pick->lat_key = Geo();
         pick->lat_mode = -1;
@@ -756,12 +763,21 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     }
     hipError_t e = svo::launch_render(p, stack_mode, s, ev0, ev1);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
-    // refresh: a new geometry, every order_every-th launch, and right after the first launch
-    // following a camera move or a change of render mode (that launch still uses the old
-    // order -- a permutation of the same tiles, placement only -- and records fresh costs)
-    const bool refresh = q && p.tile_cost &&
-                         (q->order_key != key || q->launches++ % ctx->order_every == 0 ||
-                          q->built_view != ctx->view_gen || q->built_mode != mode_now);
+    // refresh: a new geometry, every order_every-th launch, a change of render mode, and a camera
+    // move -- right after the first launch at a view the camera then holds (that launch still
+    // uses the old order, a permutation of the same tiles, placement only, and records fresh
+    // costs), but while the camera moves every launch only every move_every-th launch: each
+    // build is an order kernel plus an event on the render stream, and the last few frames'
+    // costs order a slowly moving view almost as well as its own
+    bool refresh = false;
+    if (q && p.tile_cost) {
+        const unsigned long long n = q->launches++;
+        const bool moving = q->view_prev != ctx->view_gen;   // a new view since this stream's last launch
+        q->view_prev = ctx->view_gen;
+        refresh = q->order_key != key || n % ctx->order_every == 0 || q->built_mode != mode_now ||
+                  (q->built_view != ctx->view_gen && (!moving || n - q->last_build >= (unsigned long long)ctx->move_every));
+        if (refresh) q->last_build = n;
+    }
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
         const int r = q->stats_head;
         uint32_t *st16 = q->stats ? q->stats + 16 * r : nullptr;
@@ -1100,6 +1116,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_FUSED_SHADOWS")) ctx->fused_shadows = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SHADOW_COMPACT")) ctx->shadow_compact = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
+    if (const char *k = std::getenv("SVO_MOVE_EVERY")) ctx->move_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_LAT")) ctx->lat_mode = std::atoi(k) != 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
     if (e != hipSuccess) {

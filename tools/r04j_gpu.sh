@@ -1,4 +1,5 @@
-# round-4 final-tree evidence (r04j, after the per-render marker was dropped): GPU suite, smoke,
+# round-4 final-tree evidence (TAG=r04j: after the per-render marker was dropped; r04k: the moving-camera
+# rebuild throttle): GPU suite, smoke,
 # the driver's own bench command, then the bench / kernel-trace / PMC passes that
 # tools/pmc_summary.py turns into profiles/pmc_summary.json for this tree's digest
 export TMPDIR=/tmp
