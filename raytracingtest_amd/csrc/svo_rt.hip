@@ -93,6 +93,7 @@ struct Sched {
     unsigned long long launches = 0, shadow_launches = 0;
     unsigned long long built_view = 0;   // the context's view generation the order was built under
     unsigned long long view_prev = ~0ull;   // the view generation of this stream's last launch
+    unsigned long long built_cost = ~0ull;  // the context's cost generation the order was built under
     unsigned long long last_build = 0;      // the launch count at the last order build
     int built_mode = -1;                 // shadows | stack_mode << 2 of the costs it was built from
     // loop-form choice (see launch): a ring of the last STATS_RING order builds' statistics
@@ -195,6 +196,8 @@ struct svo_ctx {
     int order_every = 32;            // env SVO_ORDER_EVERY: rebuild the order every k-th launch (and after
                                      // every camera move or change of render mode)
     unsigned long long view_gen = 0; // bumped when svo_set_camera changes the matrices
+    unsigned long long cost_gen = 0; // bumped by whatever else changes the tiles' costs: a new pixel
+                                     // offset or light, an upload
     Sched sched[MAX_SCHED];
     unsigned long long sched_clock = 0;
     // The one piece of state renders on different streams still share: the host-path /
@@ -289,6 +292,7 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         pick->order_key = pick->shadow_key = Geo();   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
         pick->view_prev = ~0ull;
+        pick->built_cost = ~0ull;
         pick->last_build = 0;
         for (int r = 0; r < Sched::STATS_RING; ++r) pick->stats_pending[r] = false;
         pick->lat_key = Geo();
@@ -380,6 +384,7 @@ void commit_upload(svo_ctx *ctx, const Upload &u) {
                        ctx->uploads.end());
     ctx->uploads.push_back(u);
     ctx->n_nodes = std::max(ctx->n_nodes, u.offset + u.count);
+    ++ctx->cost_gen;   // another pool: other costs
     recompute_depth(ctx);
 }
 
@@ -763,18 +768,22 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     }
     hipError_t e = svo::launch_render(p, stack_mode, s, ev0, ev1);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
-    // refresh: a new geometry, every order_every-th launch, a change of render mode, and a camera
-    // move -- right after the first launch at a view the camera then holds (that launch still
-    // uses the old order, a permutation of the same tiles, placement only, and records fresh
-    // costs), but while the camera moves every launch only every move_every-th launch: each
-    // build is an order kernel plus an event on the render stream, and the last few frames'
-    // costs order a slowly moving view almost as well as its own
+    // refresh: a new geometry, every order_every-th launch while costs can drift, a change of
+    // render mode, and a camera move -- right after the first launch at a view the camera then
+    // holds (that launch still uses the old order, a permutation of the same tiles, placement
+    // only, and records fresh costs), but while the camera moves every launch only every
+    // move_every-th launch: each build is an order kernel plus an event on the render stream, and
+    // the last few frames' costs order a slowly moving view almost as well as its own
     bool refresh = false;
     if (q && p.tile_cost) {
         const unsigned long long n = q->launches++;
         const bool moving = q->view_prev != ctx->view_gen;   // a new view since this stream's last launch
         q->view_prev = ctx->view_gen;
-        refresh = q->order_key != key || n % ctx->order_every == 0 || q->built_mode != mode_now ||
+        // the periodic rebuild only when costs can have changed without a new view (a jittered
+        // pixel offset, a new light or pool, per-launch sample offsets): a held view with nothing
+        // else changed records the same costs every launch, so its order stays exact
+        const bool drift = q->built_cost != ctx->cost_gen || p.samples != 0;
+        refresh = q->order_key != key || (n % ctx->order_every == 0 && drift) || q->built_mode != mode_now ||
                   (q->built_view != ctx->view_gen && (!moving || n - q->last_build >= (unsigned long long)ctx->move_every));
         if (refresh) q->last_build = n;
     }
@@ -786,6 +795,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         q->order_key = key;
         q->built_view = ctx->view_gen;
+        q->built_cost = ctx->cost_gen;
         q->built_mode = mode_now;
         if (st16) {   // slot r: a build still pending there (ring full) is simply superseded
             HIP_TRY(hipEventRecord(q->stats_ev[r], s));
@@ -1319,6 +1329,9 @@ int svo_set_camera(svo_ctx *ctx, const float c2w[16], const float inv_proj[16], 
     if (!ctx->cam_set || std::memcmp(ctx->cam.c2w, c2w, sizeof(ctx->cam.c2w)) != 0 ||
         std::memcmp(ctx->cam.inv_proj, inv_proj, sizeof(ctx->cam.inv_proj)) != 0)
         ++ctx->view_gen;
+    if (!ctx->cam_set || ctx->cam.px_off[0] != px_off_x || ctx->cam.px_off[1] != px_off_y ||
+        std::memcmp(ctx->cam.light, light, sizeof(ctx->cam.light)) != 0)
+        ++ctx->cost_gen;
     std::memcpy(ctx->cam.c2w, c2w, sizeof(ctx->cam.c2w));
     std::memcpy(ctx->cam.inv_proj, inv_proj, sizeof(ctx->cam.inv_proj));
     ctx->cam.px_off[0] = px_off_x;
