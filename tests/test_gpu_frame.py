@@ -1079,3 +1079,34 @@ def test_render_samples_multi_device(torch, oracle_mod, devices):
             rm.render_samples(96, 64, offs[:2], 0, acc.data_ptr(), layout=_lib.LAYOUT_FRAME)
     finally:
         rm.close()
+
+
+@pytest.mark.parametrize("move_every", [1, 4])
+def test_moving_camera_frames_match_oracle(torch, oracle_mod, monkeypatch, move_every):
+    """A camera that moves every frame (the interactive case, RaytracingMaster.cs:55-74): the
+    dispatch order is rebuilt every move_every-th frame from older views' costs (svo_rt.hip
+    launch, SVO_MOVE_EVERY), then the pan stops and the held view gets its own order.  Placement
+    only: every frame equals the oracle's frame for its own view, and so does the held one."""
+    monkeypatch.setenv("SVO_MOVE_EVERY", str(move_every))
+    svo = build_menger(8)
+    w, h = 320, 184
+    eyes = [(4.0 * np.sin(0.05 * i), 20.0, -40.0 + 3.0 * i) for i in range(7)]
+    cams = [overview_camera(e, (0.0, 0.0, 0.0)) for e in eyes]
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        bufs = [_bufs(torch, w * h) for _ in cams]
+        for cam, b in zip(cams, bufs):      # one frame per view, no host sync in between
+            m.UpdateShaderParameters(cam, w, h)
+            m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr())
+        held = [_bufs(torch, w * h) for _ in range(3)]
+        for b in held:                      # the pan stops: three frames at the last view
+            m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr())
+        m.synchronize()
+        for cam, b in zip(cams, bufs):
+            ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+            _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+        for b in held:
+            _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+    finally:
+        m.close()
