@@ -818,6 +818,342 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
     if (p.wave_log && lane == 0) p.wave_log[WAVE_LOG_WORDS * (size_t)blockIdx.x + 9] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 }
 
+// ------------------------------------------------------------- segmented rays
+// One ray's traversal split into SEG_K t-segments that run side by side (VERDICT r4 item 1:
+// a heavy tile's wave is a serial chain of up to ~270 trips that bounds a frame split over N
+// GPUs; modelled first, tools/segment_model.py).  Segment k of a ray with
+// starts t_1 .. t_{K-1} (any floats, NaN included: the result never depends on them, only the
+// balance does) runs the lean loop from the cube entry with three changes:
+//   * SKIP: a non-leaf child it would descend into whose exit tc_max is below t_k lies wholly
+//     before t_k.  The lane instead takes the state the loop has after descending into it and
+//     popping back -- the stack entry that PUSH stores (N:97-98, also when h allows it), t_max
+//     through the HLSL float2 round trip (N:141-143), h = 0 (N:153) -- and ADVANCEs past it.
+//     Every ADVANCE inside such a subtree has t_min <= its tc_max < t_k (the corner times
+//     p * coef - bias are monotone in p, so a sub-cell's exit cannot pass its parent's), so the
+//     lane follows the continuous loop's own path, state for state, minus those subtrees.
+//   * ARM: a hit (N:93-94) counts only once the lane is armed: segment 0 from the start,
+//     segment k at the first ADVANCE whose new t_min >= t_k (before it, a leaf is stepped past).
+//   * STOP: segment k ends, without a hit, at the first ADVANCE whose new t_min >= t_{k+1} --
+//     the very event that arms segment k + 1 on the same path.
+// The ray's record is that of its first segment that did not stop (a hit, or the ray left
+// the cube): the segments before it covered everything up to its arming event without a hit.
+// Bit-identical to the continuous loop in both stack modes (tests/test_gpu_seg.py against the
+// oracle, with real and with random starts).
+template <int MODE, bool FETCH_ALL>
+__device__ __forceinline__ void trace_seg(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk, float t_start,
+                                          float t_stop, bool armed0, uint32_t &n_lane, uint32_t &armed_at,
+                                          bool &stopped_lane) {
+    constexpr int STRIDE = TILE;
+    const int slots = p.slots;
+    for (int s = 0; s < slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
+    const int scale_lo = S_MAX - slots;
+    lmask act = LM_OF(true);
+    lmask armed = LM_OF(armed0), stopped = 0, cached = 0;
+    const int oct = r.octant_mask | 16;
+    int sh = r.idx ^ oct;
+    const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
+    constexpr uint32_t SLOT = (uint32_t)(STRIDE * sizeof(uint2));
+    constexpr int SLOT_SH = 23 - 9;
+    const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
+    const uint2 *stk_pop = stk - (127 + scale_lo) * STRIDE;
+    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots - 1);
+    int it = 0;
+    n_lane = 0;
+    armed_at = 0;
+    asm volatile("" : "+v"(r.parent), "+v"(r.cd16), "+v"(r.first));
+    lmask go;
+    do {
+        asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
+        const lmask need = FETCH_ALL ? ~(lmask)0 : act & ~cached;
+        if (FETCH_ALL || LM_ON(need)) {
+            const uint2 nd = *(const uint2 *)((const char *)p.nodes + (uint32_t)(r.parent << 3));
+            r.cd16 = nd.x;
+            r.first = nd.y;
+        }
+        cached |= need;
+        const float tx = r.px * r.cx - r.bx;             // N:67-70
+        const float ty = r.py * r.cy - r.by;
+        const float tz = r.pz * r.cz - r.bz;
+        const float tc_max = fminf(fminf(tx, ty), tz);
+        const float tv_max = vmin(r.t_max, tc_max);
+        const float half = r.sexp * 0.5f;
+        const lmask cx = LM_OF(center(half, r.cx, tx) > r.t_min);
+        const lmask cy = LM_OF(center(half, r.cy, ty) > r.t_min);
+        const lmask cz = LM_OF(center(half, r.cz, tz) > r.t_min);
+        const lmask lx = LM_OF(tx <= tc_max), ly = LM_OF(ty <= tc_max), lz = LM_OF(tz <= tc_max);
+        const lmask in_span = LM_OF(r.t_min <= tv_max), below_h = LM_OF(tc_max < r.h);
+        const lmask before = LM_OF(tc_max < t_start);    // SKIP test (NaN start: never)
+        const lmask arm_now = LM_OF(tc_max >= t_start);  // ARM / STOP tests on the ADVANCE's new t_min
+        const lmask stop_now = LM_OF(tc_max >= t_stop);
+        const uint32_t cm = r.cd16 << sh;
+        const lmask descend = act & LM_OF((int32_t)cm < 0) & in_span;
+        const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
+        const lmask inner = descend & ~leaf;
+        const lmask skip = inner & before;
+        const lmask hit = descend & leaf & armed;        // N:93-94, armed lanes only
+        const lmask push = inner & ~skip;
+        const lmask store = inner & below_h;             // PUSH's stack write, also for a SKIP
+        const lmask adv = act & ~(hit | push);           // incl. SKIP lanes and unarmed leaves
+        if (LM_ON(store)) {                              // N:97-98
+            const uint32_t a = push_base + (__float_as_uint(r.sexp) >> SLOT_SH);
+            const uint32_t tmw = MODE == 0 ? (uint32_t)cvt_i32((float)(int32_t)__float_as_uint(r.t_max))
+                                           : __float_as_uint(r.t_max);
+            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(tmw) : "memory");
+        }
+        const lmask sx = adv & lx;                       // N:122-125
+        const lmask sy = adv & ly;
+        const lmask sz = adv & lz;
+        const float se = r.sexp;
+        const float delta = LM_ON(push) ? half : -se;
+        const float ox = r.px, oy = r.py, oz = r.pz;
+        const lmask mvx = (push & cx) | sx, mvy = (push & cy) | sy, mvz = (push & cz) | sz;
+        const float qx = r.px + (LM_ON(mvx) ? delta : 0.0f);
+        const float qy = r.py + (LM_ON(mvy) ? delta : 0.0f);
+        const float qz = r.pz + (LM_ON(mvz) ? delta : 0.0f);
+        const int mv = lanes_to_idx(mvx, mvy, mvz);
+        const lmask pop = adv & LM_OF((mv & ~(sh ^ oct)) != 0);
+        const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
+        sh = (LM_ON(push) ? oct : sh) ^ mv;
+        if (LM_ON(push)) {
+            r.parent = child;
+            r.h = tc_max;
+            r.t_max = tv_max;
+            r.sexp = half;
+        }
+        if (skip != 0) {   // back at this node's level as after a POP (N:141-153)
+            if (LM_ON(skip)) {
+                if (MODE == 0) r.t_max = __int_as_float(cvt_i32((float)(int32_t)__float_as_uint(r.t_max)));
+                r.h = 0.0f;
+            }
+        }
+        r.t_min = LM_ON(adv) ? tc_max : r.t_min;
+        const lmask armed_new = adv & arm_now & ~armed;
+        if (armed_new != 0) {
+            if (LM_ON(armed_new)) armed_at = (uint32_t)it;
+            armed |= armed_new;
+        }
+        const lmask stop = adv & stop_now;
+        cached &= ~(push | pop);
+        r.px = qx; r.py = qy; r.pz = qz;
+        lmask out = 0;
+        if (pop != 0) {                                  // N:134-154
+            const uint32_t diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) |
+                                  (__float_as_uint(oy) ^ __float_as_uint(qy)) |
+                                  (__float_as_uint(oz) ^ __float_as_uint(qz));
+            const uint32_t fd = __float_as_uint((float)diff);
+            const uint32_t ef = __builtin_amdgcn_ubfe(fd, 23, 8);
+            const int scale = (int)ef - 127;
+            const uint2 e = stk_pop[min(ef, e_max) * STRIDE];
+            const uint32_t keep = 0xFFFFFFFFu << scale;
+            const uint32_t bx_ = __builtin_amdgcn_ubfe(__float_as_uint(qx), scale, 1);
+            const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
+            const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
+            const bool pl = LM_ON(pop);
+            r.sexp = pl ? __uint_as_float((ef << 23) - (23u << 23)) : r.sexp;
+            r.parent = pl ? e.x : r.parent;
+            r.t_max = pl ? __uint_as_float(e.y) : r.t_max;
+            const uint32_t k = pl ? keep : 0xFFFFFFFFu;
+            r.px = __uint_as_float(__float_as_uint(r.px) & k);
+            r.py = __uint_as_float(__float_as_uint(r.py) & k);
+            r.pz = __uint_as_float(__float_as_uint(r.pz) & k);
+            r.h = pl ? 0.0f : r.h;
+            sh = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) ^ oct : sh;
+            out = pop & LM_OF(scale >= S_MAX);
+        }
+        const lmask fin = act & (hit | out | stop);
+        if (fin != 0) {
+            if (LM_ON(fin)) n_lane = (uint32_t)it;
+            stopped |= stop;                             // STOP before the cube exit of the same trip
+            act &= ~fin;
+        }
+        asm volatile("s_cmp_lt_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(go) : "s"(it), "n"(MAX_ITERS), "s"(act) : "scc");
+    } while (go != 0);
+    if (LM_ON(act)) {   // still tracing after MAX_ITERS trips (unreachable for a tree of depth <= 13)
+        r.flags |= 2u;
+        n_lane = (uint32_t)it;
+    }
+    stopped_lane = LM_ON(stopped);
+    r.idx = sh ^ oct;
+    r.trips = it;
+}
+
+// quad (lane ^ 1, lane ^ 2) reductions: a ray's SEG_K = 4 lanes
+__device__ __forceinline__ int quad_min(int v) {
+    v = min(v, __shfl_xor(v, 1));
+    return min(v, __shfl_xor(v, 2));
+}
+__device__ __forceinline__ float quad_get(float v, int src_in_quad) {
+    return __shfl(v, (int)(threadIdx.x & ~3u) + src_in_quad);
+}
+__device__ __forceinline__ uint32_t quad_get(uint32_t v, int src_in_quad) {
+    return (uint32_t)__shfl((int)v, (int)(threadIdx.x & ~3u) + src_in_quad);
+}
+
+// The next frame's starts of one ray from this frame's segments (lane k = quad's segment k):
+// the continuous trips each segment took after arming (segment 0: all of its trips) put the
+// cumulative share at its start t_k; the new t_j is where the cumulative share reaches j / K of
+// the total, linear in t between the points (t_entry, 0), (t_k, share before k), (t_end, total).
+// Only the balance of the next trace depends on it.  Called by every lane; lane 0 of the quad
+// gets the result.
+__device__ __forceinline__ float4 seg_rebalance(float t_entry, float t_start, float t_end, uint32_t c, int f) {
+    const int k = (int)(threadIdx.x & 3u);
+    const float cf = k <= f ? (float)c : 0.0f;
+    float cum[SEG_K + 1], tp[SEG_K + 1];
+    cum[0] = 0.0f;
+    tp[0] = t_entry;
+#pragma unroll
+    for (int j = 0; j < SEG_K; ++j) {
+        cum[j + 1] = cum[j] + quad_get(cf, j);
+        tp[j + 1] = j + 1 < SEG_K ? quad_get(t_start, j + 1) : t_end;
+    }
+#pragma unroll
+    for (int j = 1; j < SEG_K; ++j)
+        if (j > f) tp[j] = t_end;   // starts past the ray's end carry nothing
+    const float tot = cum[SEG_K];
+    float out[SEG_K - 1];
+#pragma unroll
+    for (int j = 1; j < SEG_K; ++j) {
+        const float target = tot * ((float)j / (float)SEG_K);
+        float v = tp[SEG_K];
+#pragma unroll
+        for (int m = SEG_K - 1; m >= 0; --m) {
+            if (cum[m + 1] >= target) {
+                const float span = cum[m + 1] - cum[m];
+                const float fr = span > 0.0f ? (target - cum[m]) / span : 0.0f;
+                v = tp[m] + fr * (tp[m + 1] - tp[m]);
+            }
+        }
+        out[j - 1] = j > 1 ? fmaxf(v, out[j - 2]) : v;
+    }
+    if (!(tot > 0.0f)) return make_float4(__int_as_float(0x7FC00000), 0.0f, 0.0f, 0.0f);
+    return make_float4(out[0], out[1], out[2], 0.0f);
+}
+
+// Cost-ordered launch whose order (launch_order_strips with seg_cap > 0) lists each XCD's
+// heaviest tiles as SEG_K quarter entries: quarter q traces rows 2 q, 2 q + 1 of its tile, 16
+// rays x SEG_K segments (lanes 4 r + k), and writes every output of those 16 pixels from the
+// lane of the segment that holds the record.  Every other entry is one tile, traced as in
+// render_tile_kernel (lean loop, primary rays).  A quarter's chain is its longest segment:
+// ~1/K of the tile's continuous chain plus the walk to t_k.
+template <int MODE, bool FA>
+__global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))) void render_seg_kernel(LaunchParams p, int tiles_x) {
+    extern __shared__ uint2 stk_base[];
+    const int lane = threadIdx.x;
+    const uint32_t entry = p.tile_order[blockIdx.x];
+    if (entry == SEG_EMPTY) return;
+    const int t = (int)(entry & 0x0FFFFFFFu);
+    const int quarter = (int)(entry >> 28) - 1;   // -1: a whole tile
+    if (p.prio) {
+        const uint32_t *bound = p.tile_order + gridDim.x + 4 + 4 * (blockIdx.x % 8);
+        const uint32_t b = blockIdx.x / 8;
+        if (b < bound[0]) __builtin_amdgcn_s_setprio(3);
+        else if (b < bound[1]) __builtin_amdgcn_s_setprio(2);
+        else if (b < bound[2]) __builtin_amdgcn_s_setprio(1);
+    }
+    const int bx = t % tiles_x, by = t / tiles_x;
+    uint2 *stk = stk_base + lane;
+    if (quarter < 0) {   // render_tile_kernel's primary-ray path
+        const int x = bx * 8 + (lane & 7);
+        const int lr = by * 8 + (lane >> 3);
+        if (x >= p.width || lr >= p.local_rows) return;
+        const int gy = global_row(p, lr);
+        Ray r;
+        {
+            float org[3], dir[3];
+            camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
+            setup_ray(org, dir, r);
+        }
+        FRay f;
+        to_fray(r, f);
+        trace_lean<MODE, false, false, FA>(p, f, stk);
+        from_fray(f, r);
+        Record o;
+        record(p, r, x, gy, o);
+        if (p.out.hitmask) {
+            const uint64_t hm = __ballot(r.scale < S_MAX);
+            if (lane == 0) p.out.hitmask[t] = hm;
+        }
+        if (p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, (int)(SEG_COST_FLAG - 1));
+        store_outputs(p.out, out_index(p, lr, gy, x), o);
+        return;
+    }
+    // quarter q of tile t: ray ri = lane / 4 is pixel (ri % 8, 2 q + ri / 8) of the tile, k its segment
+    const int k = lane & 3, ri = lane >> 2;
+    const int x_ = bx * 8 + (ri & 7);
+    const int lr_ = by * 8 + 2 * quarter + (ri >> 3);
+    const bool inside = x_ < p.width && lr_ < p.local_rows;   // outside lanes trace a copy, store nothing
+    const int x = min(x_, p.width - 1), lr = min(lr_, p.local_rows - 1);
+    const int gy = global_row(p, lr);
+    Ray r;
+    {
+        float org[3], dir[3];
+        camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
+        setup_ray(org, dir, r);
+    }
+    const float t_entry = r.t_min, t_exit = r.t_max;
+    const size_t hi = (size_t)lr * (size_t)p.width + (size_t)x;
+    float4 hint = p.seg_hint[hi];
+    if (hint.x != hint.x) {   // none yet: an even split of the cube span
+        const float span = t_exit - t_entry;
+        hint = make_float4(t_entry + 0.25f * span, t_entry + 0.5f * span, t_entry + 0.75f * span, 0.0f);
+    }
+    if (p.seg_scramble) {   // tests: arbitrary starts (the records must not change)
+        uint32_t hsh = (uint32_t)hi * 0x9E3779B1u ^ p.seg_scramble * 0x85EBCA77u;
+        float v[3];
+        const float span = t_exit - t_entry;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            hsh ^= hsh >> 15; hsh *= 0x2C1B3C6Du; hsh ^= hsh >> 12; hsh *= 0x297A2D39u; hsh ^= hsh >> 15;
+            const uint32_t sel = hsh & 15u;
+            const float u = (float)(hsh >> 8) * (1.0f / 16777216.0f);
+            v[j] = sel == 0 ? __int_as_float(0x7FC00000) : sel == 1 ? __int_as_float(0x7F800000)
+                 : sel == 2 ? __int_as_float(0xFF800000) : t_entry + (1.4f * u - 0.2f) * span;
+        }
+        hint = make_float4(v[0], v[1], v[2], 0.0f);
+    }
+    const float qnan = __int_as_float(0x7FC00000);
+    const float hk[SEG_K - 1] = {hint.x, hint.y, hint.z};
+    const float t_start = k == 0 ? qnan : hk[k - 1];
+    const float t_stop = k == SEG_K - 1 ? qnan : hk[k];
+    FRay f;
+    to_fray(r, f);
+    uint32_t n_lane, armed_at;
+    bool stopped;
+    trace_seg<MODE, FA>(p, f, stk, t_start, t_stop, k == 0, n_lane, armed_at, stopped);
+    from_fray(f, r);
+    // the record holder: the first segment that did not stop (the last one never stops)
+    const int fsel = quad_min(stopped ? SEG_K : k);
+    const bool writer = k == fsel;
+    const uint32_t c = k == 0 ? n_lane : n_lane - armed_at;   // continuous trips after arming
+    const float t_end = quad_get(r.scale < S_MAX ? r.t_min : t_exit, fsel);
+    const float4 nh = seg_rebalance(t_entry, t_start, t_end, c, fsel);
+    uint32_t tot = 0;   // the ray's continuous trips, its tile_cost share
+#pragma unroll
+    for (int j = 0; j < SEG_K; ++j) tot += quad_get(j <= fsel ? c : 0u, j);
+    if (k == 0 && inside) p.seg_hint[hi] = nh;
+    if (p.tile_cost) {
+        uint32_t m = inside ? tot : 0u;
+#pragma unroll
+        for (int d = 4; d < 64; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+        if (lane == 0) {
+            p.part_cost[4 * (size_t)t + quarter] = (uint16_t)min(m, (uint32_t)(SEG_COST_FLAG - 1));
+            if (quarter == 0) p.tile_cost[t] = SEG_COST_FLAG;
+        }
+    }
+    if (p.out.hitmask) {   // this quarter's 16 pixels: bits 16 q .. 16 q + 15 of the tile's mask
+        const uint64_t hm = __ballot(writer && inside && r.scale < S_MAX);
+        uint32_t part16 = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) part16 |= (uint32_t)((hm >> (4 * j + 0)) | (hm >> (4 * j + 1)) | (hm >> (4 * j + 2)) |
+                                                          (hm >> (4 * j + 3))) & 1u ? (1u << j) : 0u;
+        if (lane == 0) reinterpret_cast<uint16_t *>(p.out.hitmask + t)[quarter] = (uint16_t)part16;
+    }
+    if (!writer || !inside) return;
+    Record o;
+    record(p, r, x, gy, o);
+    store_outputs(p.out, out_index(p, lr, gy, x), o);
+}
+
 // ------------------------------------------------------------- samples in flight
 // svo_render_samples: the reference's frame loop is a stream of independent jittered samples,
 // each blended into the display target (_PixelOffset = (Random.value, Random.value) per frame,
@@ -1156,6 +1492,14 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
             hipLaunchKernelGGL((render_samples_kernel<MODE, false>), grid, sblock, per * p.samples, stream, p, bx);
         return hipGetLastError();
     }
+    if (!COUNT && p.seg > 0) {   // segmented heavy tiles (the order was built with seg_cap = p.seg)
+        const dim3 sgrid((unsigned)order_strips_grid(bx * by, p.seg));
+        if (p.fetch_all)
+            hipLaunchKernelGGL((render_seg_kernel<MODE, true>), sgrid, block, lds, stream, p, bx);
+        else
+            hipLaunchKernelGGL((render_seg_kernel<MODE, false>), sgrid, block, lds, stream, p, bx);
+        return hipGetLastError();
+    }
     if (COUNT)
         hipLaunchKernelGGL((render_tile_kernel<MODE, true>), grid, block, lds, stream, p, bx);
     else if (p.lat)   // latency form (svo_rt.hip launch decides): the stack entries keep their node
@@ -1208,7 +1552,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_tiles_kernel(const uint16
 #pragma unroll
         for (int e = 0; e < ORDER_PER; ++e) {
             const int i = c * ORDER_CHUNK + tid * ORDER_PER + e;
-            const uint32_t k = (v[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu;
+            const uint32_t k = (v[e >> 1] >> ((e & 1) * 16)) & 0x7FFFu;   // (no SEG_COST_FLAG in this mode)
             if (i < n) {
                 mx = max(mx, k);
                 sum += k;
@@ -1246,7 +1590,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_tiles_kernel(const uint16
 #pragma unroll
         for (int e = 0; e < ORDER_PER; ++e) {
             const int i = c * ORDER_CHUNK + tid * ORDER_PER + e;
-            const int k = i < n ? cls((v[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu) : NC;
+            const int k = i < n ? cls((v[e >> 1] >> ((e & 1) * 16)) & 0x7FFFu) : NC;
 #pragma unroll
             for (int q = 0; q < NC; ++q) count[q] += (uint32_t)__popcll(__ballot(k == q));
         }
@@ -1274,7 +1618,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_tiles_kernel(const uint16
 #pragma unroll
         for (int e = 0; e < ORDER_PER; ++e) {
             const int i = c * ORDER_CHUNK + tid * ORDER_PER + e;
-            const int k = i < n ? cls((v[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu) : NC;
+            const int k = i < n ? cls((v[e >> 1] >> ((e & 1) * 16)) & 0x7FFFu) : NC;
             uint32_t pos = 0;
 #pragma unroll
             for (int q = 0; q < NC; ++q) {
@@ -1297,14 +1641,24 @@ size_t order_cost_capacity(int n_tiles) {
 // stats (nullable, host-visible): [2 x] = the max and [2 x + 1] = the sum of XCD x's tile
 // costs -- the launch's heaviest wave and its total wave trips, which the host uses to pick
 // the loop form of the next launches (svo_rt.hip launch).
-__global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint16_t *__restrict__ cost,
+__global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint16_t *__restrict__ cost_in,
                                                                      uint32_t *__restrict__ order, int n, int tiles_x,
-                                                                     uint32_t *stats) {
+                                                                     uint32_t *stats, int seg_cap,
+                                                                     const uint16_t *__restrict__ part_cost,
+                                                                     int seg_classes) {
     __shared__ uint32_t red[ORDER_THREADS / 64], red_sum[ORDER_THREADS / 64];
     constexpr int NC = 6;
-    __shared__ uint32_t cnt[NC], base[NC];
+    __shared__ uint32_t cnt[NC], base[NC + 1], rank[NC], segs[NC];
     const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int len = n / 8, tiles_y = n / tiles_x;
+    const int L = len + (SEG_K - 1) * seg_cap;   // every XCD's list length (grid = 8 L)
+    // a segmented tile's quarters recorded their own continuous-equivalent trips (render_seg_kernel)
+    auto cost_at = [&](int t) -> uint32_t {
+        const uint32_t k = cost_in[t];
+        if (!(k & SEG_COST_FLAG) || !part_cost) return k & 0x7FFFu;
+        const uint2 q = *reinterpret_cast<const uint2 *>(part_cost + 4 * (size_t)t);
+        return max(max(q.x & 0xFFFFu, q.x >> 16), max(q.y & 0xFFFFu, q.y >> 16));
+    };
     // position e of this XCD's list is (column c = e / tiles_y, row e % tiles_y) of its
     // strips (strip_tile); the threads walk it in steps of ORDER_THREADS with one
     // division at the start instead of integer divisions per element (11.6 -> 9.7 us
@@ -1319,7 +1673,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     auto tile_of = [&](const Walk &w) { return w.r * tiles_x + strip_col(x, w.c); };
     uint32_t mx = 0, sum = 0;
     for (Walk w = start(); w.e < len; next(w)) {
-        const uint32_t k = cost[tile_of(w)];
+        const uint32_t k = cost_at(tile_of(w));
         mx = max(mx, k);
         sum += k;
     }
@@ -1351,30 +1705,48 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     auto cls = [mx](uint32_t k) {
         return 8 * k >= 7 * mx ? 0 : 4 * k >= 3 * mx ? 1 : 2 * k >= mx ? 2 : 4 * k >= mx ? 3 : 8 * k >= mx ? 4 : 5;
     };
-    for (Walk w = start(); w.e < len; next(w)) atomicAdd(&cnt[cls(cost[tile_of(w)])], 1u);
+    for (Walk w = start(); w.e < len; next(w)) atomicAdd(&cnt[cls(cost_at(tile_of(w)))], 1u);
     __syncthreads();
+    const int G = 8 * L;   // the grid, and where the class ends go
     if (tid == 0) {
-        uint32_t run = 0;
+        // seg_cap > 0: the tiles of the three classes >= max / 2 (heaviest first, at most
+        // seg_cap per XCD) take SEG_K consecutive slots each, one per quarter
+        uint32_t run = 0, left = (uint32_t)seg_cap;
         for (int c = 0; c < NC; ++c) {
+            segs[c] = c < seg_classes ? min(cnt[c], left) : 0u;
+            left -= segs[c];
             base[c] = run;
-            run += cnt[c];
-            if (c >= 2) order[n + 4 + 4 * x + (c - 2)] = run;   // prio class ends
+            rank[c] = 0;
+            run += cnt[c] + (SEG_K - 1) * segs[c];
+            if (c >= 2) order[G + 4 + 4 * x + (c - 2)] = run;   // prio class ends
         }
-        if (x == 0) for (int c = 0; c < 4; ++c) order[n + c] = 0;   // global bounds unused in this mode
+        base[NC] = run;
+        if (x == 0) for (int c = 0; c < 4; ++c) order[G + c] = 0;   // global bounds unused in this mode
     }
     __syncthreads();
     for (Walk w = start(); w.e < len; next(w)) {
         const int t = tile_of(w);
-        const uint32_t j = atomicAdd(&base[cls(cost[t])], 1u);
-        order[(size_t)j * 8 + x] = (uint32_t)t;
+        const int c = cls(cost_at(t));
+        const uint32_t r = atomicAdd(&rank[c], 1u);
+        if (r < segs[c]) {
+            const uint32_t j = base[c] + SEG_K * r;
+#pragma unroll
+            for (int q = 0; q < SEG_K; ++q) order[(size_t)(j + q) * 8 + x] = (uint32_t)t | ((uint32_t)(q + 1) << 28);
+        } else {
+            const uint32_t j = base[c] + (SEG_K - 1) * segs[c] + r;
+            order[(size_t)j * 8 + x] = (uint32_t)t;
+        }
     }
+    for (int j = (int)base[NC] + tid; j < L; j += ORDER_THREADS) order[(size_t)j * 8 + x] = SEG_EMPTY;
 }
 
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
-                               uint32_t *stats) {
+                               uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_classes) {
     if (n_tiles <= 0) return hipSuccess;
+    if (seg_cap > 0 && (n_tiles / tiles_x) * tiles_x != n_tiles) return hipErrorInvalidValue;
+    if (seg_cap > 0 && ((size_t)order_strips_grid(n_tiles, seg_cap) >> 28) != 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
-                       stats);
+                       stats, seg_cap, part_cost, seg_classes);
     return hipGetLastError();
 }
 

@@ -64,10 +64,11 @@ enum { STAGE_KERNEL = 0, STAGE_ASSEMBLE = 1, N_STAGES = 2 };
 // The tile-order cache key: the exact geometry (and deal) an order was built for.
 struct Geo {
     int width = -1, local_rows = -1, rows = -1, rank = -1, count = -1, xcd = -1, n_tiles = -1;
+    int seg = 0;   // the order's seg_cap (segmented heavy tiles, svo_kernel.hip render_seg_kernel)
     uint64_t deal = 0;
     bool operator==(const Geo &o) const {
         return width == o.width && local_rows == o.local_rows && rows == o.rows && rank == o.rank &&
-               count == o.count && xcd == o.xcd && n_tiles == o.n_tiles && deal == o.deal;
+               count == o.count && xcd == o.xcd && n_tiles == o.n_tiles && seg == o.seg && deal == o.deal;
     }
     bool operator!=(const Geo &o) const { return !(*this == o); }
 };
@@ -87,7 +88,11 @@ struct Sched {
     uint32_t *tile_order = nullptr;
     uint16_t *shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
     uint32_t *shadow_order = nullptr;
+    uint16_t *part_cost = nullptr;     // segmented tiles: per tile and quarter (4 x cap)
     size_t cap = 0;
+    size_t order_cap = 0;              // tile_order entries allocated
+    float4 *seg_hint = nullptr;        // segmented tiles: per pixel the segment starts (svo_traverse.h)
+    size_t hint_cap = 0;
     Geo order_key;                   // geometry tile_order was built for (width -1: none)
     Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
@@ -189,6 +194,11 @@ struct svo_ctx {
     int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
     int shadow_compact = 0;          // env SVO_SHADOW_COMPACT=1: that launch over the compacted hit list
     int lat_mode = -1;               // env SVO_LAT: 0 never, 1 always, unset: by the last launch's costs (see launch)
+    int seg_mode = 0;                // env SVO_SEG: 1 trace each XCD's heaviest tiles as segmented rays (see launch)
+    int seg_cap = 96;                // env SVO_SEG_CAP: at most this many segmented tiles per XCD
+    int seg_all = 0;                 // env SVO_SEG_ALL=1 (tests): every tile segmented
+    uint32_t seg_scramble = 0;       // env SVO_SEG_SCRAMBLE=<seed> (tests): arbitrary segment starts
+    uint32_t seg_launches = 0;
     double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold
     int move_every = 4;              // env SVO_MOVE_EVERY: while the camera moves every launch, rebuild the
                                      // order only every k-th launch (see launch; 1 = at every new view).
@@ -256,11 +266,14 @@ void free_sched(Sched &q) {
     if (q.tile_order) hipFree(q.tile_order);
     if (q.shadow_cost) hipFree(q.shadow_cost);
     if (q.shadow_order) hipFree(q.shadow_order);
+    if (q.part_cost) hipFree(q.part_cost);
     q.tile_cost = nullptr;
     q.tile_order = nullptr;
     q.shadow_cost = nullptr;
     q.shadow_order = nullptr;
+    q.part_cost = nullptr;
     q.cap = 0;
+    q.order_cap = 0;
     q.order_key = q.shadow_key = Geo();
 }
 
@@ -663,17 +676,36 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         key.xcd = p.xcd_remap;
         key.n_tiles = n_tiles;
         key.deal = b.key();
-        if (q->cap < (size_t)n_tiles) {
+        // segmented heavy tiles: primary rays of a tree pool in XCD-strip order
+        key.seg = (ctx->seg_mode || ctx->seg_all) && p.xcd_remap == 2 && !p.guard && p.shadows == 0 && !p.samples
+                      ? (ctx->seg_all ? (n_tiles + 7) / 8 : ctx->seg_cap) : 0;
+        const size_t order_need = svo::order_strips_entries(n_tiles, key.seg);
+        if (q->cap < (size_t)n_tiles || q->order_cap < order_need) {
             HIP_TRY(hipStreamSynchronize(s));   // a pending launch on this stream may still use the old buffers
             free_sched(*q);
             const size_t cap = svo::order_cost_capacity(n_tiles);
             HIP_TRY(hipMalloc(&q->tile_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(q->tile_cost, 0, cap * sizeof(uint16_t)));
-            HIP_TRY(hipMalloc(&q->tile_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&q->tile_order, order_need * sizeof(uint32_t)));
             HIP_TRY(hipMalloc(&q->shadow_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(q->shadow_cost, 0, cap * sizeof(uint16_t)));
             HIP_TRY(hipMalloc(&q->shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&q->part_cost, 4 * cap * sizeof(uint16_t)));
+            HIP_TRY(hipMemset(q->part_cost, 0, 4 * cap * sizeof(uint16_t)));
             q->cap = (size_t)n_tiles;
+            q->order_cap = order_need;
+        }
+        if (key.seg) {
+            const size_t px = (size_t)width * (size_t)p.local_rows;
+            if (q->hint_cap < px) {
+                HIP_TRY(hipStreamSynchronize(s));
+                if (q->seg_hint) hipFree(q->seg_hint);
+                q->seg_hint = nullptr;
+                q->hint_cap = 0;
+                HIP_TRY(hipMalloc(&q->seg_hint, px * sizeof(float4)));
+                HIP_TRY(hipMemset(q->seg_hint, 0xFF, px * sizeof(float4)));   // NaN: no starts yet
+                q->hint_cap = px;
+            }
         }
         if (!q->stats) {
             const size_t words = 16 * Sched::STATS_RING;
@@ -684,6 +716,12 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         }
         p.tile_order = q->order_key == key ? q->tile_order : nullptr;
         p.tile_cost = q->tile_cost;
+        p.part_cost = q->part_cost;
+        if (p.tile_order && key.seg) {   // the order lists quarter entries: the segmented kernel
+            p.seg = key.seg;
+            p.seg_hint = q->seg_hint;
+            if (ctx->seg_scramble) p.seg_scramble = ctx->seg_scramble * 0x9E3779B9u + ++ctx->seg_launches;
+        }
         if (p.shadows == 1 && ctx->shadow_order_enabled) {
             p.shadow_cost = q->shadow_cost;
             p.shadow_order = q->shadow_key == key ? q->shadow_order : nullptr;
@@ -707,7 +745,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // once per new view (svo_rt.h, svo_render_device).
     const int mode_now = p.shadows | (stack_mode << 2);
     p.lat = 0;
-    if (!p.guard && p.shadows == 0 && !p.out.fetches && !p.samples && ctx->lat_mode != 0) {
+    if (!p.guard && p.shadows == 0 && !p.out.fetches && !p.samples && !p.seg && ctx->lat_mode != 0) {
         if (ctx->lat_mode == 1) {
             p.lat = 1;
         } else if (q && q->stats && p.tile_order) {
@@ -790,7 +828,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
         const int r = q->stats_head;
         uint32_t *st16 = q->stats ? q->stats + 16 * r : nullptr;
-        e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s, st16)
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s, st16,
+                                                        key.seg, q->part_cost, ctx->seg_all ? 6 : 3)
                              : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s, st16);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         q->order_key = key;
@@ -1073,6 +1112,7 @@ int destroy_single(svo_ctx *ctx) {
     if (ctx->copy_stream2) hipStreamDestroy(ctx->copy_stream2);
     for (Sched &q : ctx->sched) {
         free_sched(q);
+        if (q.seg_hint) hipFree(q.seg_hint);
         if (q.done) hipEventDestroy(q.done);
         for (int r = 0; r < Sched::STATS_RING; ++r)
             if (q.stats_ev[r]) hipEventDestroy(q.stats_ev[r]);
@@ -1128,6 +1168,10 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_MOVE_EVERY")) ctx->move_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_LAT")) ctx->lat_mode = std::atoi(k) != 0 ? 1 : 0;
+    if (const char *k = std::getenv("SVO_SEG")) ctx->seg_mode = std::atoi(k) != 0 ? 1 : 0;
+    if (const char *k = std::getenv("SVO_SEG_CAP")) ctx->seg_cap = std::max(1, std::atoi(k));
+    if (const char *k = std::getenv("SVO_SEG_ALL")) ctx->seg_all = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_SEG_SCRAMBLE")) ctx->seg_scramble = (uint32_t)std::strtoul(k, nullptr, 10);
     if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
     if (e != hipSuccess) {
         destroy_single(ctx);

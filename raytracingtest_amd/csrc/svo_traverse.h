@@ -103,7 +103,23 @@ struct LaunchParams {
     float4 *accum;             // RGBA32F accumulation (out_index layout), read and written
     uint32_t *accum8;          // display RGBA8 of the blended pixels (nullable)
     uint8_t *accum_rgb8;       // the same as 3-byte RGB, the band payload (nullable)
+    // Segmented heavy tiles (svo_kernel.hip render_seg_kernel; seg != 0 only with an order built
+    // by launch_order_strips(..., seg_cap > 0)): an order entry t | (q + 1) << 28 is quarter q of
+    // tile t, traced as SEG_K t-segments per ray (lanes 4 r .. 4 r + 3 = ray r's segments);
+    // 0xFFFFFFFF is an empty slot.  seg_hint: per pixel (band-local lr * width + x) the segment
+    // starts t_1..t_3 of the ray's last segmented trace (NaN: none), rewritten by every such
+    // trace; part_cost: per tile and quarter the wave's continuous-equivalent trips (the tile's
+    // tile_cost then holds SEG_COST_FLAG).  seg = the order's seg_cap (0: no segmented tiles).
+    int seg;
+    float4 *seg_hint;
+    uint16_t *part_cost;
+    uint32_t seg_scramble;     // tests (env SVO_SEG_SCRAMBLE): != 0 replaces every start by a hash of
+                               // (pixel, this value) -- unordered, NaN, +-inf, outside the cube
 };
+
+constexpr int SEG_K = 4;                    // segments per ray (one lane quad)
+constexpr uint16_t SEG_COST_FLAG = 0x8000;  // tile_cost of a segmented tile: read part_cost
+constexpr uint32_t SEG_EMPTY = 0xFFFFFFFFu; // order slot with nothing to trace
 
 // Re-interleave the band parts of a split frame on the display device
 // (svo_assemble_frame): part m holds the rows of bands b with b % n_parts == m,
@@ -138,11 +154,19 @@ struct AssembleParams {
 hipError_t launch_order_tiles(const uint16_t *cost, uint32_t *order, int n_tiles, hipStream_t stream,
                               uint32_t *stats = nullptr);
 size_t order_cost_capacity(int n_tiles);
-// The same per XCD strip (xcd_remap 2): order must hold n_tiles + 36 entries.  stats
-// (nullable, 16 words, host-visible memory): per XCD x the max [2 x] and the sum [2 x + 1]
-// of its tiles' costs.
+// The same per XCD strip (xcd_remap 2): order must hold order_strips_entries(n_tiles, seg_cap)
+// entries.  stats (nullable, 16 words, host-visible memory): per XCD x the max [2 x] and the
+// sum [2 x + 1] of its tiles' costs.  seg_cap > 0: each XCD's tiles of cost >= half its
+// heaviest (at most seg_cap of them, heaviest classes first) are listed as SEG_K quarter
+// entries for render_seg_kernel, the lists padded to one length with SEG_EMPTY; a segmented
+// tile's cost is the max of its part_cost entries.  The render grid is then
+// order_strips_grid(n_tiles, seg_cap) workgroups.
+// seg_classes: how many of the six cost classes qualify (3: cost >= max / 2; 6: every tile).
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
-                               uint32_t *stats = nullptr);
+                               uint32_t *stats = nullptr, int seg_cap = 0, const uint16_t *part_cost = nullptr,
+                               int seg_classes = 3);
+inline int order_strips_grid(int n_tiles, int seg_cap) { return n_tiles + 8 * (SEG_K - 1) * seg_cap; }
+inline size_t order_strips_entries(int n_tiles, int seg_cap) { return (size_t)order_strips_grid(n_tiles, seg_cap) + 36; }
 
 // Progressive accumulation (AddShader blend) of an RGBA32F sample frame.
 hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32_t sample, int num_cus,

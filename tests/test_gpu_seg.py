@@ -1,0 +1,135 @@
+"""GPU parity of the segmented-ray form (svo_kernel.hip render_seg_kernel).
+
+A heavy tile's rays are traced as SEG_K t-segments side by side.  The
+form must give every output bit-identical to the continuous loop -- i.e. to the oracle's
+IntersectSVO (NVIDIASVO.compute:57-198) -- whatever the segment starts are.  Checked here
+with every tile segmented (SVO_SEG_ALL), with only the heavy classes (SVO_SEG, the form a
+launch uses), with arbitrary starts (SVO_SEG_SCRAMBLE: unordered, NaN, +-inf, outside the
+cube), over consecutive frames (the starts are rebalanced from frame to frame), a moving
+camera, a band of a split frame and the sparse payload's hit masks, in both stack modes.
+"""
+import numpy as np
+import pytest
+
+from raytracingtest_amd import RaytracingMaster
+from raytracingtest_amd.builder import build_menger
+from raytracingtest_amd.camera import CAMERAS, main_camera, main_light, overview_camera
+
+from test_gpu_frame import _bufs, _check, _oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    t = pytest.importorskip("torch")
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+@pytest.fixture(scope="module")
+def c3_svo():
+    from bench import CONFIGS
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    cfg = CONFIGS["C3"]
+    return build_sampler_svo(cfg["sampler"], cfg["max_level"], device=0)
+
+
+def _frames(torch, oracle_mod, svo, cams, w, h, mode, n_frames=3, keys=None):
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        for cam in cams:
+            m.UpdateShaderParameters(cam, w, h)
+            ref_hits, ref_rgba, ref_pos, ref_vox = _oracle(oracle_mod, svo, cam, w, h, mode)
+            for _ in range(n_frames):   # every frame rebalances the starts of the next one
+                b = _bufs(torch, w * h)
+                m.render_frame(w, h, stack_mode=mode, **{k: v.data_ptr() for k, v in b.items()
+                                                         if keys is None or k in keys})
+                m.synchronize()
+                _check(b, oracle_mod, ref_hits, ref_rgba, ref_pos, ref_vox, keys=keys)
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_every_tile_segmented_matches_oracle(torch, oracle_mod, monkeypatch, text_svo, mode):
+    """Every tile traced as 4 segments per ray: every output of every frame equals the oracle."""
+    monkeypatch.setenv("SVO_SEG_ALL", "1")
+    _frames(torch, oracle_mod, text_svo, [main_camera(), overview_camera()], 256, 256, mode)
+    _frames(torch, oracle_mod, build_menger(8), [overview_camera()], 480, 272, mode)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_arbitrary_segment_starts_match_oracle(torch, oracle_mod, monkeypatch, mode):
+    """Starts that are unordered, NaN, +-inf or outside the cube (a new hash every launch):
+    the records do not depend on them."""
+    monkeypatch.setenv("SVO_SEG_ALL", "1")
+    monkeypatch.setenv("SVO_SEG_SCRAMBLE", "12345")
+    _frames(torch, oracle_mod, build_menger(8), [overview_camera()], 480, 272, mode, n_frames=4,
+            keys=("hits", "rgba", "position", "voxel"))
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_c3_heavy_tiles_segmented_full_frame(torch, oracle_mod, monkeypatch, c3_svo, mode):
+    """The bench workload (C3, 1920x1080, flyover) with the launch's own rule (each XCD's tiles of
+    cost >= half its heaviest): six consecutive frames, every ray equal to the oracle's."""
+    monkeypatch.setenv("SVO_SEG", "1")
+    w, h = 1920, 1080
+    _frames(torch, oracle_mod, c3_svo, [CAMERAS["flyover"]()], w, h, mode, n_frames=6, keys=("hits", "rgba"))
+
+
+def test_c3_segmented_moving_camera(torch, oracle_mod, monkeypatch, c3_svo):
+    """A pan (a new view per frame, starts carried over from the previous view), then held."""
+    monkeypatch.setenv("SVO_SEG", "1")
+    monkeypatch.setenv("SVO_MOVE_EVERY", "1")
+    from raytracingtest_amd.camera import FLYOVER_EYE, FLYOVER_TARGET
+    w, h = 1920, 1080
+    cams = []
+    for i in range(5):
+        a = 0.01 * i
+        eye = (FLYOVER_EYE[0] + 2.0 * np.sin(a), FLYOVER_EYE[1], FLYOVER_EYE[2] + 2.0 * (1.0 - np.cos(a)))
+        cams.append(overview_camera(eye, FLYOVER_TARGET))
+    _frames(torch, oracle_mod, c3_svo, cams, w, h, 0, n_frames=2, keys=("hits", "rgba"))
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_segmented_band_and_hit_masks(torch, oracle_mod, monkeypatch, mode):
+    """Rank 1's band of an 8-way 8-row split (the strong split's per-GPU launch), with the sparse
+    payload's per-tile hit masks: records, RGB payload and masks equal the oracle's."""
+    monkeypatch.setenv("SVO_SEG_ALL", "1")
+    svo = build_menger(8)
+    w, h = 512, 384
+    cam = overview_camera()
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h, mode)
+    band = (8, 1, 8)
+    ys = np.concatenate([np.arange(y0, min(y0 + 8, h)) for y0 in range(8, h, 64)])
+    rows = len(ys)
+    n_tiles = (w // 8) * ((rows + 7) // 8)
+    want_hits = ref_hits.reshape(h, w)[ys].reshape(-1)
+    want_rgba = ref_rgba.reshape(h, w, 4)[ys].reshape(-1, 4)
+    hitpx = ((want_hits["flags"] & 1) != 0).reshape(rows, w)
+    want_masks = np.zeros(n_tiles, np.uint64)
+    for ty in range((rows + 7) // 8):
+        for tx in range(w // 8):
+            blk = hitpx[ty * 8:ty * 8 + 8, tx * 8:tx * 8 + 8]
+            mask = 0
+            for r, c in zip(*np.nonzero(blk)):   # lane (bit) = row * 8 + column of the tile
+                mask |= 1 << (int(r) * 8 + int(c))
+            want_masks[ty * (w // 8) + tx] = np.uint64(mask)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        for _ in range(3):
+            b = _bufs(torch, rows * w)
+            masks = torch.full((n_tiles,), -1, dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(), rgb8=b["rgb8"].data_ptr(),
+                           stack_mode=mode, band=band, hitmask=masks.data_ptr())
+            m.synchronize()
+            _check(b, oracle_mod, want_hits, want_rgba, keys=("hits", "rgba", "rgb8"))
+            assert np.array_equal(masks.cpu().numpy().view(np.uint64), want_masks), "hit masks differ"
+    finally:
+        m.close()

@@ -1,0 +1,77 @@
+"""A/B of the segmented heavy tiles on the C3 frame: render-kernel time of the
+whole 1920x1080 flyover frame (N = 1) and of rank 1's round-robin 8-row band at N = 2, 4, 8 (the
+strong split's per-GPU launch), with SVO_SEG off and on (and the latency form's automatic choice
+in both), interleaved in one process (the env is read when a context is created).  Library
+events, median of --timed launches after a warmup past the clock ramp.
+
+  python tools/seg_ab.py [--camera flyover] [--rounds 2] > gpurun_out/seg_ab.json
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--camera", default="flyover")
+    ap.add_argument("--timed", type=int, default=200)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--variants", default="off,on")
+    ap.add_argument("--caps", default="96")
+    a = ap.parse_args()
+    import torch
+    from bench import CONFIGS
+    from raytracingtest_amd import RaytracingMaster
+    from raytracingtest_amd.camera import CAMERAS
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    cfg = CONFIGS["C3"]
+    W, H = cfg["width"], cfg["height"]
+    svo = build_sampler_svo(cfg["sampler"], cfg["max_level"], device=0)
+    hits = torch.empty(W * H * 24, dtype=torch.uint8, device="cuda")
+    rgba = torch.empty(W * H * 16, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    out = {"camera": a.camera, "frame": f"{W}x{H}", "rows": []}
+    variants = []
+    for v in a.variants.split(","):
+        if v == "on":
+            variants += [("on", c) for c in a.caps.split(",")]
+        else:
+            variants.append((v, None))
+    for rnd in range(a.rounds):
+        for name, cap in variants:
+            os.environ["SVO_SEG"] = "1" if name == "on" else "0"
+            if cap:
+                os.environ["SVO_SEG_CAP"] = cap
+            rm = RaytracingMaster(device=0, capacity_nodes=len(svo))
+            rm.SetSVOBuffer(svo)
+            rm.UpdateShaderParameters(CAMERAS[a.camera](), W, H)
+            for _ in range(400):   # past the DVFS ramp
+                rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), stream=s.cuda_stream)
+            torch.cuda.synchronize()
+            for N in (1, 2, 4, 8):
+                band = None if N == 1 else (8, 1, N)
+                for _ in range(40):
+                    rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), band=band, stream=s.cuda_stream)
+                rm.set_kernel_timing(True)
+                rm.kernel_time()
+                for _ in range(a.timed):
+                    rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), band=band, stream=s.cuda_stream)
+                t = rm.stage_times()
+                rm.set_kernel_timing(False)
+                row = {"round": rnd, "seg": name, "cap": cap, "N": N, "kernel_ms_median": round(float(np.median(t)), 4),
+                       "kernel_ms_p10": round(float(np.percentile(t, 10)), 4)}
+                out["rows"].append(row)
+                print(json.dumps(row), file=sys.stderr, flush=True)
+            rm.close()
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
