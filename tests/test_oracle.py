@@ -307,7 +307,7 @@ def test_oracle_reproduces_c1_golden_frames(oracle_mod, text_svo, mode, camera_n
 
 
 def test_shadow_iteration_counts_diagnostic(oracle_mod, text_svo):
-    """COUNT_SHADOW_ITERS (tools/simd_efficiency.py): the per-pixel output counts the
+    """COUNT_SHADOW_ITERS (the r02 shadow-compaction model): the per-pixel output counts the
     shadow ray's loop iterations, 0 exactly where no shadow ray is traced; the
     records are the same as without the diagnostic."""
     from raytracingtest_amd.camera import main_camera, main_light

@@ -22,8 +22,11 @@ def main():
     ap.add_argument("--camera", default="flyover")
     ap.add_argument("--timed", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--variants", default="off,on")
-    ap.add_argument("--caps", default="96")
+    ap.add_argument("--variants", default="off,auto",
+                    help="comma list of: off (SVO_SEG=0), auto (the library's defaults), c<n> (SVO_SEG_CLASSES=n), "
+                         "i<n> (SVO_SEG_CLASSES_ISSUE=n)")
+    ap.add_argument("--cap", default=None, help="SVO_SEG_CAP")
+    ap.add_argument("--cameras", default=None, help="comma list (default: --camera)")
     a = ap.parse_args()
     import torch
     from bench import CONFIGS
@@ -37,39 +40,43 @@ def main():
     rgba = torch.empty(W * H * 16, dtype=torch.uint8, device="cuda")
     s = torch.cuda.Stream()
     torch.cuda.synchronize()
-    out = {"camera": a.camera, "frame": f"{W}x{H}", "rows": []}
-    variants = []
-    for v in a.variants.split(","):
-        if v == "on":
-            variants += [("on", c) for c in a.caps.split(",")]
-        else:
-            variants.append((v, None))
+    out = {"frame": f"{W}x{H}", "rows": []}
+    cams = (a.cameras or a.camera).split(",")
     for rnd in range(a.rounds):
-        for name, cap in variants:
-            os.environ["SVO_SEG"] = "1" if name == "on" else "0"
-            if cap:
-                os.environ["SVO_SEG_CAP"] = cap
-            rm = RaytracingMaster(device=0, capacity_nodes=len(svo))
-            rm.SetSVOBuffer(svo)
-            rm.UpdateShaderParameters(CAMERAS[a.camera](), W, H)
-            for _ in range(400):   # past the DVFS ramp
-                rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), stream=s.cuda_stream)
-            torch.cuda.synchronize()
-            for N in (1, 2, 4, 8):
-                band = None if N == 1 else (8, 1, N)
-                for _ in range(40):
-                    rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), band=band, stream=s.cuda_stream)
-                rm.set_kernel_timing(True)
-                rm.kernel_time()
-                for _ in range(a.timed):
-                    rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), band=band, stream=s.cuda_stream)
-                t = rm.stage_times()
-                rm.set_kernel_timing(False)
-                row = {"round": rnd, "seg": name, "cap": cap, "N": N, "kernel_ms_median": round(float(np.median(t)), 4),
-                       "kernel_ms_p10": round(float(np.percentile(t, 10)), 4)}
-                out["rows"].append(row)
-                print(json.dumps(row), file=sys.stderr, flush=True)
-            rm.close()
+        for name in a.variants.split(","):
+            for k in ("SVO_SEG", "SVO_SEG_CLASSES", "SVO_SEG_CLASSES_ISSUE", "SVO_SEG_CAP"):
+                os.environ.pop(k, None)
+            if name == "off":
+                os.environ["SVO_SEG"] = "0"
+            elif name.startswith("c"):     # c<n>: SVO_SEG_CLASSES (latency-bound launches)
+                os.environ["SVO_SEG_CLASSES"] = name[1:]
+            elif name.startswith("i"):     # i<n>: SVO_SEG_CLASSES_ISSUE (issue-bound launches)
+                os.environ["SVO_SEG_CLASSES_ISSUE"] = name[1:]"
+            if a.cap:
+                os.environ["SVO_SEG_CAP"] = a.cap
+            for cam in cams:
+                rm = RaytracingMaster(device=0, capacity_nodes=len(svo))
+                rm.SetSVOBuffer(svo)
+                rm.UpdateShaderParameters(CAMERAS[cam](), W, H)
+                for _ in range(400):   # past the DVFS ramp
+                    rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), stream=s.cuda_stream)
+                torch.cuda.synchronize()
+                for N in (1, 2, 4, 8):
+                    band = None if N == 1 else (8, 1, N)
+                    for _ in range(40):
+                        rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), band=band, stream=s.cuda_stream)
+                    rm.set_kernel_timing(True)
+                    rm.kernel_time()
+                    for _ in range(a.timed):
+                        rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), band=band, stream=s.cuda_stream)
+                    t = rm.stage_times()
+                    rm.set_kernel_timing(False)
+                    row = {"round": rnd, "variant": name, "camera": cam, "N": N,
+                           "kernel_ms_median": round(float(np.median(t)), 4),
+                           "kernel_ms_p10": round(float(np.percentile(t, 10)), 4)}
+                    out["rows"].append(row)
+                    print(json.dumps(row), file=sys.stderr, flush=True)
+                rm.close()
     print(json.dumps(out, indent=1))
 
 
