@@ -300,8 +300,10 @@ def main():
                           "whole step on the host clock between synchronizes, like value"}
     host_path = host_path_rates(rm, W, H, args) if world == 1 and args.steps > 0 and args.extras else None
     in_flight = frames_in_flight(rm, W, H, args, dev) if world == 1 and args.steps > 0 and args.extras else None
-    samples = (samples_in_flight(rm, W, H, args, dev, stream)
+    samples = (samples_in_flight(rm, W, H, args, dev, stream, floor_ms=m["floor_ms"])
                if world == 1 and args.steps > 0 and args.extras and not args.shadows else None)
+    split = (strong_split_bands(rm, W, H, args, dev, stream, hits, rgba, kern_ms, m["floor_ms"])
+             if world == 1 and args.steps > 0 and args.extras and not args.shadows else None)
     poses = None
     if world == 1 and args.extras and args.svo != "menger":
         poses = extra_poses(rm, args, W, H, hits, rgba, sptr, dev)
@@ -352,8 +354,12 @@ def main():
                          "hbm_frac": None if traffic is None else round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                          "l2_frac": round(achieved / L2_PEAK_GBS, 5),
                          "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
-                         "kernel": "render_tile_kernel (primary rays; library HIP events around that kernel alone, "
-                                   "K steps after the timed region)",
+                         "kernel_ms_events": round(m["kern_ms_events"], 4),
+                         "event_floor_ms": round(m["floor_ms"], 4),
+                         "kernel_ms_le_step": bool(kern_ms <= ms_per_step),
+                         "kernel": "render_seg_kernel / render_tile_kernel (the primary-ray launch; library HIP events "
+                                   "around that kernel alone, K steps after the timed region, minus event_floor_ms: "
+                                   "the same event pair around a one-element kernel on the same stream)",
                          "bound_note": "dependent node-fetch chain at 8 waves/SIMD (DESIGN.md 5.1); frac is the "
                                        "metric's algorithmic-bytes fraction of HBM peak, hbm_frac the PMC fabric "
                                        "bytes' (FETCH_SIZE x2 + WRITE_SIZE), l2_frac algorithmic bytes vs L2 peak",
@@ -366,12 +372,16 @@ def main():
                          # the same launch under the other accountings: node and
                          # attachment reads only, and the reference's 4-byte descriptor width
                          "read_frac": round((8 * F + 8 * n_hit) / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                         # SURVEY.md 8(d)'s own formula with the V2 node width: 8*F + 8*hits + 24*rays
+                         "frac_survey": round((8 * F + 8 * n_hit + 24 * n_px) / (kern_ms * 1e-3) / 1e9
+                                              / HBM_PEAK_GBS, 5),
                          "frac_ref_node_width": round((bytes_per_launch - 4 * F) / (kern_ms * 1e-3) / 1e9
                                                       / HBM_PEAK_GBS, 5),
                          "read_frac_ref_node_width": round((4 * F + 8 * n_hit) / (kern_ms * 1e-3) / 1e9
                                                            / HBM_PEAK_GBS, 5),
                          "accountings": "frac: 8-B V2 node fetches + attachment + hit record + RGBA32F (+ payload) "
-                                        "writes; read_frac: node + attachment reads only (8*F + 8*hits); "
+                                        "writes; frac_survey: SURVEY 8(d)'s 8*F + 8*hits + 24*rays; "
+                                        "read_frac: node + attachment reads only (8*F + 8*hits); "
                                         "*_ref_node_width: the same with the reference's 4-byte descriptors (4*F); "
                                         "hbm_frac: what the PMC counters saw cross the fabric",
                          "kernel_source_sha1": digest,
@@ -406,6 +416,8 @@ def main():
             out["frames_in_flight"] = in_flight
         if samples:
             out["samples_in_flight"] = samples
+        if split:
+            out["strong_split_rehearsal"] = split
         print(json.dumps(out), flush=True)
     rm.close()
     if world > 1:
@@ -485,11 +497,15 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     for i in range(args.steps):
         step()
     drain()
-    kern_ms, n_timed = rm.kernel_time()
+    kern_ms_events, n_timed = rm.kernel_time()
     rm.set_kernel_timing(False)
     torch.cuda.synchronize(dev)
     if n_timed != args.steps:
         raise RuntimeError(f"kernel timing: {n_timed} launches recorded, {args.steps} expected")
+    # the event pair's own cost (the bracketed kernel read longer than the step
+    # it belongs to): the same two hipEventRecords around a one-element kernel on the same stream
+    floor_ms = event_floor_ms(stream, dev)
+    kern_ms = max(kern_ms_events - floor_ms, 1e-6)
     host_hits = (hits if gather is None else gather.local_hits()).cpu().numpy().view(_lib.HIT_DTYPE)
     n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
     F = int(fetch[:n_px].to(torch.int64).sum().item())
@@ -514,7 +530,25 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     return dict(gather=gather, hits=hits, rgba=rgba, n_px=n_px, n_hit=n_hit, F=F, host_hits=host_hits, band=band,
                 deal_info=deal_info, payload_choice=payload_choice, bytes_per_launch=bytes_per_launch,
                 elapsed=elapsed, kern_ms=kern_ms, kern_ms_max=kern_ms_max, stages=stages, frame_check=frame_check,
-                per_rank=per_rank, step_ms=step_ms, step=step)
+                per_rank=per_rank, step_ms=step_ms, step=step, kern_ms_events=kern_ms_events, floor_ms=floor_ms)
+
+
+def event_floor_ms(stream, dev, n=200):
+    """Median time two hipEventRecords on `stream` read around a one-element kernel: what an event
+    bracket adds to the kernel it encloses (packet processing before the dispatch and the completion
+    signal after it), subtracted from the library's bracketed render-kernel time."""
+    import torch
+    x = torch.zeros(1, dtype=torch.float32, device=dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    with torch.cuda.stream(stream):
+        for _ in range(20):
+            x.add_(1.0)
+        for a, b in ev:
+            a.record(stream)
+            x.add_(1.0)
+            b.record(stream)
+    torch.cuda.synchronize(dev)
+    return float(np.median([a.elapsed_time(b) for a, b in ev]))
 
 
 def peer_matrix(devices):
@@ -1313,7 +1347,7 @@ def frames_in_flight(rm, W, H, args, dev, n_streams=3):
     return {"streams": n_streams, "ms_per_frame": round(ms, 4), "Mrays_per_s": round(W * H / (ms * 1e-3) / 1e6, 2)}
 
 
-def samples_in_flight(rm, W, H, args, dev, stream, sizes=(1, 2, 4, 8)):
+def samples_in_flight(rm, W, H, args, dev, stream, sizes=(1, 2, 4, 8), floor_ms=0.0):
     """Samples in flight on one GPU (svo_render_samples): a step traces S jittered samples
     of the frame in ONE launch (one wave per sample and 8x8 tile, cost-ordered) and blends
     them into the accumulation in _currentSample order (RaytracingMaster.cs:35,70-73,
@@ -1348,11 +1382,45 @@ def samples_in_flight(rm, W, H, args, dev, stream, sizes=(1, 2, 4, 8)):
             step()
         kern, _ = rm.kernel_time()
         rm.set_kernel_timing(False)
+        kern = max(kern - floor_ms, 1e-6)   # the event pair's own cost, as the render kernel's
         out[str(S)] = {"ms_per_step": round(ms, 4), "kernel_ms": round(kern, 4),
                        "Mrays_per_s": round(S * W * H / (ms * 1e-3) / 1e6, 2),
                        "kernel_Mrays_per_s": round(S * W * H / (kern * 1e-3) / 1e6, 2)}
     return {"per_samples": out, "outputs": "RGBA32F accumulation (read + written) + display RGBA8 of the blended frame",
             "note": "S jittered samples per launch, rays = S x W x H per step; primary rays only"}
+
+
+def strong_split_bands(rm, W, H, args, dev, stream, hits, rgba, kern_ms, floor_ms, counts=(2, 4, 8), timed=150):
+    """One-GPU rehearsal of the metric's frame split over N GPUs: every rank's
+    round-robin 8-row band of the same frame rendered alone on this GPU (the launch each GPU of an
+    N-way split runs, segmented heavy tiles and loop form chosen by the library as there), its
+    render-kernel time (library events minus the event floor, median of `timed` launches after a
+    warmup), and the predicted N-GPU speed-up of the one-sample frame = this run's kernel_ms over
+    the slowest rank's band.  The RCCL gather and display-rank assemble are not in it (they
+    overlap the next frame's render)."""
+    import torch
+    out = {}
+    for N in counts:
+        per = []
+        for r in range(N):
+            band = (8, r, N)
+            for _ in range(30):
+                rm.render_frame(W, H, hits=hits.data_ptr(), rgba=None if rgba is None else rgba.data_ptr(),
+                                stack_mode=args.stack_mode, band=band, stream=stream.cuda_stream)
+            rm.set_kernel_timing(True)
+            rm.kernel_time()
+            for _ in range(timed):
+                rm.render_frame(W, H, hits=hits.data_ptr(), rgba=None if rgba is None else rgba.data_ptr(),
+                                stack_mode=args.stack_mode, band=band, stream=stream.cuda_stream)
+            t = rm.stage_times()
+            rm.set_kernel_timing(False)
+            per.append(max(float(np.median(t)) - floor_ms, 1e-6))
+        torch.cuda.synchronize(dev)
+        out[str(N)] = {"band_kernel_ms_per_rank": [round(x, 4) for x in per], "slowest_rank_ms": round(max(per), 4),
+                       "predicted_speedup": round(kern_ms / max(per), 3)}
+    return {"per_gpus": out, "frame": f"{W}x{H}", "one_gpu_kernel_ms": round(kern_ms, 4),
+            "note": "each rank's round-robin 8-row band rendered alone on ONE GPU (hit records + RGBA32F), "
+                    "render kernel only; predicted_speedup = one_gpu_kernel_ms / slowest_rank_ms, gather excluded"}
 
 
 def host_path_rates(rm, W, H, args, n=5):
@@ -1361,7 +1429,9 @@ def host_path_rates(rm, W, H, args, n=5):
     and svo_render_progressive (sample rendered and accumulated on the GPU, the
     display RGBA8 frame to the host, 4 B/px) -- what the Unity host pays per frame."""
     out = {}
-    for name, fn, k in (("svo_render_rgba32f_hits", lambda: rm.Render(W, H, stack_mode=args.stack_mode), n),
+    reuse = rm.Render(W, H, stack_mode=args.stack_mode)   # a render loop's arrays, written again every frame
+    for name, fn, k in (("svo_render_rgba32f_hits", lambda: rm.Render(W, H, stack_mode=args.stack_mode, out=reuse), 10),
+                        ("svo_render_rgba32f_hits_fresh_arrays", lambda: rm.Render(W, H, stack_mode=args.stack_mode), n),
                         ("svo_render_progressive_rgba8", lambda: rm.RenderProgressive(W, H, stack_mode=args.stack_mode),
                          n),
                         # the pipelined entry point: a pointer to the previous frame in pinned memory

@@ -15,6 +15,10 @@
  *  - one context is driven from one host thread at a time; its asynchronous
  *    entry points take any hipStream_t, and renders on different streams run
  *    concurrently (per-stream dispatch-order state).
+ *  - a caller stream handed to a context stays alive until svo_forget_stream,
+ *    svo_synchronize or svo_destroy of that context: the context may later
+ *    record an event on it (when a fifth stream takes its dispatch-order state
+ *    over, or another stream takes the host-path scratch).
  */
 #ifndef SVO_RT_H
 #define SVO_RT_H
@@ -321,6 +325,11 @@ int svo_get_info(svo_ctx *ctx, size_t *n_nodes, int *max_depth, int *device);
  * caller stream it rendered, assembled or accumulated on (a device-wide
  * synchronise of each of its devices). */
 int svo_synchronize(svo_ctx *ctx);
+
+/* Let go of a caller stream before the caller destroys it: waits for the work the
+ * context enqueued on it and frees the stream's dispatch-order state (a multi-device
+ * context: every member).  A stream never passed in is not an error.  (ABI 9) */
+int svo_forget_stream(svo_ctx *ctx, void *stream);
 
 /* Release device memory (the reference never Release()s its buffers). */
 int svo_destroy(svo_ctx *ctx);

@@ -27,7 +27,7 @@ assert HIT_DTYPE.itemsize == 24
 COMPACT_DTYPE = np.dtype([("parent", "<u4"), ("meta", "<u4"), ("t", "<f4")])   # svo_hit_compact
 assert COMPACT_DTYPE.itemsize == 12
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
@@ -35,7 +35,7 @@ EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera"
            "svo_kernel_time", "svo_create_multi", "svo_num_devices", "svo_get_member", "svo_render_frame",
            "svo_assemble_frame", "svo_stage_time", "svo_render_progressive", "svo_set_band_deal",
            "svo_pack_hits", "svo_get_member_link", "svo_stage_times", "svo_render_samples",
-           "svo_render_progressive_async", "svo_progressive_last")
+           "svo_render_progressive_async", "svo_progressive_last", "svo_forget_stream")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
@@ -137,6 +137,7 @@ def lib():
         "svo_set_band_deal": [vp, i, ctypes.POINTER(ctypes.c_uint8)],
         "svo_pack_hits": [vp, i, i, ctypes.POINTER(SvoBand), vp, vp, vp],
         "svo_synchronize": [vp],
+        "svo_forget_stream": [vp, vp],
         "svo_destroy": [vp],
         "svo_last_error": [],
         "svo_abi_version": [],

@@ -594,7 +594,7 @@ __device__ __forceinline__ void record(const LaunchParams &p, const Ray &r, int 
     o.w[4] = (uint32_t)__float_as_int(n[1]);
     o.w[5] = (uint32_t)__float_as_int(n[2]);
     o.rgb[0] = o.rgb[1] = o.rgb[2] = 0.0f;
-    if (p.out.rgba || p.out.rgba8 || p.out.rgb8) {
+    if (p.out.rgba || p.out.rgba8 || p.out.rgb8 || p.out.accum) {
         float alb[3];
         decode_dxt(a.x, a.y, hit_idx, alb);
         shade_hit(p.cam, n, alb, o.rgb);
@@ -643,8 +643,20 @@ __device__ __forceinline__ void store_outputs(const Outputs &out, size_t i, cons
         __builtin_nontemporal_store(u32x3{o.w[0], o.w[1], o.w[2]}, reinterpret_cast<u32x3 *>(out.compact + 3 * i));
     if (out.rgba)
         __builtin_nontemporal_store(f32x4{o.rgb[0], o.rgb[1], o.rgb[2], 1.0f}, reinterpret_cast<f32x4 *>(out.rgba + i));
+    float dr = o.rgb[0], dg = o.rgb[1], db = o.rgb[2];   // the colour the display words carry
+    if (out.accum) {   // accumulate_kernel's blend (AddShader.shader:44-47), the Result alpha is a
+        const float4 d0 = out.accum[i];
+        const float a = out.acc_a, b = out.acc_b;
+        f32x4 d;
+        d.x = o.rgb[0] * a + d0.x * b;
+        d.y = o.rgb[1] * a + d0.y * b;
+        d.z = o.rgb[2] * a + d0.z * b;
+        d.w = a * a + d0.w * b;
+        __builtin_nontemporal_store(d, reinterpret_cast<f32x4 *>(out.accum + i));
+        dr = d.x; dg = d.y; db = d.z;
+    }
     if (out.rgba8 || out.rgb8) {
-        const uint32_t w = pack_rgba8(o.rgb[0], o.rgb[1], o.rgb[2]);
+        const uint32_t w = pack_rgba8(dr, dg, db);
         if (out.rgba8) __builtin_nontemporal_store(w, out.rgba8 + i);
         if (out.rgb8) {
             uint8_t *d = out.rgb8 + 3 * i;
@@ -1034,8 +1046,9 @@ __device__ __forceinline__ float4 seg_rebalance(float t_entry, float t_start, fl
 // rays x SEG_K segments (lanes 4 r + k), and writes every output of those 16 pixels from the
 // lane of the segment that holds the record.  Every other entry is one tile, traced as in
 // render_tile_kernel (lean loop, primary rays).  A quarter's chain is its longest segment:
-// ~1/K of the tile's continuous chain plus the walk to t_k.
-template <int MODE, bool FA>
+// ~1/K of the tile's continuous chain plus the walk to t_k.  LAT: whole tiles take the
+// latency form (trace_lat, twice the LDS), as a latency-bound launch without segments would.
+template <int MODE, bool FA, bool LAT>
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))) void render_seg_kernel(LaunchParams p, int tiles_x) {
     extern __shared__ uint2 stk_base[];
     const int lane = threadIdx.x;
@@ -1065,7 +1078,8 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
         }
         FRay f;
         to_fray(r, f);
-        trace_lean<MODE, false, false, FA>(p, f, stk);
+        if (LAT) trace_lat<MODE>(p, f, stk);
+        else trace_lean<MODE, false, false, FA>(p, f, stk);
         from_fray(f, r);
         Record o;
         record(p, r, x, gy, o);
@@ -1176,11 +1190,11 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
                 : p.xcd_remap == 2 ? strip_tile((int)blockIdx.x % 8, (int)blockIdx.x / 8, tiles_x, n_tiles / tiles_x)
                                    : (int)blockIdx.x;
     const int bx = t % tiles_x, by = t / tiles_x;
-    const int x = bx * 8 + (lane & 7);
-    const int lr = by * 8 + (lane >> 3);
-    // every wave of the workgroup covers the same pixels: a lane out of the frame leaves in all
-    // of them, so the barrier below sees the same lanes from each wave
-    if (x >= p.width || lr >= p.local_rows) return;
+    // a lane out of the frame traces a copy of an inside pixel and stores nothing: every lane of
+    // every wave reaches the barrier below (no reliance on partially exited waves)
+    const bool inside = bx * 8 + (lane & 7) < p.width && by * 8 + (lane >> 3) < p.local_rows;
+    const int x = min(bx * 8 + (lane & 7), p.width - 1);
+    const int lr = min(by * 8 + (lane >> 3), p.local_rows - 1);
     if (p.tile_order && p.prio) {
         const uint32_t n = gridDim.x;
         const bool strips = p.xcd_remap == 2;
@@ -1205,7 +1219,7 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
     // wave 0 loads its pixels' accumulation before tracing, so the load's latency is hidden by
     // the trace instead of holding the wave's slot at its end
     float4 dprev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (k == 0) dprev = p.accum[out_index(p, lr, gy, x)];
+    if (k == 0 && inside) dprev = p.accum[out_index(p, lr, gy, x)];
     FRay f;
     to_fray(r, f);
     if (p.guard) trace_lean<MODE, true>(p, f, stk);
@@ -1218,7 +1232,7 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
     float4 *col = reinterpret_cast<float4 *>(stk_base + (size_t)k * region);
     col[lane] = make_float4(o.rgb[0], o.rgb[1], o.rgb[2], 1.0f);
     __syncthreads();
-    if (k != 0) return;
+    if (k != 0 || !inside) return;
     const size_t i = out_index(p, lr, gy, x);
     float4 d = dprev;
     for (int j = 0; j < p.samples; ++j) {   // accumulate_kernel's blend, sample j after sample j - 1
@@ -1494,10 +1508,12 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
     }
     if (!COUNT && p.seg > 0) {   // segmented heavy tiles (the order was built with seg_cap = p.seg)
         const dim3 sgrid((unsigned)order_strips_grid(bx * by, p.seg));
-        if (p.fetch_all)
-            hipLaunchKernelGGL((render_seg_kernel<MODE, true>), sgrid, block, lds, stream, p, bx);
+        if (p.lat)
+            hipLaunchKernelGGL((render_seg_kernel<MODE, true, true>), sgrid, block, 2 * lds, stream, p, bx);
+        else if (p.fetch_all)
+            hipLaunchKernelGGL((render_seg_kernel<MODE, true, false>), sgrid, block, lds, stream, p, bx);
         else
-            hipLaunchKernelGGL((render_seg_kernel<MODE, false>), sgrid, block, lds, stream, p, bx);
+            hipLaunchKernelGGL((render_seg_kernel<MODE, false, false>), sgrid, block, lds, stream, p, bx);
         return hipGetLastError();
     }
     if (COUNT)

@@ -26,11 +26,16 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "svo_rt.h"
@@ -64,11 +69,13 @@ enum { STAGE_KERNEL = 0, STAGE_ASSEMBLE = 1, N_STAGES = 2 };
 // The tile-order cache key: the exact geometry (and deal) an order was built for.
 struct Geo {
     int width = -1, local_rows = -1, rows = -1, rank = -1, count = -1, xcd = -1, n_tiles = -1;
-    int seg = 0;   // the order's seg_cap (segmented heavy tiles, svo_kernel.hip render_seg_kernel)
+    int seg = 0;    // the order's seg_cap (segmented heavy tiles, svo_kernel.hip render_seg_kernel) ...
+    int segc = 0;   // ... and how many cost classes it segments
     uint64_t deal = 0;
     bool operator==(const Geo &o) const {
         return width == o.width && local_rows == o.local_rows && rows == o.rows && rank == o.rank &&
-               count == o.count && xcd == o.xcd && n_tiles == o.n_tiles && seg == o.seg && deal == o.deal;
+               count == o.count && xcd == o.xcd && n_tiles == o.n_tiles && seg == o.seg && segc == o.segc &&
+               deal == o.deal;
     }
     bool operator!=(const Geo &o) const { return !(*this == o); }
 };
@@ -84,16 +91,30 @@ struct Sched {
     bool used = false;
     unsigned long long last_use = 0;
     hipEvent_t done = nullptr;       // eviction: recorded on this stream when another takes the set over
-    uint16_t *tile_cost = nullptr;
-    uint32_t *tile_order = nullptr;
+    // The dispatch order is built OFF the render stream (round 5): after launch n
+    // the order kernel runs on `side` (behind an event on the render stream) from the costs launch n
+    // wrote, into one of two order buffers, and the first launch to dispatch in it is n + 2 -- so
+    // launch n + 1 never waits for it.  Launch n writes its costs into buffer n % 2 (the build
+    // after launch n reads them while launch n + 1 writes the other one); a launch waits on the
+    // build event of a build it follows by >= 2 launches once, before its kernel, and only if the
+    // host has not already seen that build complete (a held view: never).
+    uint16_t *cost_buf[2] = {};
+    uint16_t *part_buf[2] = {};          // segmented tiles: per tile and quarter (4 x cap)
+    uint32_t *order_buf[2] = {};
+    hipStream_t side = nullptr;
+    hipEvent_t render_done = nullptr;    // recorded on the render stream behind a launch a build follows
+    hipEvent_t build_ev[2] = {};
+    long long build_at[2] = {-1, -1};    // the launch after which buffer i's order was built (-1: none)
+    bool build_seen[2] = {};             // the render stream already waits for it (or it completed)
+    Geo build_key[2];
+    int next_buf = 0;
     uint16_t *shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
     uint32_t *shadow_order = nullptr;
-    uint16_t *part_cost = nullptr;     // segmented tiles: per tile and quarter (4 x cap)
     size_t cap = 0;
-    size_t order_cap = 0;              // tile_order entries allocated
+    size_t order_cap = 0;              // order_buf entries allocated
     float4 *seg_hint = nullptr;        // segmented tiles: per pixel the segment starts (svo_traverse.h)
     size_t hint_cap = 0;
-    Geo order_key;                   // geometry tile_order was built for (width -1: none)
+    Geo order_key;                   // the newest build's key (width -1: none)
     Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
     unsigned long long built_view = 0;   // the context's view generation the order was built under
@@ -129,11 +150,68 @@ struct Peer {                       // one per member of a multi-device context 
     size_t dense_cap = 0;
     float4 *accum = nullptr;             // svo_render_samples: this member's band accumulation (band layout)
     int accum_w = 0, accum_rows = -1;
+    uint64_t accum_deal = 0;             // the band deal its rows belong to
     int link = SVO_LINK_SELF;            // how the payload reaches the display device (svo_get_member_link)
     void *local[2] = {nullptr, nullptr}; // SVO_LINK_COPY: the payload's copy on the display device
     size_t local_cap = 0;
 };
 
+
+// Host threads that move svo_render's outputs from the plugin's pinned staging into the
+// caller's (pageable) arrays, chunk by chunk, while the DMA of the next chunk runs.
+class CopyPool {
+  public:
+    explicit CopyPool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    void submit(void *dst, const void *src, size_t n) {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            q_.push_back(Job{static_cast<char *>(dst), static_cast<const char *>(src), n});
+            ++pending_;
+        }
+        cv_.notify_one();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [this] { return pending_ == 0; });
+    }
+
+  private:
+    struct Job { char *dst; const char *src; size_t n; };
+    void run() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> l(m_);
+                cv_.wait(l, [this] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;
+                j = q_.front();
+                q_.pop_front();
+            }
+            std::memcpy(j.dst, j.src, j.n);
+            {
+                std::lock_guard<std::mutex> l(m_);
+                if (--pending_ == 0) done_.notify_all();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    std::deque<Job> q_;
+    size_t pending_ = 0;
+    bool stop_ = false;
+};
 
 }  // namespace
 
@@ -157,6 +235,12 @@ struct svo_ctx {
     size_t shadow_list_cap = 0;
     void *d_out_rgba = nullptr;
     size_t out_cap_px = 0;
+    // svo_render: pinned staging of the outputs, its per-chunk events, and the host copy threads
+    void *h_stage = nullptr;
+    size_t h_stage_cap = 0;
+    static constexpr int STAGE_CHUNKS = 16;
+    hipEvent_t stage_ev[STAGE_CHUNKS] = {};
+    std::unique_ptr<CopyPool> copy_pool;
     // svo_render_progressive: the accumulated frame (RGBA32F, zeroed on a size
     // change) and its RGBA8 display words
     float4 *d_accum = nullptr;
@@ -179,6 +263,7 @@ struct svo_ctx {
     hipEvent_t pin_copied2[PIN_SLOTS] = {};
     unsigned long long pin_frames = 0;   // frames enqueued since the slots were (re)allocated
     int num_cus = 256;
+    size_t lds_per_block = 160 * 1024;   // hipDeviceProp.sharedMemPerBlock
     int xcd_remap = 2;               // env SVO_XCD_REMAP: 2 interleaved column strips (default), 0 raster
     uint32_t options = 0;            // svo_set_options
     // SVO_OPT_KERNEL_TIMING: event pairs around the primary kernel / the assemble kernel
@@ -194,7 +279,11 @@ struct svo_ctx {
     int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
     int shadow_compact = 0;          // env SVO_SHADOW_COMPACT=1: that launch over the compacted hit list
     int lat_mode = -1;               // env SVO_LAT: 0 never, 1 always, unset: by the last launch's costs (see launch)
-    int seg_mode = 0;                // env SVO_SEG: 1 trace each XCD's heaviest tiles as segmented rays (see launch)
+    int seg_mode = 1;                // env SVO_SEG=0: never trace heavy tiles as segmented rays (see launch)
+    int seg_classes = 3;             // env SVO_SEG_CLASSES: cost classes segmented in a latency-bound launch (3: the
+                                     // tiles of cost >= max / 2)
+    int seg_classes_issue = 1;       // env SVO_SEG_CLASSES_ISSUE: the same in an issue-bound launch (1: >= 7/8 max;
+                                     // 0: none)
     int seg_cap = 96;                // env SVO_SEG_CAP: at most this many segmented tiles per XCD
     int seg_all = 0;                 // env SVO_SEG_ALL=1 (tests): every tile segmented
     uint32_t seg_scramble = 0;       // env SVO_SEG_SCRAMBLE=<seed> (tests): arbitrary segment starts
@@ -226,6 +315,8 @@ struct svo_ctx {
     int deal_cycle = 0;                  // svo_set_band_deal: weighted deal over the members (0: round-robin)
     int sparse_payload = 0;              // env SVO_SPARSE_PAYLOAD=1: display-only frames travel as sparse parts
     uint8_t deal_owner[svo::MAX_CYCLE] = {};
+    uint64_t samples_deal = 0;           // the deal of the last svo_render_samples (band accumulations' rows)
+    bool samples_deal_set = false;
 };
 
 namespace {
@@ -248,33 +339,42 @@ __global__ void convert_v1_kernel(const int32_t *__restrict__ desc, uint2 *__res
 // Make stream s wait for the work the previous scratch user enqueued on another stream.
 int order_scratch(svo_ctx *ctx, hipStream_t s) {
     if (ctx->scratch_valid && ctx->scratch_stream != s) {
+        // the previous stream is alive: a caller keeps its streams until svo_forget_stream /
+        // svo_synchronize / svo_destroy (svo_rt.h)
         if (!ctx->switch_event) HIP_TRY(hipEventCreateWithFlags(&ctx->switch_event, hipEventDisableTiming));
-        if (hipEventRecord(ctx->switch_event, ctx->scratch_stream) == hipSuccess) {
-            HIP_TRY(hipStreamWaitEvent(s, ctx->switch_event, 0));
-        } else {   // the previous stream is gone: wait for the whole device instead
-            (void)hipGetLastError();
-            HIP_TRY(hipDeviceSynchronize());
-        }
+        HIP_TRY(hipEventRecord(ctx->switch_event, ctx->scratch_stream));
+        HIP_TRY(hipStreamWaitEvent(s, ctx->switch_event, 0));
     }
     ctx->scratch_stream = s;
     ctx->scratch_valid = true;
     return SVO_OK;
 }
 
+// Forget every order build of the set (the buffers stay; the caller has synchronised).
+void reset_builds(Sched &q) {
+    for (int i = 0; i < 2; ++i) {
+        q.build_at[i] = -1;
+        q.build_seen[i] = false;
+        q.build_key[i] = Geo();
+    }
+    q.order_key = q.shadow_key = Geo();
+}
+
 void free_sched(Sched &q) {
-    if (q.tile_cost) hipFree(q.tile_cost);
-    if (q.tile_order) hipFree(q.tile_order);
+    for (int i = 0; i < 2; ++i) {
+        if (q.cost_buf[i]) hipFree(q.cost_buf[i]);
+        if (q.part_buf[i]) hipFree(q.part_buf[i]);
+        if (q.order_buf[i]) hipFree(q.order_buf[i]);
+        q.cost_buf[i] = q.part_buf[i] = nullptr;
+        q.order_buf[i] = nullptr;
+    }
     if (q.shadow_cost) hipFree(q.shadow_cost);
     if (q.shadow_order) hipFree(q.shadow_order);
-    if (q.part_cost) hipFree(q.part_cost);
-    q.tile_cost = nullptr;
-    q.tile_order = nullptr;
     q.shadow_cost = nullptr;
     q.shadow_order = nullptr;
-    q.part_cost = nullptr;
     q.cap = 0;
     q.order_cap = 0;
-    q.order_key = q.shadow_key = Geo();
+    reset_builds(q);
 }
 
 // The scheduling state of stream s: its own set, or a free one, or the least recently
@@ -294,15 +394,13 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         // s takes over the set only after the renders the evicted stream was given: an event
         // recorded on that stream NOW stands behind all of them (host order = stream order).
         // Recorded here, at the rare eviction, not behind every launch: a marker packet
-        // between two renders of one stream cost ~2-3 us of GPU time per frame.
+        // between two renders of one stream cost ~2-3 us of GPU time per frame.  The evicted
+        // stream is alive: callers keep a stream until svo_forget_stream (svo_rt.h).
         if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
-        if (hipEventRecord(pick->done, pick->stream) == hipSuccess) {
-            HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
-        } else {   // that stream is gone (destroyed by its owner): wait for the whole device
-            (void)hipGetLastError();
-            HIP_TRY(hipDeviceSynchronize());
-        }
-        pick->order_key = pick->shadow_key = Geo();   // built for another stream's frames
+        HIP_TRY(hipEventRecord(pick->done, pick->stream));
+        HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
+        if (pick->side) HIP_TRY(hipStreamSynchronize(pick->side));   // its order builds (rare: an eviction)
+        reset_builds(*pick);   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
         pick->view_prev = ~0ull;
         pick->built_cost = ~0ull;
@@ -589,6 +687,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     HIP_TRY(hipSetDevice(ctx->device));
     svo::LaunchParams p;
     std::memset(&p, 0, sizeof p);
+    bool jittered = false;   // per-launch pixel offsets: the tiles' costs drift without a new view
     p.nodes = ctx->d_nodes;
     p.att = ctx->d_att;
     p.n_nodes = (uint32_t)std::min<size_t>(ctx->n_nodes, 0xFFFFFFFFu);
@@ -616,7 +715,30 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.xcd_remap = ctx->xcd_remap;
     if (p.xcd_remap == 2 && ((width + 7) / 8) % (8 * svo::STRIP_K) != 0) p.xcd_remap = 0;
     p.shadows = (ctx->options & SVO_OPT_SHADOW_RAYS) ? (ctx->shadow_compact ? 3 : ctx->fused_shadows ? 2 : 1) : 0;
+    if (sa && sa->n == 1) {
+        // one sample: the one-sample launch itself with AddShader's blend in its store epilogue (the
+        // samples kernel's S waves per tile, barrier and blend loop cost S = 1 ~13 %)
+        std::memset(&p.out, 0, sizeof p.out);
+        p.out.accum = sa->accum;
+        p.out.acc_a = 1.0f / ((float)sa->first + 1.0f);   // launch_accumulate's a and b, _Sample = first
+        p.out.acc_b = 1.0f - p.out.acc_a;
+        p.out.rgba8 = sa->rgba8;
+        p.out.rgb8 = sa->rgb8;
+        p.out.frame_layout = sa->layout == SVO_LAYOUT_FRAME && b.count > 1 ? 1 : 0;
+        p.cam.px_off[0] = sa->offsets[0];   // this sample's _PixelOffset
+        p.cam.px_off[1] = sa->offsets[1];
+        p.shadows = 0;
+        jittered = true;
+        sa = nullptr;
+    }
     if (sa) {   // samples in flight: primary rays only, the blend replaces every other output
+        // S stack regions of max(slots, 2) x 64 x 8 bytes in one workgroup (svo_kernel.hip)
+        const size_t lds = (size_t)std::max(p.slots, 2) * svo::TILE * sizeof(uint2) * (size_t)sa->n;
+        if (lds > ctx->lds_per_block)
+            return fail(SVO_ERR_ARG, "svo_render_samples: " + std::to_string(sa->n) + " samples of a depth-" +
+                                         std::to_string(ctx->depth) + " pool need " + std::to_string(lds) +
+                                         " bytes of LDS per workgroup, the device allows " +
+                                         std::to_string(ctx->lds_per_block) + ": use fewer samples per launch");
         p.samples = sa->n;
         for (int k = 0; k < sa->n; ++k) {
             p.sample_off[k][0] = sa->offsets[2 * k];
@@ -661,7 +783,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     p.prio = ctx->prio;
     const bool ordered = ctx->tile_order && !p.out.fetches;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
-    Geo key;
+    Geo key;        // the geometry (seg 0): the key of the costs and of the loop-form decision
+    Geo okey;       // the order's key: key + the seg_cap its order was built with
+    int seg_cap = 0;
     Sched *q = nullptr;
     if (ordered) {
         rc = sched_for(ctx, s, &q);
@@ -677,25 +801,33 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         key.n_tiles = n_tiles;
         key.deal = b.key();
         // segmented heavy tiles: primary rays of a tree pool in XCD-strip order
-        key.seg = (ctx->seg_mode || ctx->seg_all) && p.xcd_remap == 2 && !p.guard && p.shadows == 0 && !p.samples
+        seg_cap = (ctx->seg_mode || ctx->seg_all) && p.xcd_remap == 2 && !p.guard && p.shadows == 0 && !p.samples
                       ? (ctx->seg_all ? (n_tiles + 7) / 8 : ctx->seg_cap) : 0;
-        const size_t order_need = svo::order_strips_entries(n_tiles, key.seg);
+        const size_t order_need = svo::order_strips_entries(n_tiles, seg_cap);
+        if (!q->side) {
+            HIP_TRY(hipStreamCreateWithFlags(&q->side, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&q->render_done, hipEventDisableTiming));
+            for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&q->build_ev[i], hipEventDisableTiming));
+        }
         if (q->cap < (size_t)n_tiles || q->order_cap < order_need) {
             HIP_TRY(hipStreamSynchronize(s));   // a pending launch on this stream may still use the old buffers
+            HIP_TRY(hipStreamSynchronize(q->side));   // ... or an order build
             free_sched(*q);
             const size_t cap = svo::order_cost_capacity(n_tiles);
-            HIP_TRY(hipMalloc(&q->tile_cost, cap * sizeof(uint16_t)));
-            HIP_TRY(hipMemset(q->tile_cost, 0, cap * sizeof(uint16_t)));
-            HIP_TRY(hipMalloc(&q->tile_order, order_need * sizeof(uint32_t)));
+            for (int i = 0; i < 2; ++i) {
+                HIP_TRY(hipMalloc(&q->cost_buf[i], cap * sizeof(uint16_t)));
+                HIP_TRY(hipMemset(q->cost_buf[i], 0, cap * sizeof(uint16_t)));
+                HIP_TRY(hipMalloc(&q->part_buf[i], 4 * cap * sizeof(uint16_t)));
+                HIP_TRY(hipMemset(q->part_buf[i], 0, 4 * cap * sizeof(uint16_t)));
+                HIP_TRY(hipMalloc(&q->order_buf[i], order_need * sizeof(uint32_t)));
+            }
             HIP_TRY(hipMalloc(&q->shadow_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(q->shadow_cost, 0, cap * sizeof(uint16_t)));
             HIP_TRY(hipMalloc(&q->shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
-            HIP_TRY(hipMalloc(&q->part_cost, 4 * cap * sizeof(uint16_t)));
-            HIP_TRY(hipMemset(q->part_cost, 0, 4 * cap * sizeof(uint16_t)));
             q->cap = (size_t)n_tiles;
             q->order_cap = order_need;
         }
-        if (key.seg) {
+        if (seg_cap) {
             const size_t px = (size_t)width * (size_t)p.local_rows;
             if (q->hint_cap < px) {
                 HIP_TRY(hipStreamSynchronize(s));
@@ -714,14 +846,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             for (int r = 0; r < Sched::STATS_RING; ++r)
                 HIP_TRY(hipEventCreateWithFlags(&q->stats_ev[r], hipEventDisableTiming));
         }
-        p.tile_order = q->order_key == key ? q->tile_order : nullptr;
-        p.tile_cost = q->tile_cost;
-        p.part_cost = q->part_cost;
-        if (p.tile_order && key.seg) {   // the order lists quarter entries: the segmented kernel
-            p.seg = key.seg;
-            p.seg_hint = q->seg_hint;
-            if (ctx->seg_scramble) p.seg_scramble = ctx->seg_scramble * 0x9E3779B9u + ++ctx->seg_launches;
-        }
+        p.tile_cost = q->cost_buf[q->launches & 1];   // this launch's costs (see Sched)
+        p.part_cost = q->part_buf[q->launches & 1];
         if (p.shadows == 1 && ctx->shadow_order_enabled) {
             p.shadow_cost = q->shadow_cost;
             p.shadow_order = q->shadow_key == key ? q->shadow_order : nullptr;
@@ -743,12 +869,17 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // The costs (and so the decision) are keyed on the render mode too: a shadowed launch's
     // tile costs include its shadow trips.  The wait can block the host for up to a frame,
     // once per new view (svo_rt.h, svo_render_device).
+    // The same statistics decide whether the heaviest tiles are traced as segmented rays
+    // (SVO_SEG unset: exactly when the launch is latency-bound, i.e. its heaviest chain and not
+    // its issued work bounds it -- a strong split's band).
     const int mode_now = p.shadows | (stack_mode << 2);
     p.lat = 0;
-    if (!p.guard && p.shadows == 0 && !p.out.fetches && !p.samples && !p.seg && ctx->lat_mode != 0) {
+    bool latency_bound = false;
+    const bool have_order = q && [&] { Geo g = q->order_key; g.seg = g.segc = 0; return g == key; }();
+    if (!p.guard && p.shadows == 0 && !p.out.fetches && !p.samples && (ctx->lat_mode != 0 || seg_cap)) {
         if (ctx->lat_mode == 1) {
-            p.lat = 1;
-        } else if (q && q->stats && p.tile_order) {
+            latency_bound = true;
+        } else if (q && q->stats && have_order) {
             // the newest pending build first: wait for it if it is this view's and this view has
             // no decision yet (once per view), else take the newest build that has completed
             // (stream order: then every older one has too) and drop the older ones
@@ -761,7 +892,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 const hipError_t st = wait ? hipEventSynchronize(q->stats_ev[r]) : hipEventQuery(q->stats_ev[r]);
                 if (st == hipErrorNotReady) continue;
                 if (st != hipSuccess) return fail(SVO_ERR_HIP, std::string("order build event: ") + hipGetErrorString(st));
-                for (int j = 0; j < Sched::STATS_RING; ++j) q->stats_pending[j] = false;   // r and everything older
+                for (int j = i; j <= Sched::STATS_RING; ++j)   // r and every older build (newer ones stay pending)
+                    q->stats_pending[(q->stats_head + Sched::STATS_RING - j) % Sched::STATS_RING] = false;
                 if (q->stats_key[r] == key && q->stats_mode[r] == mode_now) {
                     const volatile uint32_t *st16 = q->stats + 16 * r;
                     uint32_t m = 0;
@@ -782,9 +914,39 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 }
                 break;
             }
-            p.lat = q->lat_key == key && q->lat_mode == mode_now ? q->lat_cache : 0;
+            latency_bound = q->lat_key == key && q->lat_mode == mode_now && q->lat_cache;
         }
     }
+    if (q) {   // the order this launch dispatches in: with segmented heavy tiles if so decided
+        okey = key;
+        okey.segc = ctx->seg_all ? 6 : latency_bound ? ctx->seg_classes : ctx->seg_classes_issue;
+        okey.seg = seg_cap && okey.segc ? seg_cap : 0;
+        if (!okey.seg) okey.segc = 0;
+        // the newest build it follows by >= 2 launches (Sched): a build that launch n - 2 was
+        // followed by read the cost buffer this launch writes, so it is waited for whatever its key
+        const long long n = (long long)q->launches;
+        int use = -1;
+        for (int i = 0; i < 2; ++i) {
+            if (q->build_at[i] < 0 || q->build_at[i] > n - 2) continue;
+            if (!q->build_seen[i]) {
+                const hipError_t st = hipEventQuery(q->build_ev[i]);
+                if (st == hipErrorNotReady) HIP_TRY(hipStreamWaitEvent(s, q->build_ev[i], 0));
+                else if (st != hipSuccess) return fail(SVO_ERR_HIP, std::string("order build: ") + hipGetErrorString(st));
+                q->build_seen[i] = true;
+            }
+            if (q->build_key[i] == okey && (use < 0 || q->build_at[i] > q->build_at[use])) use = i;
+        }
+        p.tile_order = use >= 0 ? q->order_buf[use] : nullptr;
+        if (p.tile_order && okey.seg) {   // the order lists quarter entries: the segmented kernel
+            p.seg = okey.seg;
+            p.seg_hint = q->seg_hint;
+            if (ctx->seg_scramble) p.seg_scramble = ctx->seg_scramble * 0x9E3779B9u + ++ctx->seg_launches;
+        }
+    }
+    // with segmented tiles the whole tiles keep the lean loop: the latency form's doubled LDS halves
+    // the resident waves of the quarters too (C3 flyover bands, profiles/r05b_seg_ab.json: N = 2
+    // 0.0804 ms with it against 0.0629 without, N = 4 0.0500 / 0.0457, N = 8 0.0388 / 0.0395)
+    p.lat = latency_bound && ctx->lat_mode != 0 && (!p.seg || ctx->lat_mode == 1) ? 1 : 0;
     const char *log_path = std::getenv("SVO_WAVE_LOG");
     const size_t n_wave = (size_t)n_tiles;
     if (log_path && !p.out.fetches) {
@@ -814,30 +976,39 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // the last few frames' costs order a slowly moving view almost as well as its own
     bool refresh = false;
     if (q && p.tile_cost) {
-        const unsigned long long n = q->launches++;
+        const unsigned long long n = q->launches++;   // (p.tile_cost is cost_buf[n % 2])
         const bool moving = q->view_prev != ctx->view_gen;   // a new view since this stream's last launch
         q->view_prev = ctx->view_gen;
         // the periodic rebuild only when costs can have changed without a new view (a jittered
         // pixel offset, a new light or pool, per-launch sample offsets): a held view with nothing
         // else changed records the same costs every launch, so its order stays exact
-        const bool drift = q->built_cost != ctx->cost_gen || p.samples != 0;
-        refresh = q->order_key != key || (n % ctx->order_every == 0 && drift) || q->built_mode != mode_now ||
+        const bool drift = q->built_cost != ctx->cost_gen || p.samples != 0 || jittered;
+        refresh = q->order_key != okey || (n % ctx->order_every == 0 && drift) || q->built_mode != mode_now ||
                   (q->built_view != ctx->view_gen && (!moving || n - q->last_build >= (unsigned long long)ctx->move_every));
         if (refresh) q->last_build = n;
     }
-    if (refresh) {   // the next launch at this geometry dispatches the heaviest tiles first
+    if (refresh) {   // the launch after next at this geometry dispatches the heaviest tiles first
         const int r = q->stats_head;
         uint32_t *st16 = q->stats ? q->stats + 16 * r : nullptr;
-        e = p.xcd_remap == 2 ? svo::launch_order_strips(q->tile_cost, q->tile_order, n_tiles, (width + 7) / 8, s, st16,
-                                                        key.seg, q->part_cost, ctx->seg_all ? 6 : 3)
-                             : svo::launch_order_tiles(q->tile_cost, q->tile_order, n_tiles, s, st16);
+        const int bi = q->next_buf;
+        q->next_buf ^= 1;
+        // on the side stream, behind this launch (its costs; and every launch that read buffer bi)
+        HIP_TRY(hipEventRecord(q->render_done, s));
+        HIP_TRY(hipStreamWaitEvent(q->side, q->render_done, 0));
+        e = p.xcd_remap == 2 ? svo::launch_order_strips(p.tile_cost, q->order_buf[bi], n_tiles, (width + 7) / 8, q->side,
+                                                        st16, okey.seg, p.part_cost, okey.segc)
+                             : svo::launch_order_tiles(p.tile_cost, q->order_buf[bi], n_tiles, q->side, st16);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
-        q->order_key = key;
+        HIP_TRY(hipEventRecord(q->build_ev[bi], q->side));
+        q->build_at[bi] = (long long)q->launches - 1;   // launches was incremented above
+        q->build_seen[bi] = false;
+        q->build_key[bi] = okey;
+        q->order_key = okey;
         q->built_view = ctx->view_gen;
         q->built_cost = ctx->cost_gen;
         q->built_mode = mode_now;
         if (st16) {   // slot r: a build still pending there (ring full) is simply superseded
-            HIP_TRY(hipEventRecord(q->stats_ev[r], s));
+            HIP_TRY(hipEventRecord(q->stats_ev[r], q->side));
             q->stats_pending[r] = true;
             q->stats_key[r] = key;
             q->stats_view[r] = ctx->view_gen;
@@ -946,6 +1117,18 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
                     : (out.hits || out.rgba || out.compact) ? SVO_PART_COMPACT
                     : ctx->sparse_payload ? SVO_PART_SPARSE_RGB8 : SVO_PART_RGB8;
     const size_t elem = fmt == SVO_PART_COMPACT ? 12 : 3;
+    // the band accumulations hold the rows of the deal they were blended under: a continued
+    // accumulation (first sample > 0) under another deal would blend into other members' rows
+    uint64_t dkey = 1469598103934665603ull ^ (uint64_t)n ^ ((uint64_t)ctx->band_rows << 16);
+    for (int i = 0; i < ctx->deal_cycle; ++i) dkey = (dkey ^ ctx->deal_owner[i]) * 1099511628211ull;
+    dkey ^= (uint64_t)ctx->deal_cycle << 40;
+    if (sa) {
+        if (sa->first > 0 && ctx->samples_deal_set && ctx->samples_deal != dkey)
+            return fail(SVO_ERR_STATE, "the band deal changed since the last svo_render_samples: restart the "
+                                       "accumulation at first_sample 0");
+        ctx->samples_deal = dkey;
+        ctx->samples_deal_set = true;
+    }
     const int k = ctx->parity;
     ctx->parity ^= 1;
     svo_ctx *m0 = ctx->members[0];
@@ -991,7 +1174,7 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
             HIP_TRY(hipMalloc(&pr.dense, std::max<size_t>((size_t)rows_i * width * 3, 16)));
             pr.dense_cap = (size_t)rows_i * width * 3;
         }
-        if (sa && (pr.accum_w != width || pr.accum_rows != rows_i)) {   // this member's band accumulation
+        if (sa && (pr.accum_w != width || pr.accum_rows != rows_i || pr.accum_deal != dkey)) {   // this member's band accumulation
             HIP_TRY(hipStreamSynchronize(m->stream));
             if (pr.accum) hipFree(pr.accum);
             pr.accum = nullptr;
@@ -1002,6 +1185,7 @@ int multi_render(svo_ctx *ctx, int width, int height, int stack_mode, const svo_
             HIP_TRY(hipMemsetAsync(pr.accum, 0, abytes, m->stream));   // a fresh render target
             pr.accum_w = width;
             pr.accum_rows = rows_i;
+            pr.accum_deal = dkey;
         }
         if (ctx->gathered_used[k]) HIP_TRY(hipStreamWaitEvent(m->stream, ctx->gathered[k], 0));   // payload k is free
         svo::Outputs oi{};
@@ -1110,12 +1294,23 @@ int destroy_single(svo_ctx *ctx) {
     free_pinned(ctx);
     if (ctx->copy_stream) hipStreamDestroy(ctx->copy_stream);
     if (ctx->copy_stream2) hipStreamDestroy(ctx->copy_stream2);
+    ctx->copy_pool.reset();
+    if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    for (int i = 0; i < svo_ctx::STAGE_CHUNKS; ++i)
+        if (ctx->stage_ev[i]) hipEventDestroy(ctx->stage_ev[i]);
     for (Sched &q : ctx->sched) {
         free_sched(q);
         if (q.seg_hint) hipFree(q.seg_hint);
         if (q.done) hipEventDestroy(q.done);
         for (int r = 0; r < Sched::STATS_RING; ++r)
             if (q.stats_ev[r]) hipEventDestroy(q.stats_ev[r]);
+        if (q.side) {
+            hipStreamSynchronize(q.side);
+            hipStreamDestroy(q.side);
+        }
+        if (q.render_done) hipEventDestroy(q.render_done);
+        for (int i = 0; i < 2; ++i)
+            if (q.build_ev[i]) hipEventDestroy(q.build_ev[i]);
         if (q.stats) hipHostFree(q.stats);
     }
     for (auto &v : ctx->timing_events)
@@ -1132,7 +1327,7 @@ int destroy_single(svo_ctx *ctx) {
 
 extern "C" {
 
-int svo_abi_version(void) { return 8; }
+int svo_abi_version(void) { return 9; }
 
 const char *svo_last_error(void) { return g_last_error.c_str(); }
 
@@ -1158,6 +1353,9 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (e == hipSuccess) e = hipMemsetAsync(ctx->d_att, 0, capacity_nodes * sizeof(uint2), ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
+    int lds_block = 0;
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&lds_block, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
+    if (e == hipSuccess && lds_block > 0) ctx->lds_per_block = (size_t)lds_block;
     if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) == 0 ? 0 : 2;
     if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;
@@ -1169,6 +1367,8 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_MOVE_EVERY")) ctx->move_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_LAT")) ctx->lat_mode = std::atoi(k) != 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_SEG")) ctx->seg_mode = std::atoi(k) != 0 ? 1 : 0;
+    if (const char *k = std::getenv("SVO_SEG_CLASSES")) ctx->seg_classes = std::min(6, std::max(1, std::atoi(k)));
+    if (const char *k = std::getenv("SVO_SEG_CLASSES_ISSUE")) ctx->seg_classes_issue = std::min(6, std::max(0, std::atoi(k)));
     if (const char *k = std::getenv("SVO_SEG_CAP")) ctx->seg_cap = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_SEG_ALL")) ctx->seg_all = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SEG_SCRAMBLE")) ctx->seg_scramble = (uint32_t)std::strtoul(k, nullptr, 10);
@@ -1465,11 +1665,64 @@ int svo_render(svo_ctx *ctx, int width, int height, int stack_mode, float *rgba_
     }
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    if (hits_out)
-        HIP_TRY(hipMemcpyAsync(hits_out, c->d_out_hits, px * sizeof(svo_hit), hipMemcpyDeviceToHost, c->stream));
-    if (rgba_out)
-        HIP_TRY(hipMemcpyAsync(rgba_out, c->d_out_rgba, px * 4 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    // The outputs reach the caller's pageable arrays through plugin-owned pinned staging: the DMA of
+    // chunk i (at the link's rate) runs while host threads copy chunk i - 1 out of the staging
+    // (a pageable hipMemcpy stages through the runtime's own small buffer: ~13 GB/s, 6.2 ms for the
+    // 83 MB of a 1080p frame, BENCH_r04.json host_path).
+    const size_t hb = hits_out ? px * sizeof(svo_hit) : 0, rb = rgba_out ? px * 4 * sizeof(float) : 0;
+    if (c->h_stage_cap < hb + rb) {
+        if (c->h_stage) hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->h_stage_cap = 0;
+        HIP_TRY(hipHostMalloc(&c->h_stage, hb + rb, hipHostMallocDefault));
+        c->h_stage_cap = hb + rb;
+    }
+    if (!c->stage_ev[0])
+        for (int i = 0; i < svo_ctx::STAGE_CHUNKS; ++i)
+            HIP_TRY(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
+    if (!c->copy_pool) {
+        int n = (int)std::thread::hardware_concurrency() / 2;
+        if (const char *v = std::getenv("SVO_HOST_COPY_THREADS")) n = std::atoi(v);
+        c->copy_pool.reset(new CopyPool(std::max(1, std::min(n, 16))));
+    }
+    struct Part { char *dst; const char *dev; char *stage; size_t bytes; };
+    Part parts[2];
+    int np = 0;
+    if (hb) parts[np++] = {reinterpret_cast<char *>(hits_out), static_cast<const char *>(c->d_out_hits),
+                           static_cast<char *>(c->h_stage), hb};
+    if (rb) parts[np++] = {reinterpret_cast<char *>(rgba_out), static_cast<const char *>(c->d_out_rgba),
+                           static_cast<char *>(c->h_stage) + hb, rb};
+    const size_t total = hb + rb;
+    const size_t chunk = ((total + svo_ctx::STAGE_CHUNKS - 1) / svo_ctx::STAGE_CHUNKS + 4095) & ~(size_t)4095;
+    // chunk i covers bytes [i chunk, (i + 1) chunk) of the concatenated outputs
+    auto for_range = [&](size_t lo, size_t hi, auto fn) {
+        size_t base = 0;
+        for (int k = 0; k < np; ++k) {
+            const size_t a = std::max(lo, base), b = std::min(hi, base + parts[k].bytes);
+            if (a < b) fn(parts[k], a - base, b - a);
+            base += parts[k].bytes;
+        }
+    };
+    int n_chunks = 0;
+    for (size_t lo = 0; lo < total; lo += chunk, ++n_chunks) {
+        const size_t hi = std::min(total, lo + chunk);
+        hipError_t e = hipSuccess;
+        for_range(lo, hi, [&](const Part &q, size_t off, size_t n) {
+            if (e == hipSuccess) e = hipMemcpyAsync(q.stage + off, q.dev + off, n, hipMemcpyDeviceToHost, c->stream);
+        });
+        HIP_TRY(e);
+        HIP_TRY(hipEventRecord(c->stage_ev[n_chunks], c->stream));
+    }
+    CopyPool &pool = *c->copy_pool;
+    for (int i = 0; i < n_chunks; ++i) {
+        HIP_TRY(hipEventSynchronize(c->stage_ev[i]));
+        const size_t lo = (size_t)i * chunk, hi = std::min(total, lo + chunk);
+        for_range(lo, hi, [&](const Part &q, size_t off, size_t n) {
+            const size_t per = ((n + pool.size() - 1) / pool.size() + 63) & ~(size_t)63;
+            for (size_t o = 0; o < n; o += per) pool.submit(q.dst + off + o, q.stage + off + o, std::min(per, n - o));
+        });
+    }
+    pool.wait();
     return SVO_OK;
 }
 
@@ -1739,6 +1992,41 @@ int svo_accumulate(svo_ctx *ctx, void *d_accum, const void *d_sample, size_t n_p
     hipError_t e = svo::launch_accumulate(reinterpret_cast<float4 *>(d_accum), reinterpret_cast<const float4 *>(d_sample),
                                           n_px, sample, c->num_cus, s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("accumulate launch: ") + hipGetErrorString(e));
+    return SVO_OK;
+}
+
+int svo_forget_stream(svo_ctx *ctx, void *stream) {
+    if (!ctx) return fail(SVO_ERR_ARG, "null context");
+    if (!stream) return SVO_OK;   // the context's own stream lives as long as the context
+    for (svo_ctx *m : ctx->members) {
+        int rc = svo_forget_stream(m, stream);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    bool known = ctx->scratch_valid && ctx->scratch_stream == s;
+    for (Sched &q : ctx->sched) known = known || (q.used && q.stream == s);
+    if (!known) return SVO_OK;
+    HIP_TRY(hipStreamSynchronize(s));
+    for (Sched &q : ctx->sched) {
+        if (!q.used || q.stream != s) continue;
+        // the set's buffers stay allocated for the next stream; only the stream is forgotten
+        if (q.side) HIP_TRY(hipStreamSynchronize(q.side));
+        q.used = false;
+        q.stream = nullptr;
+        reset_builds(q);
+        q.launches = q.shadow_launches = 0;
+        q.view_prev = ~0ull;
+        q.built_cost = ~0ull;
+        q.last_build = 0;
+        for (int r = 0; r < Sched::STATS_RING; ++r) q.stats_pending[r] = false;
+        q.lat_key = Geo();
+        q.lat_mode = -1;
+    }
+    if (ctx->scratch_valid && ctx->scratch_stream == s) {
+        ctx->scratch_valid = false;
+        ctx->scratch_stream = nullptr;
+    }
     return SVO_OK;
 }
 

@@ -61,6 +61,11 @@ struct Outputs {
                                    // (lr / 8) * tiles_x + x / 8): the wave's ballot of its hit lanes
     uint32_t *fetches;         // instrumented launch: descriptor fetches per ray
     int frame_layout;          // 1: index by global row (full-frame buffers)
+    // one sample blended into an RGBA32F accumulation (svo_render_samples with S = 1: the one-sample
+    // launch itself, AddShader's blend in its epilogue): accum = colour * acc_a + accum * acc_b,
+    // and rgba8 / rgb8 then carry the BLENDED colour
+    float4 *accum;
+    float acc_a, acc_b;
 };
 
 struct LaunchParams {

@@ -179,10 +179,17 @@ class RaytracingMaster:
         return _MemberView(self, c)
 
     # ----------------------------------------------------------------- render
-    def Render(self, width, height, stack_mode=STACK_HLSL, want_rgba=True, want_hits=True):
-        """Blocking render into host arrays: (rgba[H, W, 4] float32, hits[H, W] svo_hit)."""
-        rgba = np.zeros((height, width, 4), np.float32) if want_rgba else None
-        hits = np.zeros((height, width), HIT_DTYPE) if want_hits else None
+    def Render(self, width, height, stack_mode=STACK_HLSL, want_rgba=True, want_hits=True, out=None):
+        """Blocking render into host arrays: (rgba[H, W, 4] float32, hits[H, W] svo_hit).
+        out: an earlier call's (rgba, hits) to write again (a render loop's reused arrays; fresh
+        arrays pay the first-touch page faults of 83 MB per 1080p frame)."""
+        if out is not None:
+            rgba, hits = out
+            assert rgba is None or (rgba.dtype == np.float32 and rgba.size == height * width * 4 and rgba.flags.c_contiguous)
+            assert hits is None or (hits.dtype == HIT_DTYPE and hits.size == height * width and hits.flags.c_contiguous)
+        else:
+            rgba = np.zeros((height, width, 4), np.float32) if want_rgba else None
+            hits = np.zeros((height, width), HIT_DTYPE) if want_hits else None
         check(_lib.lib().svo_render(self._ctx, width, height, stack_mode,
                                     None if rgba is None else rgba.ctypes.data,
                                     None if hits is None else hits.ctypes.data), "svo_render")
@@ -314,6 +321,10 @@ class RaytracingMaster:
         check(_lib.lib().svo_accumulate(self._ctx, accum_ptr, sample_ptr, int(n_px), n, stream), "svo_accumulate")
         if sample is None:
             self.currentSample += 1
+
+    def forget_stream(self, stream):
+        """svo_forget_stream: the caller is about to destroy `stream` (a hipStream_t handle)."""
+        check(_lib.lib().svo_forget_stream(self._ctx, stream), "svo_forget_stream")
 
     def synchronize(self):
         check(_lib.lib().svo_synchronize(self._ctx), "svo_synchronize")

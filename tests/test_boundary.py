@@ -41,7 +41,7 @@ def test_exports_every_declared_symbol(native):
 
 def test_abi_version_and_error_text(native):
     from raytracingtest_amd import _lib
-    assert native.svo_abi_version() == _lib.ABI_VERSION == 8
+    assert native.svo_abi_version() == _lib.ABI_VERSION == 9
     assert isinstance(native.svo_last_error(), bytes)
 
 

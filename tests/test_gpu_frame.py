@@ -643,6 +643,35 @@ def test_two_streams_every_pixel_written(torch, oracle_mod, n_streams):
         m.close()
 
 
+def test_forgotten_streams_destroyed_then_new_ones(torch, oracle_mod):
+    """a caller stream must stay alive until svo_forget_stream.  Four streams fill the
+    context's dispatch-order sets, each is forgotten and destroyed, then six fresh streams (HIP
+    may reuse the old handles) render again: no event lands on a dead stream, every frame is
+    complete and equal to the oracle's, and forgetting an unknown stream is not an error."""
+    svo = build_menger(8)
+    w, h = 320, 184
+    cam = overview_camera()
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        for generation in range(2):
+            streams = [torch.cuda.Stream() for _ in range(4 if generation == 0 else 6)]
+            outs = [_bufs(torch, w * h) for _ in range(2 * len(streams))]
+            for i, b in enumerate(outs):
+                m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(),
+                               stream=streams[i % len(streams)].cuda_stream)
+            for st in streams:
+                m.forget_stream(st.cuda_stream)
+            for b in outs:   # forget_stream waited for each stream's renders
+                _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+            del streams
+        m.forget_stream(torch.cuda.Stream().cuda_stream)
+    finally:
+        m.close()
+
+
 def _rand_subtree(rng, depth, nodes, att, p_leaf=0.5):
     """Append a random V2 subtree of exactly `depth` descriptor levels (one
     branch always goes to the bottom) in the builder's layout: a node's non-leaf

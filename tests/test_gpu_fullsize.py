@@ -268,3 +268,23 @@ def test_c3_weak_scaling_frame_split_over_eight_ranks(gpu, oracle_mod):
             got = frame.cpu().numpy().view(np.uint32)
             bad = np.count_nonzero(got != want)
             assert bad == 0, f"format {fmt}: {bad} of {W * H} display words differ"
+
+
+def test_blocking_render_into_reused_host_arrays(gpu, oracle_mod):
+    """svo_render (the drop-in's blocking Render, RaytracingMaster.cs:60-74) on the C3 frame, through
+    the plugin's pinned staging and host copy threads, into the SAME host arrays for two poses in a
+    row: each call's hit records and Result equal the oracle's frame for its own pose (nothing of
+    the previous frame survives, every chunk arrives)."""
+    cfg = CONFIGS["C3"]
+    svo = _svo(cfg)
+    w, h = cfg["width"], cfg["height"]
+    with RaytracingMaster(device=0, capacity_nodes=len(svo)) as rm:
+        rm.SetSVOBuffer(svo)
+        arrays = None
+        for pose in ("flyover", "main", "flyover"):
+            cam = CAMERAS[pose]()
+            rm.UpdateShaderParameters(cam, w, h)
+            arrays = rm.Render(w, h, stack_mode=cfg["stack_mode"], out=arrays)
+            rgba, hits = arrays
+            ref_rgba, ref_hits = _oracle(oracle_mod, svo, cfg, cam)
+            _assert_same(hits.reshape(-1), rgba.reshape(-1, 4), ref_hits, ref_rgba, f"svo_render {pose}")

@@ -172,9 +172,11 @@ public class RaytracingMasterNative : MonoBehaviour {
                                                  UnityEngine.Random.value, UnityEngine.Random.value,
                                                  new[] { l.x, l.y, l.z, DirectionalLight.intensity }), "svo_set_camera");
         int w = Screen.width, h = Screen.height;
-        if (_frame == null || _frame.width != w || _frame.height != h) {
-            // the pipelined path moves 3-byte pixels (RGB24: a quarter fewer bytes over PCIe)
-            _frame = new Texture2D(w, h, pipelined ? TextureFormat.RGB24 : TextureFormat.RGBA32, false, true);
+        // the pipelined path moves 3-byte pixels (RGB24: a quarter fewer bytes over PCIe); `pipelined`
+        // is an Inspector field, so a toggle at run time recreates the texture in the other format
+        TextureFormat want = pipelined ? TextureFormat.RGB24 : TextureFormat.RGBA32;
+        if (_frame == null || _frame.width != w || _frame.height != h || _frame.format != want) {
+            _frame = new Texture2D(w, h, want, false, true);
             _rgba8 = new uint[w * h];
             _currentSample = 0;   // a new render target: the plugin starts a fresh accumulation frame
         }
