@@ -632,28 +632,29 @@ typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void store_outputs(const Outputs &out, size_t i, const Record &o) {
+    // the words as scalars first: vectors built straight from the array kept it in private memory
+    // in render_seg_kernel
+    const uint32_t w0 = o.w[0], w1 = o.w[1], w2 = o.w[2], w3 = o.w[3], w4 = o.w[4], w5 = o.w[5];
     if (out.hits) {
         u32x2 *dst = reinterpret_cast<u32x2 *>(out.hits + i);
-        __builtin_nontemporal_store(u32x2{o.w[0], o.w[1]}, dst + 0);
-        __builtin_nontemporal_store(u32x2{o.w[2], o.w[3]}, dst + 1);
-        __builtin_nontemporal_store(u32x2{o.w[4], o.w[5]}, dst + 2);
+        __builtin_nontemporal_store(u32x2{w0, w1}, dst + 0);
+        __builtin_nontemporal_store(u32x2{w2, w3}, dst + 1);
+        __builtin_nontemporal_store(u32x2{w4, w5}, dst + 2);
     }
     if (out.compact)
         // a 3-vector is 16 bytes apart in arrays: address the 12-byte record explicitly
-        __builtin_nontemporal_store(u32x3{o.w[0], o.w[1], o.w[2]}, reinterpret_cast<u32x3 *>(out.compact + 3 * i));
+        __builtin_nontemporal_store(u32x3{w0, w1, w2}, reinterpret_cast<u32x3 *>(out.compact + 3 * i));
     if (out.rgba)
         __builtin_nontemporal_store(f32x4{o.rgb[0], o.rgb[1], o.rgb[2], 1.0f}, reinterpret_cast<f32x4 *>(out.rgba + i));
     float dr = o.rgb[0], dg = o.rgb[1], db = o.rgb[2];   // the colour the display words carry
     if (out.accum) {   // accumulate_kernel's blend (AddShader.shader:44-47), the Result alpha is a
         const float4 d0 = out.accum[i];
         const float a = out.acc_a, b = out.acc_b;
-        f32x4 d;
-        d.x = o.rgb[0] * a + d0.x * b;
-        d.y = o.rgb[1] * a + d0.y * b;
-        d.z = o.rgb[2] * a + d0.z * b;
-        d.w = a * a + d0.w * b;
-        __builtin_nontemporal_store(d, reinterpret_cast<f32x4 *>(out.accum + i));
-        dr = d.x; dg = d.y; db = d.z;
+        dr = o.rgb[0] * a + d0.x * b;
+        dg = o.rgb[1] * a + d0.y * b;
+        db = o.rgb[2] * a + d0.z * b;
+        const float dw = a * a + d0.w * b;
+        __builtin_nontemporal_store(f32x4{dr, dg, db, dw}, reinterpret_cast<f32x4 *>(out.accum + i));
     }
     if (out.rgba8 || out.rgb8) {
         const uint32_t w = pack_rgba8(dr, dg, db);
@@ -831,7 +832,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
 }
 
 // ------------------------------------------------------------- segmented rays
-// One ray's traversal split into SEG_K t-segments that run side by side (VERDICT r4 item 1:
+// One ray's traversal split into K t-segments that run side by side (VERDICT r4 item 1:
 // a heavy tile's wave is a serial chain of up to ~270 trips that bounds a frame split over N
 // GPUs; modelled first, tools/segment_model.py).  Segment k of a ray with
 // starts t_1 .. t_{K-1} (any floats, NaN included: the result never depends on them, only the
@@ -989,65 +990,157 @@ __device__ __forceinline__ void trace_seg(const LaunchParams &p, FRay &r, uint2 
     r.trips = it;
 }
 
-// quad (lane ^ 1, lane ^ 2) reductions: a ray's SEG_K = 4 lanes
-__device__ __forceinline__ int quad_min(int v) {
+// a ray's K segments are K consecutive lanes (K = 4 or 8, wave-uniform)
+__device__ __forceinline__ int group_min(int v, int K) {
     v = min(v, __shfl_xor(v, 1));
-    return min(v, __shfl_xor(v, 2));
+    v = min(v, __shfl_xor(v, 2));
+    if (K == 8) v = min(v, __shfl_xor(v, 4));
+    return v;
 }
-__device__ __forceinline__ float quad_get(float v, int src_in_quad) {
-    return __shfl(v, (int)(threadIdx.x & ~3u) + src_in_quad);
+__device__ __forceinline__ float group_get(float v, int K, int j) {
+    return __shfl(v, (int)(threadIdx.x & ~(uint32_t)(K - 1)) + j);
 }
-__device__ __forceinline__ uint32_t quad_get(uint32_t v, int src_in_quad) {
-    return (uint32_t)__shfl((int)v, (int)(threadIdx.x & ~3u) + src_in_quad);
+__device__ __forceinline__ uint32_t group_get(uint32_t v, int K, int j) {
+    return (uint32_t)__shfl((int)v, (int)(threadIdx.x & ~(uint32_t)(K - 1)) + j);
 }
 
-// The next frame's starts of one ray from this frame's segments (lane k = quad's segment k):
-// the continuous trips each segment took after arming (segment 0: all of its trips) put the
-// cumulative share at its start t_k; the new t_j is where the cumulative share reaches j / K of
-// the total, linear in t between the points (t_entry, 0), (t_k, share before k), (t_end, total).
-// Only the balance of the next trace depends on it.  Called by every lane; lane 0 of the quad
-// gets the result.
-__device__ __forceinline__ float4 seg_rebalance(float t_entry, float t_start, float t_end, uint32_t c, int f) {
-    const int k = (int)(threadIdx.x & 3u);
-    const float cf = k <= f ? (float)c : 0.0f;
-    float cum[SEG_K + 1], tp[SEG_K + 1];
-    cum[0] = 0.0f;
-    tp[0] = t_entry;
-#pragma unroll
-    for (int j = 0; j < SEG_K; ++j) {
-        cum[j + 1] = cum[j] + quad_get(cf, j);
-        tp[j + 1] = j + 1 < SEG_K ? quad_get(t_start, j + 1) : t_end;
+// The next frame's starts of one ray from this frame's K segments: the continuous trips each
+// segment took after arming (segment 0: all of its trips) put the cumulative share at its start
+// t_k; the new start at fraction e / 8 (e = 1..7, whatever K the next trace uses) is where the
+// cumulative share reaches e / 8 of the total, linear in t between the points (t_entry, 0),
+// (t_k, share before k), (t_end, total).  Only the balance of the next trace depends on it.
+// `slot`: this wave's dead stack (LDS, one uint2 per lane): each lane parks (its share, its
+// start) there, and lane 0 of the group walks the K entries in order -- no per-lane arrays, so
+// the kernel keeps the lean loop's register budget.  Returns false if the ray gave no information.
+__device__ __forceinline__ void seg_rebalance(uint2 *slot, float t_entry, float t_start, float t_end, uint32_t c,
+                                              int f, int K, float tot, float *hint8, bool store) {
+    const int lane = (int)threadIdx.x, k = lane & (K - 1);
+    // a start past the ray's end carries nothing: it sits at the end
+    slot[lane] = make_uint2(k <= f ? c : 0u, __float_as_uint(k == 0 ? t_entry : k > f ? t_end : t_start));
+    if (k != 0 || !store) return;
+    if (!(tot > 0.0f)) {   // no information: the next trace splits the cube span evenly
+        hint8[0] = __int_as_float(0x7FC00000);
+        return;
     }
-#pragma unroll
-    for (int j = 1; j < SEG_K; ++j)
-        if (j > f) tp[j] = t_end;   // starts past the ray's end carry nothing
-    const float tot = cum[SEG_K];
-    float out[SEG_K - 1];
-#pragma unroll
-    for (int j = 1; j < SEG_K; ++j) {
-        const float target = tot * ((float)j / (float)SEG_K);
-        float v = tp[SEG_K];
-#pragma unroll
-        for (int m = SEG_K - 1; m >= 0; --m) {
-            if (cum[m + 1] >= target) {
-                const float span = cum[m + 1] - cum[m];
-                const float fr = span > 0.0f ? (target - cum[m]) / span : 0.0f;
-                v = tp[m] + fr * (tp[m + 1] - tp[m]);
-            }
+    const uint2 *g = slot + lane;   // the group's K entries
+    int m = 0;
+    float cum = 0.0f, cm = (float)g[0].x, t0 = t_entry, prev = 0.0f;
+    float t1 = K > 1 ? __uint_as_float(g[1].y) : t_end;
+    for (int e = 1; e < SEG_KMAX; ++e) {
+        const float target = tot * ((float)e / (float)SEG_KMAX);
+        while (m < K - 1 && cum + cm < target) {   // the segment holding the target
+            cum += cm;
+            ++m;
+            cm = (float)g[m].x;
+            t0 = t1;
+            t1 = m + 1 < K ? __uint_as_float(g[m + 1].y) : t_end;
         }
-        out[j - 1] = j > 1 ? fmaxf(v, out[j - 2]) : v;
+        const float fr = cm > 0.0f ? fminf(fmaxf((target - cum) / cm, 0.0f), 1.0f) : 0.0f;
+        const float v = t0 + fr * (t1 - t0);
+        prev = e > 1 ? fmaxf(v, prev) : v;
+        hint8[e - 1] = prev;
     }
-    if (!(tot > 0.0f)) return make_float4(__int_as_float(0x7FC00000), 0.0f, 0.0f, 0.0f);
-    return make_float4(out[0], out[1], out[2], 0.0f);
+}
+
+// Start of the segment at fraction e / 8 of the ray's trace (e = 0 or 8: none, NaN): the
+// pixel's stored starts, an even split of the cube span before it has any, or (tests,
+// p.seg_scramble) a hash -- unordered, NaN, +-inf or outside the cube.
+__device__ __forceinline__ float seg_start(const LaunchParams &p, const float *hint8, bool have, size_t hi, int e,
+                                           float t_entry, float t_exit) {
+    if (e <= 0 || e >= SEG_KMAX) return __int_as_float(0x7FC00000);
+    const float span = t_exit - t_entry;
+    if (p.seg_scramble) {
+        uint32_t hsh = (uint32_t)hi * 0x9E3779B1u ^ p.seg_scramble * 0x85EBCA77u ^ (uint32_t)e * 0x27D4EB2Fu;
+        hsh ^= hsh >> 15; hsh *= 0x2C1B3C6Du; hsh ^= hsh >> 12; hsh *= 0x297A2D39u; hsh ^= hsh >> 15;
+        const uint32_t sel = hsh & 15u;
+        const float u = (float)(hsh >> 8) * (1.0f / 16777216.0f);
+        return sel == 0 ? __int_as_float(0x7FC00000) : sel == 1 ? __int_as_float(0x7F800000)
+             : sel == 2 ? __int_as_float(0xFF800000) : t_entry + (1.4f * u - 0.2f) * span;
+    }
+    return have ? hint8[e - 1] : t_entry + ((float)e / (float)SEG_KMAX) * span;
 }
 
 // Cost-ordered launch whose order (launch_order_strips with seg_cap > 0) lists each XCD's
-// heaviest tiles as SEG_K quarter entries: quarter q traces rows 2 q, 2 q + 1 of its tile, 16
-// rays x SEG_K segments (lanes 4 r + k), and writes every output of those 16 pixels from the
-// lane of the segment that holds the record.  Every other entry is one tile, traced as in
-// render_tile_kernel (lean loop, primary rays).  A quarter's chain is its longest segment:
-// ~1/K of the tile's continuous chain plus the walk to t_k.  LAT: whole tiles take the
-// latency form (trace_lat, twice the LDS), as a latency-bound launch without segments would.
+// heaviest tiles as K part entries (K = 4 or 8 by cost class): part q traces 64 / K rays of its
+// tile -- rows q * 8 / K onward -- as K segments each (lanes K r .. K r + K - 1 = ray r), and
+// writes every output of those pixels from the lane of the segment that holds the record.  Every
+// other entry is one tile, traced as in render_tile_kernel (lean loop, primary rays).  A part's
+// chain is its longest segment: ~1/K of the tile's continuous chain plus the walk to t_k.  LAT:
+// whole tiles take the latency form (trace_lat, twice the LDS).
+// Part `part` of a tile traced as K segments per ray (render_seg_kernel; K a template constant so
+// the part's wave-uniform values need no SGPRs across the traversal loop).
+template <int MODE, bool FA, int K>
+__device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restrict__ stk_base, int t, int part, int bx,
+                                         int by) {
+    const int lane = threadIdx.x;
+    uint2 *stk = stk_base + lane;
+    constexpr int R = TILE / K;                // rays of this part: rows part * R / 8 .. of the tile
+    const int k = lane & (K - 1), ri = lane / K;
+    const int x_ = bx * 8 + (ri & 7);
+    const int lr_ = by * 8 + part * (R / 8) + (ri >> 3);
+    const bool inside = x_ < p.width && lr_ < p.local_rows;   // outside lanes trace a copy, store nothing
+    const int x = min(x_, p.width - 1), lr = min(lr_, p.local_rows - 1);
+    const int gy = global_row(p, lr);
+    Ray r;
+    {
+        float org[3], dir[3];
+        camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
+        setup_ray(org, dir, r);
+    }
+    const float t_entry = r.t_min, t_exit = r.t_max;
+    // the pixel's starts at fractions e / 8 of its trace (8 floats: e = 1..7 + spare); segment k of
+    // K runs from fraction k / K to (k + 1) / K
+    const size_t hi = (size_t)lr * (size_t)p.width + (size_t)x;
+    float *hint8 = reinterpret_cast<float *>(p.seg_hint + 2 * hi);
+    const int e0 = k * (SEG_KMAX / K), e1 = e0 + SEG_KMAX / K;   // 0 and 8: none
+    const bool have = hint8[0] == hint8[0];                        // NaN: none yet
+    const float t_start = seg_start(p, hint8, have, hi, e0, t_entry, t_exit);
+    const float t_stop = seg_start(p, hint8, have, hi, e1, t_entry, t_exit);
+    FRay f;
+    to_fray(r, f);
+    uint32_t n_lane, armed_at;
+    bool stopped;
+    trace_seg<MODE, FA>(p, f, stk, t_start, t_stop, k == 0, n_lane, armed_at, stopped);
+    from_fray(f, r);
+    // the record holder: the first segment that did not stop (the last one never stops)
+    const int fsel = group_min(stopped ? K : k, K);
+    const bool writer = k == fsel;
+    const uint32_t c = k == 0 ? n_lane : n_lane - armed_at;   // continuous trips after arming
+    const float t_end = group_get(r.scale < S_MAX ? r.t_min : t_exit, K, fsel);
+    uint32_t tot = k <= fsel ? c : 0u;   // the ray's continuous trips, its tile_cost share
+    tot += (uint32_t)__shfl_xor((int)tot, 1);
+    tot += (uint32_t)__shfl_xor((int)tot, 2);
+    if (K == 8) tot += (uint32_t)__shfl_xor((int)tot, 4);
+    seg_rebalance(stk_base, t_entry, t_start, t_end, c, fsel, K, (float)tot, hint8, inside);
+    if (p.tile_cost) {
+        uint32_t m = inside ? tot : 0u;
+        for (int d = K; d < TILE; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+        if (lane == 0) {
+            p.part_cost[SEG_KMAX * (size_t)t + part] = (uint16_t)min(m, (uint32_t)(SEG_COST_FLAG - 1));
+            if (part == 0) p.tile_cost[t] = (uint16_t)(SEG_COST_FLAG | K);
+        }
+    }
+    if (p.out.hitmask) {   // this part's R pixels: bits part * R .. part * R + R - 1 of the tile's mask
+        // OR of the ray's group: the writer lane's hit, gathered into lane K r, then one ballot
+        uint32_t hit_w = (writer && inside && r.scale < S_MAX) ? 1u : 0u;
+        hit_w |= (uint32_t)__shfl_xor((int)hit_w, 1);
+        hit_w |= (uint32_t)__shfl_xor((int)hit_w, 2);
+        if (K == 8) hit_w |= (uint32_t)__shfl_xor((int)hit_w, 4);
+        const uint64_t hm = __ballot(k == 0 && hit_w != 0);   // bit K r = ray r
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < R; ++j) bits |= (uint32_t)((hm >> (K * j)) & 1ull) << j;
+        if (lane == 0) {
+            if (K == 4) reinterpret_cast<uint16_t *>(p.out.hitmask)[4 * (size_t)t + part] = (uint16_t)bits;
+            else reinterpret_cast<uint8_t *>(p.out.hitmask)[8 * (size_t)t + part] = (uint8_t)bits;
+        }
+    }
+    if (!writer || !inside) return;
+    Record o;
+    record(p, r, x, gy, o);
+    store_outputs(p.out, out_index(p, lr, gy, x), o);
+}
+
 template <int MODE, bool FA, bool LAT>
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))) void render_seg_kernel(LaunchParams p, int tiles_x) {
     extern __shared__ uint2 stk_base[];
@@ -1055,7 +1148,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
     const uint32_t entry = p.tile_order[blockIdx.x];
     if (entry == SEG_EMPTY) return;
     const int t = (int)(entry & 0x0FFFFFFFu);
-    const int quarter = (int)(entry >> 28) - 1;   // -1: a whole tile
+    const int code = (int)(entry >> 28);   // 0: a whole tile; 1..4: part of a K = 4 tile; 5..12: K = 8
     if (p.prio) {
         const uint32_t *bound = p.tile_order + gridDim.x + 4 + 4 * (blockIdx.x % 8);
         const uint32_t b = blockIdx.x / 8;
@@ -1065,7 +1158,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
     }
     const int bx = t % tiles_x, by = t / tiles_x;
     uint2 *stk = stk_base + lane;
-    if (quarter < 0) {   // render_tile_kernel's primary-ray path
+    if (code == 0) {   // render_tile_kernel's primary-ray path
         const int x = bx * 8 + (lane & 7);
         const int lr = by * 8 + (lane >> 3);
         if (x >= p.width || lr >= p.local_rows) return;
@@ -1091,81 +1184,8 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
         store_outputs(p.out, out_index(p, lr, gy, x), o);
         return;
     }
-    // quarter q of tile t: ray ri = lane / 4 is pixel (ri % 8, 2 q + ri / 8) of the tile, k its segment
-    const int k = lane & 3, ri = lane >> 2;
-    const int x_ = bx * 8 + (ri & 7);
-    const int lr_ = by * 8 + 2 * quarter + (ri >> 3);
-    const bool inside = x_ < p.width && lr_ < p.local_rows;   // outside lanes trace a copy, store nothing
-    const int x = min(x_, p.width - 1), lr = min(lr_, p.local_rows - 1);
-    const int gy = global_row(p, lr);
-    Ray r;
-    {
-        float org[3], dir[3];
-        camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
-        setup_ray(org, dir, r);
-    }
-    const float t_entry = r.t_min, t_exit = r.t_max;
-    const size_t hi = (size_t)lr * (size_t)p.width + (size_t)x;
-    float4 hint = p.seg_hint[hi];
-    if (hint.x != hint.x) {   // none yet: an even split of the cube span
-        const float span = t_exit - t_entry;
-        hint = make_float4(t_entry + 0.25f * span, t_entry + 0.5f * span, t_entry + 0.75f * span, 0.0f);
-    }
-    if (p.seg_scramble) {   // tests: arbitrary starts (the records must not change)
-        uint32_t hsh = (uint32_t)hi * 0x9E3779B1u ^ p.seg_scramble * 0x85EBCA77u;
-        float v[3];
-        const float span = t_exit - t_entry;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            hsh ^= hsh >> 15; hsh *= 0x2C1B3C6Du; hsh ^= hsh >> 12; hsh *= 0x297A2D39u; hsh ^= hsh >> 15;
-            const uint32_t sel = hsh & 15u;
-            const float u = (float)(hsh >> 8) * (1.0f / 16777216.0f);
-            v[j] = sel == 0 ? __int_as_float(0x7FC00000) : sel == 1 ? __int_as_float(0x7F800000)
-                 : sel == 2 ? __int_as_float(0xFF800000) : t_entry + (1.4f * u - 0.2f) * span;
-        }
-        hint = make_float4(v[0], v[1], v[2], 0.0f);
-    }
-    const float qnan = __int_as_float(0x7FC00000);
-    const float hk[SEG_K - 1] = {hint.x, hint.y, hint.z};
-    const float t_start = k == 0 ? qnan : hk[k - 1];
-    const float t_stop = k == SEG_K - 1 ? qnan : hk[k];
-    FRay f;
-    to_fray(r, f);
-    uint32_t n_lane, armed_at;
-    bool stopped;
-    trace_seg<MODE, FA>(p, f, stk, t_start, t_stop, k == 0, n_lane, armed_at, stopped);
-    from_fray(f, r);
-    // the record holder: the first segment that did not stop (the last one never stops)
-    const int fsel = quad_min(stopped ? SEG_K : k);
-    const bool writer = k == fsel;
-    const uint32_t c = k == 0 ? n_lane : n_lane - armed_at;   // continuous trips after arming
-    const float t_end = quad_get(r.scale < S_MAX ? r.t_min : t_exit, fsel);
-    const float4 nh = seg_rebalance(t_entry, t_start, t_end, c, fsel);
-    uint32_t tot = 0;   // the ray's continuous trips, its tile_cost share
-#pragma unroll
-    for (int j = 0; j < SEG_K; ++j) tot += quad_get(j <= fsel ? c : 0u, j);
-    if (k == 0 && inside) p.seg_hint[hi] = nh;
-    if (p.tile_cost) {
-        uint32_t m = inside ? tot : 0u;
-#pragma unroll
-        for (int d = 4; d < 64; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
-        if (lane == 0) {
-            p.part_cost[4 * (size_t)t + quarter] = (uint16_t)min(m, (uint32_t)(SEG_COST_FLAG - 1));
-            if (quarter == 0) p.tile_cost[t] = SEG_COST_FLAG;
-        }
-    }
-    if (p.out.hitmask) {   // this quarter's 16 pixels: bits 16 q .. 16 q + 15 of the tile's mask
-        const uint64_t hm = __ballot(writer && inside && r.scale < S_MAX);
-        uint32_t part16 = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) part16 |= (uint32_t)((hm >> (4 * j + 0)) | (hm >> (4 * j + 1)) | (hm >> (4 * j + 2)) |
-                                                          (hm >> (4 * j + 3))) & 1u ? (1u << j) : 0u;
-        if (lane == 0) reinterpret_cast<uint16_t *>(p.out.hitmask + t)[quarter] = (uint16_t)part16;
-    }
-    if (!writer || !inside) return;
-    Record o;
-    record(p, r, x, gy, o);
-    store_outputs(p.out, out_index(p, lr, gy, x), o);
+    if (code <= 4) seg_part<MODE, FA, 4>(p, stk_base, t, code - 1, bx, by);
+    else seg_part<MODE, FA, 8>(p, stk_base, t, code - 5, bx, by);
 }
 
 // ------------------------------------------------------------- samples in flight
@@ -1507,7 +1527,7 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
         return hipGetLastError();
     }
     if (!COUNT && p.seg > 0) {   // segmented heavy tiles (the order was built with seg_cap = p.seg)
-        const dim3 sgrid((unsigned)order_strips_grid(bx * by, p.seg));
+        const dim3 sgrid((unsigned)order_strips_grid(bx * by, p.seg, p.seg_kmax));
         if (p.lat)
             hipLaunchKernelGGL((render_seg_kernel<MODE, true, true>), sgrid, block, 2 * lds, stream, p, bx);
         else if (p.fetch_all)
@@ -1661,19 +1681,21 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
                                                                      uint32_t *__restrict__ order, int n, int tiles_x,
                                                                      uint32_t *stats, int seg_cap,
                                                                      const uint16_t *__restrict__ part_cost,
-                                                                     int seg_classes) {
+                                                                     int seg_kpack) {
     __shared__ uint32_t red[ORDER_THREADS / 64], red_sum[ORDER_THREADS / 64];
     constexpr int NC = 6;
     __shared__ uint32_t cnt[NC], base[NC + 1], rank[NC], segs[NC];
     const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int len = n / 8, tiles_y = n / tiles_x;
-    const int L = len + (SEG_K - 1) * seg_cap;   // every XCD's list length (grid = 8 L)
-    // a segmented tile's quarters recorded their own continuous-equivalent trips (render_seg_kernel)
+    const int L = len + (seg_kmax_of(seg_kpack) - 1) * seg_cap;   // every XCD's list length (grid = 8 L)
+    // a segmented tile's parts recorded their own continuous-equivalent trips (render_seg_kernel)
     auto cost_at = [&](int t) -> uint32_t {
         const uint32_t k = cost_in[t];
         if (!(k & SEG_COST_FLAG) || !part_cost) return k & 0x7FFFu;
-        const uint2 q = *reinterpret_cast<const uint2 *>(part_cost + 4 * (size_t)t);
-        return max(max(q.x & 0xFFFFu, q.x >> 16), max(q.y & 0xFFFFu, q.y >> 16));
+        const uint4 q = *reinterpret_cast<const uint4 *>(part_cost + SEG_KMAX * (size_t)t);
+        uint32_t m = max(max(q.x & 0xFFFFu, q.x >> 16), max(q.y & 0xFFFFu, q.y >> 16));
+        if ((k & 15u) == 8u) m = max(m, max(max(q.z & 0xFFFFu, q.z >> 16), max(q.w & 0xFFFFu, q.w >> 16)));
+        return m;
     };
     // position e of this XCD's list is (column c = e / tiles_y, row e % tiles_y) of its
     // strips (strip_tile); the threads walk it in steps of ORDER_THREADS with one
@@ -1725,15 +1747,16 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     __syncthreads();
     const int G = 8 * L;   // the grid, and where the class ends go
     if (tid == 0) {
-        // seg_cap > 0: the tiles of the three classes >= max / 2 (heaviest first, at most
-        // seg_cap per XCD) take SEG_K consecutive slots each, one per quarter
+        // seg_cap > 0: the tiles of the classes seg_kpack segments (heaviest first, at most seg_cap
+        // per XCD) take K consecutive slots each, one per part
         uint32_t run = 0, left = (uint32_t)seg_cap;
         for (int c = 0; c < NC; ++c) {
-            segs[c] = c < seg_classes ? min(cnt[c], left) : 0u;
+            const uint32_t kc = (uint32_t)(seg_kpack >> (4 * c)) & 15u;
+            segs[c] = kc > 1 ? min(cnt[c], left) : 0u;
             left -= segs[c];
             base[c] = run;
             rank[c] = 0;
-            run += cnt[c] + (SEG_K - 1) * segs[c];
+            run += cnt[c] + (kc > 1 ? kc - 1 : 0u) * segs[c];
             if (c >= 2) order[G + 4 + 4 * x + (c - 2)] = run;   // prio class ends
         }
         base[NC] = run;
@@ -1744,12 +1767,13 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         const int t = tile_of(w);
         const int c = cls(cost_at(t));
         const uint32_t r = atomicAdd(&rank[c], 1u);
+        const uint32_t kc = (uint32_t)(seg_kpack >> (4 * c)) & 15u;
         if (r < segs[c]) {
-            const uint32_t j = base[c] + SEG_K * r;
-#pragma unroll
-            for (int q = 0; q < SEG_K; ++q) order[(size_t)(j + q) * 8 + x] = (uint32_t)t | ((uint32_t)(q + 1) << 28);
+            const uint32_t j = base[c] + kc * r;
+            const uint32_t code0 = kc == 4 ? 1u : 5u;   // part q: code0 + q
+            for (uint32_t q = 0; q < kc; ++q) order[(size_t)(j + q) * 8 + x] = (uint32_t)t | ((code0 + q) << 28);
         } else {
-            const uint32_t j = base[c] + (SEG_K - 1) * segs[c] + r;
+            const uint32_t j = base[c] + (kc > 1 ? kc - 1 : 0u) * segs[c] + r;
             order[(size_t)j * 8 + x] = (uint32_t)t;
         }
     }
@@ -1757,12 +1781,17 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
 }
 
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
-                               uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_classes) {
+                               uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_kpack) {
     if (n_tiles <= 0) return hipSuccess;
     if (seg_cap > 0 && (n_tiles / tiles_x) * tiles_x != n_tiles) return hipErrorInvalidValue;
-    if (seg_cap > 0 && ((size_t)order_strips_grid(n_tiles, seg_cap) >> 28) != 0) return hipErrorInvalidValue;
+    for (int c = 0; c < 6; ++c) {
+        const int kc = (seg_kpack >> (4 * c)) & 15;
+        if (kc != 0 && kc != 4 && kc != 8) return hipErrorInvalidValue;
+    }
+    if (seg_cap > 0 && ((size_t)order_strips_grid(n_tiles, seg_cap, seg_kmax_of(seg_kpack)) >> 28) != 0)
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
-                       stats, seg_cap, part_cost, seg_classes);
+                       stats, seg_cap, part_cost, seg_kpack);
     return hipGetLastError();
 }
 

@@ -70,11 +70,11 @@ enum { STAGE_KERNEL = 0, STAGE_ASSEMBLE = 1, N_STAGES = 2 };
 struct Geo {
     int width = -1, local_rows = -1, rows = -1, rank = -1, count = -1, xcd = -1, n_tiles = -1;
     int seg = 0;    // the order's seg_cap (segmented heavy tiles, svo_kernel.hip render_seg_kernel) ...
-    int segc = 0;   // ... and how many cost classes it segments
+    int kpack = 0;  // ... and the K of each cost class (launch_order_strips' seg_kpack)
     uint64_t deal = 0;
     bool operator==(const Geo &o) const {
         return width == o.width && local_rows == o.local_rows && rows == o.rows && rank == o.rank &&
-               count == o.count && xcd == o.xcd && n_tiles == o.n_tiles && seg == o.seg && segc == o.segc &&
+               count == o.count && xcd == o.xcd && n_tiles == o.n_tiles && seg == o.seg && kpack == o.kpack &&
                deal == o.deal;
     }
     bool operator!=(const Geo &o) const { return !(*this == o); }
@@ -99,7 +99,7 @@ struct Sched {
     // build event of a build it follows by >= 2 launches once, before its kernel, and only if the
     // host has not already seen that build complete (a held view: never).
     uint16_t *cost_buf[2] = {};
-    uint16_t *part_buf[2] = {};          // segmented tiles: per tile and quarter (4 x cap)
+    uint16_t *part_buf[2] = {};          // segmented tiles: per tile and part (SEG_KMAX x cap)
     uint32_t *order_buf[2] = {};
     hipStream_t side = nullptr;
     hipEvent_t render_done = nullptr;    // recorded on the render stream behind a launch a build follows
@@ -280,12 +280,11 @@ struct svo_ctx {
     int shadow_compact = 0;          // env SVO_SHADOW_COMPACT=1: that launch over the compacted hit list
     int lat_mode = -1;               // env SVO_LAT: 0 never, 1 always, unset: by the last launch's costs (see launch)
     int seg_mode = 1;                // env SVO_SEG=0: never trace heavy tiles as segmented rays (see launch)
-    int seg_classes = 3;             // env SVO_SEG_CLASSES: cost classes segmented in a latency-bound launch (3: the
-                                     // tiles of cost >= max / 2)
-    int seg_classes_issue = 1;       // env SVO_SEG_CLASSES_ISSUE: the same in an issue-bound launch (1: >= 7/8 max;
-                                     // 0: none)
+    int seg_kpack_lat = 0x444;       // env SVO_SEG_LAT=<hex>: the K of each cost class (nibble c: class c, >= 7/8,
+                                     // 3/4, 1/2, 1/4, 1/8 of the max, rest; 0 none, 4 or 8) in a latency-bound launch
+    int seg_kpack_issue = 0x4;       // env SVO_SEG_ISSUE=<hex>: the same in an issue-bound launch
     int seg_cap = 96;                // env SVO_SEG_CAP: at most this many segmented tiles per XCD
-    int seg_all = 0;                 // env SVO_SEG_ALL=1 (tests): every tile segmented
+    int seg_all = 0;                 // env SVO_SEG_ALL=4|8 (tests; 1 = 4): every tile segmented with that K
     uint32_t seg_scramble = 0;       // env SVO_SEG_SCRAMBLE=<seed> (tests): arbitrary segment starts
     uint32_t seg_launches = 0;
     double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold
@@ -817,8 +816,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             for (int i = 0; i < 2; ++i) {
                 HIP_TRY(hipMalloc(&q->cost_buf[i], cap * sizeof(uint16_t)));
                 HIP_TRY(hipMemset(q->cost_buf[i], 0, cap * sizeof(uint16_t)));
-                HIP_TRY(hipMalloc(&q->part_buf[i], 4 * cap * sizeof(uint16_t)));
-                HIP_TRY(hipMemset(q->part_buf[i], 0, 4 * cap * sizeof(uint16_t)));
+                HIP_TRY(hipMalloc(&q->part_buf[i], svo::SEG_KMAX * cap * sizeof(uint16_t)));
+                HIP_TRY(hipMemset(q->part_buf[i], 0, svo::SEG_KMAX * cap * sizeof(uint16_t)));
                 HIP_TRY(hipMalloc(&q->order_buf[i], order_need * sizeof(uint32_t)));
             }
             HIP_TRY(hipMalloc(&q->shadow_cost, cap * sizeof(uint16_t)));
@@ -834,8 +833,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 if (q->seg_hint) hipFree(q->seg_hint);
                 q->seg_hint = nullptr;
                 q->hint_cap = 0;
-                HIP_TRY(hipMalloc(&q->seg_hint, px * sizeof(float4)));
-                HIP_TRY(hipMemset(q->seg_hint, 0xFF, px * sizeof(float4)));   // NaN: no starts yet
+                HIP_TRY(hipMalloc(&q->seg_hint, 2 * px * sizeof(float4)));
+                HIP_TRY(hipMemset(q->seg_hint, 0xFF, 2 * px * sizeof(float4)));   // NaN: no starts yet
                 q->hint_cap = px;
             }
         }
@@ -875,7 +874,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     const int mode_now = p.shadows | (stack_mode << 2);
     p.lat = 0;
     bool latency_bound = false;
-    const bool have_order = q && [&] { Geo g = q->order_key; g.seg = g.segc = 0; return g == key; }();
+    const bool have_order = q && [&] { Geo g = q->order_key; g.seg = g.kpack = 0; return g == key; }();
     if (!p.guard && p.shadows == 0 && !p.out.fetches && !p.samples && (ctx->lat_mode != 0 || seg_cap)) {
         if (ctx->lat_mode == 1) {
             latency_bound = true;
@@ -919,9 +918,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     }
     if (q) {   // the order this launch dispatches in: with segmented heavy tiles if so decided
         okey = key;
-        okey.segc = ctx->seg_all ? 6 : latency_bound ? ctx->seg_classes : ctx->seg_classes_issue;
-        okey.seg = seg_cap && okey.segc ? seg_cap : 0;
-        if (!okey.seg) okey.segc = 0;
+        okey.kpack = ctx->seg_all ? ctx->seg_all * 0x111111 : latency_bound ? ctx->seg_kpack_lat : ctx->seg_kpack_issue;
+        okey.seg = seg_cap && okey.kpack ? seg_cap : 0;
+        if (!okey.seg) okey.kpack = 0;
         // the newest build it follows by >= 2 launches (Sched): a build that launch n - 2 was
         // followed by read the cost buffer this launch writes, so it is waited for whatever its key
         const long long n = (long long)q->launches;
@@ -939,6 +938,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         p.tile_order = use >= 0 ? q->order_buf[use] : nullptr;
         if (p.tile_order && okey.seg) {   // the order lists quarter entries: the segmented kernel
             p.seg = okey.seg;
+            p.seg_kmax = svo::seg_kmax_of(okey.kpack);
             p.seg_hint = q->seg_hint;
             if (ctx->seg_scramble) p.seg_scramble = ctx->seg_scramble * 0x9E3779B9u + ++ctx->seg_launches;
         }
@@ -996,7 +996,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         HIP_TRY(hipEventRecord(q->render_done, s));
         HIP_TRY(hipStreamWaitEvent(q->side, q->render_done, 0));
         e = p.xcd_remap == 2 ? svo::launch_order_strips(p.tile_cost, q->order_buf[bi], n_tiles, (width + 7) / 8, q->side,
-                                                        st16, okey.seg, p.part_cost, okey.segc)
+                                                        st16, okey.seg, p.part_cost, okey.kpack)
                              : svo::launch_order_tiles(p.tile_cost, q->order_buf[bi], n_tiles, q->side, st16);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         HIP_TRY(hipEventRecord(q->build_ev[bi], q->side));
@@ -1367,10 +1367,20 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_MOVE_EVERY")) ctx->move_every = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_LAT")) ctx->lat_mode = std::atoi(k) != 0 ? 1 : 0;
     if (const char *k = std::getenv("SVO_SEG")) ctx->seg_mode = std::atoi(k) != 0 ? 1 : 0;
-    if (const char *k = std::getenv("SVO_SEG_CLASSES")) ctx->seg_classes = std::min(6, std::max(1, std::atoi(k)));
-    if (const char *k = std::getenv("SVO_SEG_CLASSES_ISSUE")) ctx->seg_classes_issue = std::min(6, std::max(0, std::atoi(k)));
+    auto kpack_env = [](const char *name, int dflt) {
+        const char *k = std::getenv(name);
+        if (!k) return dflt;
+        const int v = (int)std::strtol(k, nullptr, 16);
+        for (int c = 0; c < 6; ++c) {
+            const int kc = (v >> (4 * c)) & 15;
+            if (kc != 0 && kc != 4 && kc != 8) return dflt;   // not a valid table: the default
+        }
+        return v & 0xFFFFFF;
+    };
+    ctx->seg_kpack_lat = kpack_env("SVO_SEG_LAT", ctx->seg_kpack_lat);
+    ctx->seg_kpack_issue = kpack_env("SVO_SEG_ISSUE", ctx->seg_kpack_issue);
     if (const char *k = std::getenv("SVO_SEG_CAP")) ctx->seg_cap = std::max(1, std::atoi(k));
-    if (const char *k = std::getenv("SVO_SEG_ALL")) ctx->seg_all = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_SEG_ALL")) ctx->seg_all = std::atoi(k) == 8 ? 8 : std::atoi(k) != 0 ? 4 : 0;
     if (const char *k = std::getenv("SVO_SEG_SCRAMBLE")) ctx->seg_scramble = (uint32_t)std::strtoul(k, nullptr, 10);
     if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
     if (e != hipSuccess) {

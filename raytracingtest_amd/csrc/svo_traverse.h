@@ -109,21 +109,22 @@ struct LaunchParams {
     uint32_t *accum8;          // display RGBA8 of the blended pixels (nullable)
     uint8_t *accum_rgb8;       // the same as 3-byte RGB, the band payload (nullable)
     // Segmented heavy tiles (svo_kernel.hip render_seg_kernel; seg != 0 only with an order built
-    // by launch_order_strips(..., seg_cap > 0)): an order entry t | (q + 1) << 28 is quarter q of
-    // tile t, traced as SEG_K t-segments per ray (lanes 4 r .. 4 r + 3 = ray r's segments);
-    // 0xFFFFFFFF is an empty slot.  seg_hint: per pixel (band-local lr * width + x) the segment
-    // starts t_1..t_3 of the ray's last segmented trace (NaN: none), rewritten by every such
-    // trace; part_cost: per tile and quarter the wave's continuous-equivalent trips (the tile's
-    // tile_cost then holds SEG_COST_FLAG).  seg = the order's seg_cap (0: no segmented tiles).
-    int seg;
+    // by launch_order_strips(..., seg_cap > 0)): an order entry t | code << 28 is part q of tile t
+    // traced as K t-segments per ray (code 1 + q for K = 4, 5 + q for K = 8; lanes K r .. K r + K - 1
+    // = ray r's segments); 0xFFFFFFFF is an empty slot.  seg_hint: per pixel (band-local lr * width
+    // + x) two float4, the starts at fractions 1/8 .. 7/8 of the ray's last segmented trace (NaN:
+    // none), rewritten by every such trace; part_cost: per tile SEG_KMAX entries, each part's
+    // continuous-equivalent trips (the tile's tile_cost then holds SEG_COST_FLAG | K).
+    // seg = the order's seg_cap (0: no segmented tiles), seg_kmax its largest K.
+    int seg, seg_kmax;
     float4 *seg_hint;
     uint16_t *part_cost;
     uint32_t seg_scramble;     // tests (env SVO_SEG_SCRAMBLE): != 0 replaces every start by a hash of
                                // (pixel, this value) -- unordered, NaN, +-inf, outside the cube
 };
 
-constexpr int SEG_K = 4;                    // segments per ray (one lane quad)
-constexpr uint16_t SEG_COST_FLAG = 0x8000;  // tile_cost of a segmented tile: read part_cost
+constexpr int SEG_KMAX = 8;                 // segments per ray: 4 (a lane quad) or 8, by cost class
+constexpr uint16_t SEG_COST_FLAG = 0x8000;  // tile_cost of a segmented tile (| its K): read part_cost
 constexpr uint32_t SEG_EMPTY = 0xFFFFFFFFu; // order slot with nothing to trace
 
 // Re-interleave the band parts of a split frame on the display device
@@ -166,12 +167,23 @@ size_t order_cost_capacity(int n_tiles);
 // entries for render_seg_kernel, the lists padded to one length with SEG_EMPTY; a segmented
 // tile's cost is the max of its part_cost entries.  The render grid is then
 // order_strips_grid(n_tiles, seg_cap) workgroups.
-// seg_classes: how many of the six cost classes qualify (3: cost >= max / 2; 6: every tile).
+// seg_kpack: the K of cost class c (>= 7/8, 3/4, 1/2, 1/4, 1/8 of the XCD's max, rest) in bits
+// 4 c .. 4 c + 3: 0 = not segmented, 4 or 8.
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
                                uint32_t *stats = nullptr, int seg_cap = 0, const uint16_t *part_cost = nullptr,
-                               int seg_classes = 3);
-inline int order_strips_grid(int n_tiles, int seg_cap) { return n_tiles + 8 * (SEG_K - 1) * seg_cap; }
-inline size_t order_strips_entries(int n_tiles, int seg_cap) { return (size_t)order_strips_grid(n_tiles, seg_cap) + 36; }
+                               int seg_kpack = 0);
+__host__ __device__ inline int seg_kmax_of(int kpack) {
+    int m = 1;
+    for (int c = 0; c < 6; ++c) {
+        const int k = (kpack >> (4 * c)) & 15;
+        m = k > m ? k : m;
+    }
+    return m;
+}
+inline int order_strips_grid(int n_tiles, int seg_cap, int kmax) { return n_tiles + 8 * (kmax - 1) * seg_cap; }
+inline size_t order_strips_entries(int n_tiles, int seg_cap, int kmax = SEG_KMAX) {
+    return (size_t)order_strips_grid(n_tiles, seg_cap, kmax) + 36;
+}
 
 // Progressive accumulation (AddShader blend) of an RGBA32F sample frame.
 hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32_t sample, int num_cus,

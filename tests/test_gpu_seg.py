@@ -53,36 +53,38 @@ def _frames(torch, oracle_mod, svo, cams, w, h, mode, n_frames=3, keys=None):
         m.close()
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_every_tile_segmented_matches_oracle(torch, oracle_mod, monkeypatch, text_svo, mode):
-    """Every tile traced as 4 segments per ray: every output of every frame equals the oracle."""
-    monkeypatch.setenv("SVO_SEG_ALL", "1")
+@pytest.mark.parametrize("mode,k", [(0, 4), (1, 4), (0, 8), (1, 8)])
+def test_every_tile_segmented_matches_oracle(torch, oracle_mod, monkeypatch, text_svo, mode, k):
+    """Every tile traced as K = 4 or 8 segments per ray: every output of every frame equals the oracle."""
+    monkeypatch.setenv("SVO_SEG_ALL", str(k))
     _frames(torch, oracle_mod, text_svo, [main_camera(), overview_camera()], 256, 256, mode)
     _frames(torch, oracle_mod, build_menger(8), [overview_camera()], 480, 272, mode)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_arbitrary_segment_starts_match_oracle(torch, oracle_mod, monkeypatch, mode):
+@pytest.mark.parametrize("mode,k", [(0, 4), (1, 4), (0, 8), (1, 8)])
+def test_arbitrary_segment_starts_match_oracle(torch, oracle_mod, monkeypatch, mode, k):
     """Starts that are unordered, NaN, +-inf or outside the cube (a new hash every launch):
     the records do not depend on them."""
-    monkeypatch.setenv("SVO_SEG_ALL", "1")
+    monkeypatch.setenv("SVO_SEG_ALL", str(k))
     monkeypatch.setenv("SVO_SEG_SCRAMBLE", "12345")
     _frames(torch, oracle_mod, build_menger(8), [overview_camera()], 480, 272, mode, n_frames=4,
             keys=("hits", "rgba", "position", "voxel"))
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_c3_heavy_tiles_segmented_full_frame(torch, oracle_mod, monkeypatch, c3_svo, mode):
-    """The bench workload (C3, 1920x1080, flyover) with the launch's own rule (each XCD's tiles of
-    cost >= half its heaviest): six consecutive frames, every ray equal to the oracle's."""
-    monkeypatch.setenv("SVO_SEG", "1")
+@pytest.mark.parametrize("mode,table", [(0, "448"), (1, "448"), (0, "888")])
+def test_c3_heavy_tiles_segmented_full_frame(torch, oracle_mod, monkeypatch, c3_svo, mode, table):
+    """The bench workload (C3, 1920x1080, flyover), each XCD's heaviest classes segmented as the
+    launch's own rule does (the class table forced for every launch, K = 4 and 8 mixed): six
+    consecutive frames, every ray equal to the oracle's."""
+    monkeypatch.setenv("SVO_SEG_LAT", table)
+    monkeypatch.setenv("SVO_SEG_ISSUE", table)
     w, h = 1920, 1080
     _frames(torch, oracle_mod, c3_svo, [CAMERAS["flyover"]()], w, h, mode, n_frames=6, keys=("hits", "rgba"))
 
 
 def test_c3_segmented_moving_camera(torch, oracle_mod, monkeypatch, c3_svo):
     """A pan (a new view per frame, starts carried over from the previous view), then held."""
-    monkeypatch.setenv("SVO_SEG", "1")
+    monkeypatch.setenv("SVO_SEG_ISSUE", "488")
     monkeypatch.setenv("SVO_MOVE_EVERY", "1")
     from raytracingtest_amd.camera import FLYOVER_EYE, FLYOVER_TARGET
     w, h = 1920, 1080
@@ -94,11 +96,11 @@ def test_c3_segmented_moving_camera(torch, oracle_mod, monkeypatch, c3_svo):
     _frames(torch, oracle_mod, c3_svo, cams, w, h, 0, n_frames=2, keys=("hits", "rgba"))
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_segmented_band_and_hit_masks(torch, oracle_mod, monkeypatch, mode):
+@pytest.mark.parametrize("mode,k", [(0, 4), (1, 4), (0, 8)])
+def test_segmented_band_and_hit_masks(torch, oracle_mod, monkeypatch, mode, k):
     """Rank 1's band of an 8-way 8-row split (the strong split's per-GPU launch), with the sparse
     payload's per-tile hit masks: records, RGB payload and masks equal the oracle's."""
-    monkeypatch.setenv("SVO_SEG_ALL", "1")
+    monkeypatch.setenv("SVO_SEG_ALL", str(k))
     svo = build_menger(8)
     w, h = 512, 384
     cam = overview_camera()

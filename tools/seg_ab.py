@@ -23,8 +23,8 @@ def main():
     ap.add_argument("--timed", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--variants", default="off,auto",
-                    help="comma list of: off (SVO_SEG=0), auto (the library's defaults), c<n> (SVO_SEG_CLASSES=n), "
-                         "i<n> (SVO_SEG_CLASSES_ISSUE=n)")
+                    help="comma list of: off (SVO_SEG=0), auto (the library's defaults), or '+'-joined "
+                         "l<hex> (SVO_SEG_LAT: K per cost class, class 0 in the low nibble) and i<hex> (SVO_SEG_ISSUE)")
     ap.add_argument("--cap", default=None, help="SVO_SEG_CAP")
     ap.add_argument("--cameras", default=None, help="comma list (default: --camera)")
     a = ap.parse_args()
@@ -44,14 +44,15 @@ def main():
     cams = (a.cameras or a.camera).split(",")
     for rnd in range(a.rounds):
         for name in a.variants.split(","):
-            for k in ("SVO_SEG", "SVO_SEG_CLASSES", "SVO_SEG_CLASSES_ISSUE", "SVO_SEG_CAP"):
+            for k in ("SVO_SEG", "SVO_SEG_LAT", "SVO_SEG_ISSUE", "SVO_SEG_CAP"):
                 os.environ.pop(k, None)
-            if name == "off":
-                os.environ["SVO_SEG"] = "0"
-            elif name.startswith("c"):     # c<n>: SVO_SEG_CLASSES (latency-bound launches)
-                os.environ["SVO_SEG_CLASSES"] = name[1:]
-            elif name.startswith("i"):     # i<n>: SVO_SEG_CLASSES_ISSUE (issue-bound launches)
-                os.environ["SVO_SEG_CLASSES_ISSUE"] = name[1:]"
+            for part in name.split("+"):
+                if part == "off":
+                    os.environ["SVO_SEG"] = "0"
+                elif part.startswith("l"):     # l<hex>: SVO_SEG_LAT, the class table of latency-bound launches
+                    os.environ["SVO_SEG_LAT"] = part[1:]
+                elif part.startswith("i"):     # i<hex>: SVO_SEG_ISSUE, the same for issue-bound launches
+                    os.environ["SVO_SEG_ISSUE"] = part[1:]"
             if a.cap:
                 os.environ["SVO_SEG_CAP"] = a.cap
             for cam in cams:
