@@ -229,6 +229,7 @@ def main():
     bytes_per_launch, elapsed, kern_ms, kern_ms_max = (m["bytes_per_launch"], m["elapsed"], m["kern_ms"],
                                                        m["kern_ms_max"])
     stages, frame_check, per_rank, step_ms = m["stages"], m["frame_check"], m["per_rank"], m["step_ms"]
+    F_ref = m["F_ref"]
 
     # the other frame of an N > 1 run, reported beside `value` and labelled: the
     # weak frame (sqrt(N) x the linear resolution, ~W x H rays per GPU) when the run
@@ -347,7 +348,8 @@ def main():
                                                                else "built_on_every_rank"),
                        "rays_per_step": rays_per_step, "rays_per_gpu_step": n_px,
                        "hit_fraction_rank0": round(n_hit / n_px, 4),
-                       "fetches_per_ray_rank0": round(F / n_px, 3), "parallelism": par},
+                       "fetches_per_ray_rank0": round(F / n_px, 3),
+                       "fetches_per_ray_reference_rank0": round(F_ref / n_px, 3), "parallelism": par},
             "roofline": {"bound": "latency", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
@@ -375,12 +377,19 @@ def main():
                          # SURVEY.md 8(d)'s own formula with the V2 node width: 8*F + 8*hits + 24*rays
                          "frac_survey": round((8 * F + 8 * n_hit + 24 * n_px) / (kern_ms * 1e-3) / 1e9
                                               / HBM_PEAK_GBS, 5),
+                         # the reference's walk from the cube entry (F_ref fetches): the work the kernel
+                         # replaces, over its time -- an effective rate, not bytes moved
+                         "frac_reference_work": round((bytes_per_launch + 8 * (F_ref - F)) / (kern_ms * 1e-3) / 1e9
+                                                      / HBM_PEAK_GBS, 5),
                          "frac_ref_node_width": round((bytes_per_launch - 4 * F) / (kern_ms * 1e-3) / 1e9
                                                       / HBM_PEAK_GBS, 5),
                          "read_frac_ref_node_width": round((4 * F + 8 * n_hit) / (kern_ms * 1e-3) / 1e9
                                                            / HBM_PEAK_GBS, 5),
-                         "accountings": "frac: 8-B V2 node fetches + attachment + hit record + RGBA32F (+ payload) "
-                                        "writes; frac_survey: SURVEY 8(d)'s 8*F + 8*hits + 24*rays; "
+                         "accountings": "F = the node fetches of the walk the kernel runs (from the beam start, "
+                                        "DESIGN.md 3.1d); frac: 8-B V2 node fetches + attachment + hit record + "
+                                        "RGBA32F (+ payload) writes; frac_survey: SURVEY 8(d)'s 8*F + 8*hits + 24*rays; "
+                                        "frac_reference_work: frac with the reference walk's fetches (F_ref, from the "
+                                        "cube entry) in place of F; "
                                         "read_frac: node + attachment reads only (8*F + 8*hits); "
                                         "*_ref_node_width: the same with the reference's 4-byte descriptors (4*F); "
                                         "hbm_frac: what the PMC counters saw cross the fabric",
@@ -461,6 +470,12 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     # instrumented pass (outside the timed region): per-ray fetch counts
     fetch = torch.zeros(max(n_px, 1), dtype=torch.int32, device=dev)
     rm.count_fetches_device(W, H, fetch.data_ptr(), stack_mode=args.stack_mode, band=band, stream=sptr)
+    # ... and of the walk the render runs (from the beam start): the node reads the
+    # kernel actually makes, the `frac` accounting; the reference's walk above gives frac_reference_work
+    fetch_run = torch.zeros_like(fetch)
+    rm.set_count_beam(True)
+    rm.count_fetches_device(W, H, fetch_run.data_ptr(), stack_mode=args.stack_mode, band=band, stream=sptr)
+    rm.set_count_beam(False)
     for _ in range(max(1, args.warmup)):
         step()
     drain()
@@ -508,7 +523,8 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     kern_ms = max(kern_ms_events - floor_ms, 1e-6)
     host_hits = (hits if gather is None else gather.local_hits()).cpu().numpy().view(_lib.HIT_DTYPE)
     n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
-    F = int(fetch[:n_px].to(torch.int64).sum().item())
+    F_ref = int(fetch[:n_px].to(torch.int64).sum().item())
+    F = int(fetch_run[:n_px].to(torch.int64).sum().item())
     bytes_per_launch = 8 * F + 8 * n_hit + 24 * n_px + (0 if args.no_rgba else 16 * n_px)
     if gather is not None:
         # the RGBA8 display words (rank 0, in the frame) or band payload (3 B RGB / 4 B RGBA8 /
@@ -527,7 +543,8 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     else:
         kern_ms_max = kern_ms
         per_rank = None
-    return dict(gather=gather, hits=hits, rgba=rgba, n_px=n_px, n_hit=n_hit, F=F, host_hits=host_hits, band=band,
+    return dict(gather=gather, hits=hits, rgba=rgba, n_px=n_px, n_hit=n_hit, F=F, F_ref=F_ref, host_hits=host_hits,
+                band=band,
                 deal_info=deal_info, payload_choice=payload_choice, bytes_per_launch=bytes_per_launch,
                 elapsed=elapsed, kern_ms=kern_ms, kern_ms_max=kern_ms_max, stages=stages, frame_check=frame_check,
                 per_rank=per_rank, step_ms=step_ms, step=step, kern_ms_events=kern_ms_events, floor_ms=floor_ms)

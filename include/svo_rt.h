@@ -241,7 +241,10 @@ int svo_pack_hits(svo_ctx *ctx, int width, int height, const svo_band *band, con
 
 /* Instrumented trace: per-ray descriptor-fetch counts (device uint32 array,
  * NVIDIASVO.compute:60-62 executions), used for the algorithmic-bytes figure
- * of the roofline.  Same arguments as svo_render_device plus d_fetches. */
+ * of the roofline.  Same arguments as svo_render_device plus d_fetches.
+ * By default the reference's own walk from the cube entry; with the option
+ * SVO_OPT_COUNT_BEAM the walk the render actually runs, from the beam start
+ * (DESIGN.md 3.1d). */
 int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode,
                       const svo_band *band, void *d_fetches, void *stream);
 
@@ -250,7 +253,7 @@ int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode,
  * the reference's shadow test is commented out at RaytraceCompute.compute:105-112):
  * origin = world hit point + 0.001 * normal; an occluded pixel gets hit flag
  * bit 3 and a black Result. */
-enum { SVO_OPT_SHADOW_RAYS = 1, SVO_OPT_KERNEL_TIMING = 2 };
+enum { SVO_OPT_SHADOW_RAYS = 1, SVO_OPT_KERNEL_TIMING = 2, SVO_OPT_COUNT_BEAM = 4 };
 int svo_set_options(svo_ctx *ctx, uint32_t options);
 
 /* SVO_OPT_KERNEL_TIMING: every render launch brackets its primary-ray kernel

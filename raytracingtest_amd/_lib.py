@@ -38,6 +38,7 @@ EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera"
            "svo_render_progressive_async", "svo_progressive_last", "svo_forget_stream")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
+SVO_OPT_COUNT_BEAM = 4
 LAYOUT_BAND, LAYOUT_FRAME = 0, 1
 PART_COMPACT, PART_RGBA8, PART_RGB8, PART_SPARSE_RGB8 = 0, 1, 2, 3
 LINK_SELF, LINK_PEER, LINK_COPY = 0, 1, 2

@@ -700,6 +700,199 @@ __device__ __forceinline__ size_t out_index(const LaunchParams &p, int lr, int g
     return (size_t)(p.out.frame_layout ? gy : lr) * (size_t)p.width + (size_t)x;
 }
 
+// ------------------------------------------------------------- segmented rays
+// One ray's traversal split into K t-segments that run side by side (VERDICT r4 item 1:
+// a heavy tile's wave is a serial chain of up to ~270 trips that bounds a frame split over N
+// GPUs, DESIGN.md 6.1; modelled first, tools/segment_model.py).  Segment k of a ray with
+// starts t_1 .. t_{K-1} (any floats, NaN included: the result never depends on them, only the
+// balance does) runs the lean loop from the cube entry with three changes:
+//   * SKIP: a non-leaf child it would descend into whose exit tc_max is below t_k lies wholly
+//     before t_k.  The lane instead takes the state the loop has after descending into it and
+//     popping back -- the stack entry that PUSH stores (N:97-98, also when h allows it), t_max
+//     through the HLSL float2 round trip (N:141-143), h = 0 (N:153) -- and ADVANCEs past it.
+//     Every ADVANCE inside such a subtree has t_min <= its tc_max < t_k (the corner times
+//     p * coef - bias are monotone in p, so a sub-cell's exit cannot pass its parent's), so the
+//     lane follows the continuous loop's own path, state for state, minus those subtrees.
+//   * ARM: a hit (N:93-94) counts only once the lane is armed: segment 0 from the start,
+//     segment k at the first ADVANCE whose new t_min >= t_k (before it, a leaf is stepped past).
+//   * STOP: segment k ends, without a hit, at the first ADVANCE whose new t_min >= t_{k+1} --
+//     the very event that arms segment k + 1 on the same path.
+// The ray's record is that of its first segment that did not stop (a hit, or the ray left
+// the cube): the segments before it covered everything up to its arming event without a hit.
+// Bit-identical to the continuous loop in both stack modes (tests/test_gpu_seg.py against the
+// oracle, with real and with random starts).
+// SEGS = false: one segment from t_start with no stop (a beam start): no STOP test
+// and no per-lane trip bookkeeping.
+// COUNT: per-lane descriptor fetches in r.fetches, with the HLSL re-fetch of a zero descriptor
+// (trace_lean's COUNT form; svo_count_fetches under SVO_OPT_COUNT_BEAM).
+template <int MODE, bool FETCH_ALL, bool SEGS = true, bool COUNT = false>
+__device__ __forceinline__ void trace_seg(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk, float t_start,
+                                          float t_stop, bool armed0, uint32_t &n_lane, uint32_t &armed_at,
+                                          bool &stopped_lane) {
+    constexpr int STRIDE = TILE;
+    const int slots = p.slots;
+    for (int s = 0; s < slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
+    const int scale_lo = S_MAX - slots;
+    lmask act = LM_OF(true);
+    lmask armed = LM_OF(armed0), stopped = 0, cached = 0;
+    const int oct = r.octant_mask | 16;
+    int sh = r.idx ^ oct;
+    const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
+    constexpr uint32_t SLOT = (uint32_t)(STRIDE * sizeof(uint2));
+    constexpr int SLOT_SH = 23 - 9;
+    const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
+    const uint2 *stk_pop = stk - (127 + scale_lo) * STRIDE;
+    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots - 1);
+    int it = 0;
+    n_lane = 0;
+    armed_at = 0;
+    asm volatile("" : "+v"(r.parent), "+v"(r.cd16), "+v"(r.first));
+    lmask go;
+    do {
+        asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
+        const lmask need = FETCH_ALL ? ~(lmask)0 : act & ~cached;
+        if (FETCH_ALL || LM_ON(need)) {
+            const uint2 nd = *(const uint2 *)((const char *)p.nodes + (uint32_t)(r.parent << 3));
+            r.cd16 = nd.x;
+            r.first = nd.y;
+            if (COUNT) r.fetches += 1u;
+        }
+        cached |= COUNT ? (need & LM_OF((r.cd16 | r.first) != 0u)) : need;
+        const float tx = r.px * r.cx - r.bx;             // N:67-70
+        const float ty = r.py * r.cy - r.by;
+        const float tz = r.pz * r.cz - r.bz;
+        const float tc_max = fminf(fminf(tx, ty), tz);
+        const float tv_max = vmin(r.t_max, tc_max);
+        const float half = r.sexp * 0.5f;
+        const lmask cx = LM_OF(center(half, r.cx, tx) > r.t_min);
+        const lmask cy = LM_OF(center(half, r.cy, ty) > r.t_min);
+        const lmask cz = LM_OF(center(half, r.cz, tz) > r.t_min);
+        const lmask lx = LM_OF(tx <= tc_max), ly = LM_OF(ty <= tc_max), lz = LM_OF(tz <= tc_max);
+        const lmask in_span = LM_OF(r.t_min <= tv_max), below_h = LM_OF(tc_max < r.h);
+        const lmask before = LM_OF(tc_max < t_start);    // SKIP test (NaN start: never)
+        const lmask arm_now = LM_OF(tc_max >= t_start);  // ARM / STOP tests on the ADVANCE's new t_min
+        const lmask stop_now = SEGS ? LM_OF(tc_max >= t_stop) : (lmask)0;
+        const uint32_t cm = r.cd16 << sh;
+        const lmask descend = act & LM_OF((int32_t)cm < 0) & in_span;
+        const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
+        const lmask inner = descend & ~leaf;
+        const lmask skip = inner & before;
+        const lmask hit = descend & leaf & armed;        // N:93-94, armed lanes only
+        const lmask push = inner & ~skip;
+        const lmask store = inner & below_h;             // PUSH's stack write, also for a SKIP
+        const lmask adv = act & ~(hit | push);           // incl. SKIP lanes and unarmed leaves
+        if (LM_ON(store)) {                              // N:97-98
+            const uint32_t a = push_base + (__float_as_uint(r.sexp) >> SLOT_SH);
+            const uint32_t tmw = MODE == 0 ? (uint32_t)cvt_i32((float)(int32_t)__float_as_uint(r.t_max))
+                                           : __float_as_uint(r.t_max);
+            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(tmw) : "memory");
+        }
+        const lmask sx = adv & lx;                       // N:122-125
+        const lmask sy = adv & ly;
+        const lmask sz = adv & lz;
+        const float se = r.sexp;
+        const float delta = LM_ON(push) ? half : -se;
+        const float ox = r.px, oy = r.py, oz = r.pz;
+        const lmask mvx = (push & cx) | sx, mvy = (push & cy) | sy, mvz = (push & cz) | sz;
+        const float qx = r.px + (LM_ON(mvx) ? delta : 0.0f);
+        const float qy = r.py + (LM_ON(mvy) ? delta : 0.0f);
+        const float qz = r.pz + (LM_ON(mvz) ? delta : 0.0f);
+        const int mv = lanes_to_idx(mvx, mvy, mvz);
+        const lmask pop = adv & LM_OF((mv & ~(sh ^ oct)) != 0);
+        const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
+        sh = (LM_ON(push) ? oct : sh) ^ mv;
+        if (LM_ON(push)) {
+            r.parent = child;
+            r.h = tc_max;
+            r.t_max = tv_max;
+            r.sexp = half;
+        }
+        if (skip != 0) {   // back at this node's level as after a POP (N:141-153)
+            if (LM_ON(skip)) {
+                if (MODE == 0) r.t_max = __int_as_float(cvt_i32((float)(int32_t)__float_as_uint(r.t_max)));
+                r.h = 0.0f;
+            }
+        }
+        r.t_min = LM_ON(adv) ? tc_max : r.t_min;
+        const lmask armed_new = adv & arm_now & ~armed;
+        if (armed_new != 0) {
+            if (SEGS && LM_ON(armed_new)) armed_at = (uint32_t)it;
+            armed |= armed_new;
+        }
+        const lmask stop = SEGS ? adv & stop_now : (lmask)0;
+        cached &= ~(push | pop);
+        r.px = qx; r.py = qy; r.pz = qz;
+        lmask out = 0;
+        if (pop != 0) {                                  // N:134-154
+            const uint32_t diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) |
+                                  (__float_as_uint(oy) ^ __float_as_uint(qy)) |
+                                  (__float_as_uint(oz) ^ __float_as_uint(qz));
+            const uint32_t fd = __float_as_uint((float)diff);
+            const uint32_t ef = __builtin_amdgcn_ubfe(fd, 23, 8);
+            const int scale = (int)ef - 127;
+            const uint2 e = stk_pop[min(ef, e_max) * STRIDE];
+            const uint32_t keep = 0xFFFFFFFFu << scale;
+            const uint32_t bx_ = __builtin_amdgcn_ubfe(__float_as_uint(qx), scale, 1);
+            const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
+            const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
+            const bool pl = LM_ON(pop);
+            r.sexp = pl ? __uint_as_float((ef << 23) - (23u << 23)) : r.sexp;
+            r.parent = pl ? e.x : r.parent;
+            r.t_max = pl ? __uint_as_float(e.y) : r.t_max;
+            const uint32_t k = pl ? keep : 0xFFFFFFFFu;
+            r.px = __uint_as_float(__float_as_uint(r.px) & k);
+            r.py = __uint_as_float(__float_as_uint(r.py) & k);
+            r.pz = __uint_as_float(__float_as_uint(r.pz) & k);
+            r.h = pl ? 0.0f : r.h;
+            sh = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) ^ oct : sh;
+            out = pop & LM_OF(scale >= S_MAX);
+        }
+        const lmask fin = act & (hit | out | stop);
+        if (fin != 0) {
+            if (SEGS && LM_ON(fin)) n_lane = (uint32_t)it;
+            stopped |= stop;                             // STOP before the cube exit of the same trip
+            act &= ~fin;
+        }
+        asm volatile("s_cmp_lt_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(go) : "s"(it), "n"(MAX_ITERS), "s"(act) : "scc");
+    } while (go != 0);
+    if (LM_ON(act)) {   // still tracing after MAX_ITERS trips (unreachable for a tree of depth <= 13)
+        r.flags |= 2u;
+        if (SEGS) n_lane = (uint32_t)it;
+    }
+    stopped_lane = LM_ON(stopped);
+    r.idx = sh ^ oct;
+    r.trips = it;
+}
+
+
+// ------------------------------------------------------------- beam starts
+// The start of a primary ray of pixel (x, gy) (global row) under a launch's beam starts
+// (DESIGN.md 3.1d): the min of its tile's, super tile's and the global lower bound, less a margin
+// for rounding.  The bound d is exact geometry (the distance from the camera to the nearest box
+// that can hold a voxel on the ray); the loop's hit t is a corner time p * coef - bias in f32,
+// whose error is at most ~2 ulps of its larger term, 2 ulp(2 |coef| + |bias|) -- a quarter of the
+// margin (2 |coef| + |bias|) 2^-20 summed over the axes -- plus the relative error of d (2^-16).  A ray parallel to an axis (|coef| = inf) starts at -inf: everything
+// as without a beam.  Returns -inf without beam starts.
+__device__ __forceinline__ float beam_start(const LaunchParams &p, const FRay &f, int x, int gy) {
+    if (!p.tile_start) return -__builtin_inff();
+    float d = p.tile_start[(gy >> 3) * p.ts_tiles_x + (x >> 3)];
+    d = fminf(d, p.tile_start[p.ts_super_off + (gy >> 6) * p.ts_super_x + (x >> 6)]);
+    d = fminf(d, p.tile_start[p.ts_global_off]);
+    const float m = (2.0f * (fabsf(f.cx) + fabsf(f.cy) + fabsf(f.cz)) + fabsf(f.bx) + fabsf(f.by) + fabsf(f.bz)) *
+                    0x1p-20f;
+    const float s = d * (1.0f - 0x1p-16f) - m;
+    return s == s ? s : -__builtin_inff();
+}
+
+// The lean loop from a beam start (trace_seg, one segment, no stop): a lane whose cube entry lies
+// at or past the start is armed from the first trip and runs the continuous loop.
+template <int MODE, bool FA, bool COUNT = false>
+__device__ __forceinline__ void trace_beam(const LaunchParams &p, FRay &f, uint2 *__restrict__ stk, float start) {
+    uint32_t n_lane, armed_at;
+    bool stopped;
+    trace_seg<MODE, FA, false, COUNT>(p, f, stk, start, __builtin_inff(), f.t_min >= start, n_lane, armed_at, stopped);
+}
+
 // ------------------------------------------------------------- tile kernel
 // Interleaved XCD column strips (xcd_remap 2).  Workgroups b with b % 8 == x
 // land on XCD x (MI355X_MICROARCH.md "Workgroup dispatch"); tile column c
@@ -770,13 +963,17 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
     FRay f;
     to_fray(r, f);
     LeanDiag dg;
-    if (COUNT) trace_lean<MODE, true, false, false, true>(p, f, stk);
+    if (COUNT) {
+        if (p.tile_start) trace_beam<MODE, false, true>(p, f, stk, beam_start(p, f, x, gy));   // SVO_OPT_COUNT_BEAM
+        else trace_lean<MODE, true, false, false, true>(p, f, stk);
+    }
     else if (LAT) trace_lat<MODE>(p, f, stk);
     else if (!SH && p.wave_log) {
         if (p.guard) trace_lean<MODE, true, true>(p, f, stk, &dg);
         else trace_lean<MODE, false, true>(p, f, stk, &dg);
     }
     else if (p.guard) trace_lean<MODE, true>(p, f, stk);
+    else if (p.tile_start) trace_beam<MODE, FA>(p, f, stk, beam_start(p, f, x, gy));
     else trace_lean<MODE, false, false, FA>(p, f, stk);
     from_fray(f, r);
     if (COUNT) {
@@ -829,165 +1026,6 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
     }
     store_outputs(p.out, out_index(p, lr, gy, x), o);
     if (p.wave_log && lane == 0) p.wave_log[WAVE_LOG_WORDS * (size_t)blockIdx.x + 9] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-}
-
-// ------------------------------------------------------------- segmented rays
-// One ray's traversal split into K t-segments that run side by side (VERDICT r4 item 1:
-// a heavy tile's wave is a serial chain of up to ~270 trips that bounds a frame split over N
-// GPUs, DESIGN.md 6.1; modelled first, tools/segment_model.py).  Segment k of a ray with
-// starts t_1 .. t_{K-1} (any floats, NaN included: the result never depends on them, only the
-// balance does) runs the lean loop from the cube entry with three changes:
-//   * SKIP: a non-leaf child it would descend into whose exit tc_max is below t_k lies wholly
-//     before t_k.  The lane instead takes the state the loop has after descending into it and
-//     popping back -- the stack entry that PUSH stores (N:97-98, also when h allows it), t_max
-//     through the HLSL float2 round trip (N:141-143), h = 0 (N:153) -- and ADVANCEs past it.
-//     Every ADVANCE inside such a subtree has t_min <= its tc_max < t_k (the corner times
-//     p * coef - bias are monotone in p, so a sub-cell's exit cannot pass its parent's), so the
-//     lane follows the continuous loop's own path, state for state, minus those subtrees.
-//   * ARM: a hit (N:93-94) counts only once the lane is armed: segment 0 from the start,
-//     segment k at the first ADVANCE whose new t_min >= t_k (before it, a leaf is stepped past).
-//   * STOP: segment k ends, without a hit, at the first ADVANCE whose new t_min >= t_{k+1} --
-//     the very event that arms segment k + 1 on the same path.
-// The ray's record is that of its first segment that did not stop (a hit, or the ray left
-// the cube): the segments before it covered everything up to its arming event without a hit.
-// Bit-identical to the continuous loop in both stack modes (tests/test_gpu_seg.py against the
-// oracle, with real and with random starts).
-template <int MODE, bool FETCH_ALL>
-__device__ __forceinline__ void trace_seg(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk, float t_start,
-                                          float t_stop, bool armed0, uint32_t &n_lane, uint32_t &armed_at,
-                                          bool &stopped_lane) {
-    constexpr int STRIDE = TILE;
-    const int slots = p.slots;
-    for (int s = 0; s < slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
-    const int scale_lo = S_MAX - slots;
-    lmask act = LM_OF(true);
-    lmask armed = LM_OF(armed0), stopped = 0, cached = 0;
-    const int oct = r.octant_mask | 16;
-    int sh = r.idx ^ oct;
-    const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
-    constexpr uint32_t SLOT = (uint32_t)(STRIDE * sizeof(uint2));
-    constexpr int SLOT_SH = 23 - 9;
-    const uint32_t push_base = stk_base - (uint32_t)(104 + scale_lo) * SLOT;
-    const uint2 *stk_pop = stk - (127 + scale_lo) * STRIDE;
-    const uint32_t e_max = (uint32_t)(127 + scale_lo + slots - 1);
-    int it = 0;
-    n_lane = 0;
-    armed_at = 0;
-    asm volatile("" : "+v"(r.parent), "+v"(r.cd16), "+v"(r.first));
-    lmask go;
-    do {
-        asm volatile("s_add_u32 %0, %0, 1" : "+s"(it) : : "scc");
-        const lmask need = FETCH_ALL ? ~(lmask)0 : act & ~cached;
-        if (FETCH_ALL || LM_ON(need)) {
-            const uint2 nd = *(const uint2 *)((const char *)p.nodes + (uint32_t)(r.parent << 3));
-            r.cd16 = nd.x;
-            r.first = nd.y;
-        }
-        cached |= need;
-        const float tx = r.px * r.cx - r.bx;             // N:67-70
-        const float ty = r.py * r.cy - r.by;
-        const float tz = r.pz * r.cz - r.bz;
-        const float tc_max = fminf(fminf(tx, ty), tz);
-        const float tv_max = vmin(r.t_max, tc_max);
-        const float half = r.sexp * 0.5f;
-        const lmask cx = LM_OF(center(half, r.cx, tx) > r.t_min);
-        const lmask cy = LM_OF(center(half, r.cy, ty) > r.t_min);
-        const lmask cz = LM_OF(center(half, r.cz, tz) > r.t_min);
-        const lmask lx = LM_OF(tx <= tc_max), ly = LM_OF(ty <= tc_max), lz = LM_OF(tz <= tc_max);
-        const lmask in_span = LM_OF(r.t_min <= tv_max), below_h = LM_OF(tc_max < r.h);
-        const lmask before = LM_OF(tc_max < t_start);    // SKIP test (NaN start: never)
-        const lmask arm_now = LM_OF(tc_max >= t_start);  // ARM / STOP tests on the ADVANCE's new t_min
-        const lmask stop_now = LM_OF(tc_max >= t_stop);
-        const uint32_t cm = r.cd16 << sh;
-        const lmask descend = act & LM_OF((int32_t)cm < 0) & in_span;
-        const lmask leaf = LM_OF((cm & 0x00800000u) == 0u);
-        const lmask inner = descend & ~leaf;
-        const lmask skip = inner & before;
-        const lmask hit = descend & leaf & armed;        // N:93-94, armed lanes only
-        const lmask push = inner & ~skip;
-        const lmask store = inner & below_h;             // PUSH's stack write, also for a SKIP
-        const lmask adv = act & ~(hit | push);           // incl. SKIP lanes and unarmed leaves
-        if (LM_ON(store)) {                              // N:97-98
-            const uint32_t a = push_base + (__float_as_uint(r.sexp) >> SLOT_SH);
-            const uint32_t tmw = MODE == 0 ? (uint32_t)cvt_i32((float)(int32_t)__float_as_uint(r.t_max))
-                                           : __float_as_uint(r.t_max);
-            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" : : "v"(a), "v"(r.parent), "v"(tmw) : "memory");
-        }
-        const lmask sx = adv & lx;                       // N:122-125
-        const lmask sy = adv & ly;
-        const lmask sz = adv & lz;
-        const float se = r.sexp;
-        const float delta = LM_ON(push) ? half : -se;
-        const float ox = r.px, oy = r.py, oz = r.pz;
-        const lmask mvx = (push & cx) | sx, mvy = (push & cy) | sy, mvz = (push & cz) | sz;
-        const float qx = r.px + (LM_ON(mvx) ? delta : 0.0f);
-        const float qy = r.py + (LM_ON(mvy) ? delta : 0.0f);
-        const float qz = r.pz + (LM_ON(mvz) ? delta : 0.0f);
-        const int mv = lanes_to_idx(mvx, mvy, mvz);
-        const lmask pop = adv & LM_OF((mv & ~(sh ^ oct)) != 0);
-        const uint32_t child = r.first + (uint32_t)__builtin_popcount(cm & 0x007F0000u);
-        sh = (LM_ON(push) ? oct : sh) ^ mv;
-        if (LM_ON(push)) {
-            r.parent = child;
-            r.h = tc_max;
-            r.t_max = tv_max;
-            r.sexp = half;
-        }
-        if (skip != 0) {   // back at this node's level as after a POP (N:141-153)
-            if (LM_ON(skip)) {
-                if (MODE == 0) r.t_max = __int_as_float(cvt_i32((float)(int32_t)__float_as_uint(r.t_max)));
-                r.h = 0.0f;
-            }
-        }
-        r.t_min = LM_ON(adv) ? tc_max : r.t_min;
-        const lmask armed_new = adv & arm_now & ~armed;
-        if (armed_new != 0) {
-            if (LM_ON(armed_new)) armed_at = (uint32_t)it;
-            armed |= armed_new;
-        }
-        const lmask stop = adv & stop_now;
-        cached &= ~(push | pop);
-        r.px = qx; r.py = qy; r.pz = qz;
-        lmask out = 0;
-        if (pop != 0) {                                  // N:134-154
-            const uint32_t diff = (__float_as_uint(ox) ^ __float_as_uint(qx)) |
-                                  (__float_as_uint(oy) ^ __float_as_uint(qy)) |
-                                  (__float_as_uint(oz) ^ __float_as_uint(qz));
-            const uint32_t fd = __float_as_uint((float)diff);
-            const uint32_t ef = __builtin_amdgcn_ubfe(fd, 23, 8);
-            const int scale = (int)ef - 127;
-            const uint2 e = stk_pop[min(ef, e_max) * STRIDE];
-            const uint32_t keep = 0xFFFFFFFFu << scale;
-            const uint32_t bx_ = __builtin_amdgcn_ubfe(__float_as_uint(qx), scale, 1);
-            const uint32_t by_ = __builtin_amdgcn_ubfe(__float_as_uint(qy), scale, 1);
-            const uint32_t bz_ = __builtin_amdgcn_ubfe(__float_as_uint(qz), scale, 1);
-            const bool pl = LM_ON(pop);
-            r.sexp = pl ? __uint_as_float((ef << 23) - (23u << 23)) : r.sexp;
-            r.parent = pl ? e.x : r.parent;
-            r.t_max = pl ? __uint_as_float(e.y) : r.t_max;
-            const uint32_t k = pl ? keep : 0xFFFFFFFFu;
-            r.px = __uint_as_float(__float_as_uint(r.px) & k);
-            r.py = __uint_as_float(__float_as_uint(r.py) & k);
-            r.pz = __uint_as_float(__float_as_uint(r.pz) & k);
-            r.h = pl ? 0.0f : r.h;
-            sh = pl ? (int)(bx_ | (by_ << 1) | (bz_ << 2)) ^ oct : sh;
-            out = pop & LM_OF(scale >= S_MAX);
-        }
-        const lmask fin = act & (hit | out | stop);
-        if (fin != 0) {
-            if (LM_ON(fin)) n_lane = (uint32_t)it;
-            stopped |= stop;                             // STOP before the cube exit of the same trip
-            act &= ~fin;
-        }
-        asm volatile("s_cmp_lt_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(go) : "s"(it), "n"(MAX_ITERS), "s"(act) : "scc");
-    } while (go != 0);
-    if (LM_ON(act)) {   // still tracing after MAX_ITERS trips (unreachable for a tree of depth <= 13)
-        r.flags |= 2u;
-        n_lane = (uint32_t)it;
-    }
-    stopped_lane = LM_ON(stopped);
-    r.idx = sh ^ oct;
-    r.trips = it;
 }
 
 // a ray's K segments are K consecutive lanes (K = 4 or 8, wave-uniform)
@@ -1087,7 +1125,12 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
         camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
         setup_ray(org, dir, r);
     }
-    const float t_entry = r.t_min, t_exit = r.t_max;
+    FRay f;
+    to_fray(r, f);
+    // segment 0 starts at the beam start (-inf without one); the even split and the rebalance
+    // then spread the segments over the part of the ray after it
+    const float bs = beam_start(p, f, x, gy);
+    const float t_entry = fmaxf(r.t_min, bs), t_exit = r.t_max;
     // the pixel's starts at fractions e / 8 of its trace (8 floats: e = 1..7 + spare); segment k of
     // K runs from fraction k / K to (k + 1) / K
     const size_t hi = (size_t)lr * (size_t)p.width + (size_t)x;
@@ -1096,11 +1139,10 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
     const bool have = hint8[0] == hint8[0];                        // NaN: none yet
     const float t_start = seg_start(p, hint8, have, hi, e0, t_entry, t_exit);
     const float t_stop = seg_start(p, hint8, have, hi, e1, t_entry, t_exit);
-    FRay f;
-    to_fray(r, f);
     uint32_t n_lane, armed_at;
     bool stopped;
-    trace_seg<MODE, FA>(p, f, stk, t_start, t_stop, k == 0, n_lane, armed_at, stopped);
+    trace_seg<MODE, FA>(p, f, stk, k == 0 ? bs : t_start, t_stop, k == 0 && r.t_min >= bs, n_lane, armed_at,
+                        stopped);
     from_fray(f, r);
     // the record holder: the first segment that did not stop (the last one never stops)
     const int fsel = group_min(stopped ? K : k, K);
@@ -1172,6 +1214,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
         FRay f;
         to_fray(r, f);
         if (LAT) trace_lat<MODE>(p, f, stk);
+        else if (p.tile_start) trace_beam<MODE, FA>(p, f, stk, beam_start(p, f, x, gy));
         else trace_lean<MODE, false, false, FA>(p, f, stk);
         from_fray(f, r);
         Record o;
@@ -1243,6 +1286,7 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
     FRay f;
     to_fray(r, f);
     if (p.guard) trace_lean<MODE, true>(p, f, stk);
+    else if (p.tile_start) trace_beam<MODE, FA>(p, f, stk, beam_start(p, f, x, gy));
     else trace_lean<MODE, false, false, FA>(p, f, stk);
     from_fray(f, r);
     Record o;
@@ -2088,6 +2132,104 @@ hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------- beam splat
+// One thread per box of the pool's splat list (svo_rt.hip build_beam_boxes): the box's Euclidean
+// distance from the camera bounds from below the t at which any ray can enter it, so that
+// distance is min-ed into every 8x8 tile whose rays can reach the box -- those whose pixel area
+// (any offset in [0, 1]) meets the box's screen projection.  The projection is the bounding box of
+// the projected corners, after clipping the box to the part in front of the camera (q_z > eps:
+// the edges crossing that plane add their crossing points).  A box a tile's rays miss only costs
+// that tile a lower start; a box they can reach is never left out, so every tile's value is <=
+// the hit t of each of its rays (exact).
+__device__ __forceinline__ void beam_min(float *a, float v) {
+    if (__float_as_uint(v) < __float_as_uint(*a)) atomicMin(reinterpret_cast<unsigned int *>(a), __float_as_uint(v));
+}
+
+__global__ __launch_bounds__(256) void beam_splat_kernel(BeamParams b) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= b.n_boxes) return;
+    const uint2 e = b.boxes[i];
+    const int dep = (int)(e.y >> 16);
+    const float size = __uint_as_float((uint32_t)(127 - dep) << 23);   // 2^-depth
+    const float lo[3] = {1.0f + (float)(e.x & 0xFFFFu) * size, 1.0f + (float)(e.x >> 16) * size,
+                         1.0f + (float)(e.y & 0xFFFFu) * size};   // exact (17 significant bits)
+    float rel[3], d2 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        rel[k] = lo[k] - b.org[k];
+        const float m = fmaxf(fmaxf(rel[k], -(rel[k] + size)), 0.0f);   // gap to the box along axis k
+        d2 += m * m;
+    }
+    const float dist = sqrtf(d2);
+    // outside a side plane of the view frustum (the planes sit a pixel outside the frame): no ray
+    const float span = fabsf(rel[0]) + fabsf(rel[1]) + fabsf(rel[2]) + 3.0f * size;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float *n = b.plane[j];
+        const float top = n[0] * rel[0] + n[1] * rel[1] + n[2] * rel[2] +
+                          size * (fmaxf(n[0], 0.0f) + fmaxf(n[1], 0.0f) + fmaxf(n[2], 0.0f));
+        if (top < -1e-5f * span) return;
+    }
+    // corners in (fx, fy, 1)-space: q = Minv (P - o), linear in the corner
+    float q0[3], g[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        q0[r] = b.minv[3 * r] * rel[0] + b.minv[3 * r + 1] * rel[1] + b.minv[3 * r + 2] * rel[2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) g[k][r] = b.minv[3 * r + k] * size;
+    }
+    float qx[8], qy[8], qz[8], zmax = -__builtin_inff();
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        qx[c] = q0[0] + ((c & 1) ? g[0][0] : 0.0f) + ((c & 2) ? g[1][0] : 0.0f) + ((c & 4) ? g[2][0] : 0.0f);
+        qy[c] = q0[1] + ((c & 1) ? g[0][1] : 0.0f) + ((c & 2) ? g[1][1] : 0.0f) + ((c & 4) ? g[2][1] : 0.0f);
+        qz[c] = q0[2] + ((c & 1) ? g[0][2] : 0.0f) + ((c & 2) ? g[1][2] : 0.0f) + ((c & 4) ? g[2][2] : 0.0f);
+        zmax = fmaxf(zmax, qz[c]);
+    }
+    if (!(zmax > 0.0f)) return;   // wholly behind the camera
+    float* const ts = b.tile_start;
+    if (dist <= 1e-3f * size) {   // the camera at the box: every ray
+        beam_min(ts + b.global_off, dist);
+        return;
+    }
+    const float eps = zmax * 1e-5f;
+    float x0 = __builtin_inff(), x1 = -__builtin_inff(), y0 = __builtin_inff(), y1 = -__builtin_inff();
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        if (qz[c] > eps) {
+            const float fx = qx[c] / qz[c], fy = qy[c] / qz[c];
+            x0 = fminf(x0, fx); x1 = fmaxf(x1, fx); y0 = fminf(y0, fy); y1 = fmaxf(y1, fy);
+        }
+#pragma unroll
+        for (int bit = 1; bit < 8; bit <<= 1) {   // the 12 edges (c, c | bit), c without bit
+            if (c & bit) continue;
+            const int d = c | bit;
+            if ((qz[c] > eps) == (qz[d] > eps)) continue;
+            const float s = (eps - qz[c]) / (qz[d] - qz[c]);
+            const float fx = (qx[c] + s * (qx[d] - qx[c])) / eps, fy = (qy[c] + s * (qy[d] - qy[c])) / eps;
+            x0 = fminf(x0, fx); x1 = fmaxf(x1, fx); y0 = fminf(y0, fy); y1 = fmaxf(y1, fy);
+        }
+    }
+    const float mg = 0.05f;   // pixels: rounding of the projection and of the rays' own u, v
+    x0 -= mg; y0 -= mg; x1 += mg; y1 += mg;
+    if (!(x1 >= 0.0f && y1 >= 0.0f && x0 <= (float)b.width && y0 <= (float)b.height)) return;
+    const int tx0 = (int)(fmaxf(x0, 0.0f) * 0.125f), ty0 = (int)(fmaxf(y0, 0.0f) * 0.125f);
+    const int tx1 = min((int)(fminf(x1, (float)b.width) * 0.125f), b.tiles_x - 1);
+    const int ty1 = min((int)(fminf(y1, (float)b.height) * 0.125f), b.tiles_y - 1);
+    if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) <= 32) {
+        for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) beam_min(ts + ty * b.tiles_x + tx, dist);
+        return;
+    }
+    const int sx0 = tx0 >> 3, sx1 = tx1 >> 3, sy0 = ty0 >> 3, sy1 = ty1 >> 3;
+    if ((sx1 - sx0 + 1) * (sy1 - sy0 + 1) <= 32) {
+        for (int sy = sy0; sy <= sy1; ++sy)
+            for (int sx = sx0; sx <= sx1; ++sx) beam_min(ts + b.super_off + sy * b.super_x + sx, dist);
+        return;
+    }
+    beam_min(ts + b.global_off, dist);
+}
+
 template <int MODE>
 static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
     const int bx = (p.width + 7) / 8, by = (p.local_rows + 7) / 8;
@@ -2096,6 +2238,12 @@ static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
         hipLaunchKernelGGL((shadow_tile_kernel<MODE, true>), dim3((unsigned)(bx * by)), dim3(TILE), lds, stream, p, bx);
     else
         hipLaunchKernelGGL((shadow_tile_kernel<MODE>), dim3((unsigned)(bx * by)), dim3(TILE), lds, stream, p, bx);
+    return hipGetLastError();
+}
+
+hipError_t launch_beam_splat(const BeamParams &b, hipStream_t stream) {
+    if (b.n_boxes == 0) return hipSuccess;
+    hipLaunchKernelGGL(beam_splat_kernel, dim3((b.n_boxes + 255u) / 256u), dim3(256), 0, stream, b);
     return hipGetLastError();
 }
 

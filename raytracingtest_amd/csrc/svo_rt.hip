@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdio>
@@ -62,6 +64,9 @@ struct Upload {
     int depth;
     bool external;   // has child links outside its own range (sub-SVO linking)
     bool tree;       // every node reached once from the upload's first node (no sharing, no cycles)
+    // beam starts: the splat list of a self-contained tree at offset 0 (null: none)
+    std::shared_ptr<const std::vector<uint2>> boxes;
+    uint64_t boxes_id;   // unique per list (the device copy's key)
 };
 
 enum { STAGE_KERNEL = 0, STAGE_ASSEMBLE = 1, N_STAGES = 2 };
@@ -114,6 +119,8 @@ struct Sched {
     size_t order_cap = 0;              // order_buf entries allocated
     float4 *seg_hint = nullptr;        // segmented tiles: per pixel the segment starts (svo_traverse.h)
     size_t hint_cap = 0;
+    float *tile_start = nullptr;       // beam starts of this stream's launches (svo_traverse.h)
+    size_t ts_cap = 0;
     Geo order_key;                   // the newest build's key (width -1: none)
     Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
@@ -287,6 +294,14 @@ struct svo_ctx {
     int seg_all = 0;                 // env SVO_SEG_ALL=4|8 (tests; 1 = 4): every tile segmented with that K
     uint32_t seg_scramble = 0;       // env SVO_SEG_SCRAMBLE=<seed> (tests): arbitrary segment starts
     uint32_t seg_launches = 0;
+    int beam = 1;                    // env SVO_BEAM=0: no beam starts
+    int beam_back = 2;               // env SVO_BEAM_BACK: splat the boxes this many levels above the leaves
+    uint2 *d_boxes = nullptr;        // the device copy of the root upload's splat list ...
+    size_t boxes_cap = 0;
+    uint32_t n_boxes = 0;
+    uint64_t boxes_id = 0;           // ... made from the list with this id (0: none)
+    float *count_ts = nullptr;       // beam starts of an instrumented launch (SVO_OPT_COUNT_BEAM)
+    size_t count_ts_cap = 0;
     double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold
     int move_every = 4;              // env SVO_MOVE_EVERY: while the camera moves every launch, rebuild the
                                      // order only every k-th launch (see launch; 1 = at every new view).
@@ -474,6 +489,41 @@ void recompute_depth(svo_ctx *ctx) {
     ctx->depth = ctx->depth_exact ? root_depth : 22;
 }
 
+// The splat list of a tree: every box a primary ray can first hit a voxel in, at
+// a fixed depth ds = depth - back -- the non-leaf nodes at ds and the leaves above it -- as
+// (x | y << 16, z | depth << 16), box [1 + i 2^-depth, 1 + (i + 1) 2^-depth]^3 in SVO space.
+// Child c of a node (bit c of its masks, NVIDIASVO.compute:83-94 with slot 7 - c) takes the upper
+// half on axis k iff bit k of c is set; its node is first + (non-leaf children before it).
+std::shared_ptr<const std::vector<uint2>> build_beam_boxes(const uint32_t *lo, const uint32_t *first, size_t n,
+                                                           int depth, int back) {
+    const int ds = std::min(depth - back, 16);   // 16-bit coordinates
+    if (ds < 1 || n == 0) return nullptr;
+    auto out = std::make_shared<std::vector<uint2>>();
+    struct Item { uint32_t node, x, y, z; };
+    std::vector<Item> cur{{0u, 0u, 0u, 0u}}, nxt;
+    for (int d = 0; d < ds && !cur.empty(); ++d) {
+        nxt.clear();
+        for (const Item &it : cur) {
+            const uint32_t m = lo[it.node] & 0xFFu, v = (lo[it.node] >> 8) & 0xFFu;
+            uint32_t rank = 0;
+            for (uint32_t c = 0; c < 8; ++c) {
+                const bool inner = (m >> c) & 1u;
+                const uint32_t child = inner ? first[it.node] + rank++ : 0u;
+                if (!((v >> c) & 1u)) continue;
+                const uint32_t x = 2 * it.x + (c & 1u), y = 2 * it.y + ((c >> 1) & 1u), z = 2 * it.z + ((c >> 2) & 1u);
+                if (inner && d + 1 < ds) {
+                    if (child < n) nxt.push_back({child, x, y, z});
+                } else {
+                    out->push_back(make_uint2(x | (y << 16), z | ((uint32_t)(d + 1) << 16)));
+                }
+            }
+        }
+        cur.swap(nxt);
+    }
+    if (out->size() >= 0xFFFFFFFFull) return nullptr;
+    return out;
+}
+
 int validate_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, size_t n, size_t base, Upload *out) {
     std::string err;
     int depth = 0;
@@ -483,7 +533,12 @@ int validate_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, siz
     // capacity is legal; the pool is zero-filled at svo_create, so a link into a
     // region not uploaded yet reads empty descriptors
     if (walk_depth(lo, first, n, base, ctx->capacity, &depth, &ext, &tree, &err) != 0) return fail(SVO_ERR_FORMAT, err);
-    *out = Upload{base, n, depth, ext, tree};
+    *out = Upload{base, n, depth, ext, tree, nullptr, 0};
+    if (base == 0 && tree && !ext && ctx->beam) {
+        static std::atomic<uint64_t> next_id{0};
+        out->boxes = build_beam_boxes(lo, first, n, depth, ctx->beam_back);
+        out->boxes_id = ++next_id;
+    }
     return SVO_OK;
 }
 
@@ -670,6 +725,75 @@ struct SampleArgs {
     uint8_t *rgb8;
     int layout;
 };
+
+// The splat's view of a camera (svo_traverse.h BeamParams): origin, the inverse of the pixel ->
+// direction map and the frustum's side planes, in double from the render's own formulas
+// (svo_kernel.hip camera_ray).  False for a camera the splat cannot bound (non-finite, singular,
+// or a field of view so wide that the projection's clipping margin no longer holds).
+bool beam_camera(const svo::Camera &c, int width, int height, svo::BeamParams *bp) {
+    double A[3], B[3], C[3];
+    for (int r = 0; r < 3; ++r) {   // dir = C3 (IP (u, v, 0, 1)).xyz, u = 2 fx / W - 1, v = 2 fy / H - 1
+        A[r] = B[r] = C[r] = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            A[r] += (double)c.c2w[k * 4 + r] * c.inv_proj[0 * 4 + k];
+            B[r] += (double)c.c2w[k * 4 + r] * c.inv_proj[1 * 4 + k];
+            C[r] += (double)c.c2w[k * 4 + r] * c.inv_proj[3 * 4 + k];
+        }
+    }
+    double M[3][3];
+    for (int r = 0; r < 3; ++r) {
+        M[r][0] = 2.0 * A[r] / width;
+        M[r][1] = 2.0 * B[r] / height;
+        M[r][2] = C[r] - A[r] - B[r];
+    }
+    const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
+                       M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
+                       M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+    if (!std::isfinite(det) || det == 0.0) return false;
+    double inv[3][3];
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) {
+            const int r1 = (k + 1) % 3, r2 = (k + 2) % 3, c1 = (r + 1) % 3, c2 = (r + 2) % 3;
+            inv[r][k] = (M[r1][c1] * M[r2][c2] - M[r1][c2] * M[r2][c1]) / det;   // adjugate / det
+        }
+    auto dir = [&](double fx, double fy, double d[3]) {
+        for (int r = 0; r < 3; ++r) d[r] = M[r][0] * fx + M[r][1] * fy + M[r][2];
+    };
+    auto len = [](const double d[3]) { return std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]); };
+    double D[4][3], mid[3];
+    dir(-1.0, -1.0, D[0]);
+    dir(width + 1.0, -1.0, D[1]);
+    dir(width + 1.0, height + 1.0, D[2]);
+    dir(-1.0, height + 1.0, D[3]);
+    dir(0.5 * width, 0.5 * height, mid);
+    double lmin = len(mid), lmax = len(mid);
+    for (int j = 0; j < 4; ++j) {
+        lmin = std::min(lmin, len(D[j]));
+        lmax = std::max(lmax, len(D[j]));
+    }
+    if (!(lmin > 0.0) || lmax > 30.0 * lmin) return false;
+    for (int j = 0; j < 4; ++j) {
+        const double *a = D[j], *b = D[(j + 1) % 4];
+        double n[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+        const double sgn = n[0] * mid[0] + n[1] * mid[1] + n[2] * mid[2] < 0.0 ? -1.0 : 1.0;
+        const double l = len(n);
+        if (!(l > 0.0) || !std::isfinite(l)) return false;
+        for (int k = 0; k < 3; ++k) bp->plane[j][k] = (float)(sgn * n[k] / l);
+    }
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) {
+            bp->minv[3 * r + k] = (float)inv[r][k];
+            if (!std::isfinite(bp->minv[3 * r + k])) return false;
+        }
+    for (int k = 0; k < 3; ++k) {   // mul4(c2w, (0, 0, 0, 1)) then to_svo, in f32 (both steps exact or one rounding)
+        const float w = c.c2w[12 + k];
+        if (!std::isfinite(w)) return false;
+        for (int j = 0; j < 3; ++j)
+            if (!std::isfinite(c.c2w[4 * j + k])) return false;
+        bp->org[k] = w * (1.0f / 32.0f) + 1.5f;
+    }
+    return true;
+}
 
 int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *band, svo::Outputs out,
            hipStream_t stream, const SampleArgs *sa = nullptr) {
@@ -960,6 +1084,77 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         }
         HIP_TRY(hipMemsetAsync(ctx->d_wave_log, 0, n_wave * 4 * svo::WAVE_LOG_WORDS, s));
         p.wave_log = ctx->d_wave_log;
+    }
+    // Beam starts: a tree pool's primary rays start at a per-tile lower bound of
+    // their hit t, splatted from the pool's boxes right before the render, on its stream, every
+    // launch (a function of the camera and the pool only; pixel offsets in [0, 1] are covered).
+    const bool count_beam = p.out.fetches && (ctx->options & SVO_OPT_COUNT_BEAM);
+    if (ctx->beam && (q || count_beam) && !p.guard && (!p.out.fetches || count_beam) && ctx->depth_exact) {
+        const Upload *root = nullptr;
+        for (const Upload &u : ctx->uploads)
+            if (u.offset == 0) root = &u;
+        auto in01 = [](float v) { return v >= 0.0f && v <= 1.0f; };
+        bool offs = in01(p.cam.px_off[0]) && in01(p.cam.px_off[1]);
+        if (p.samples) {
+            offs = true;
+            for (int k = 0; k < p.samples; ++k) offs = offs && in01(p.sample_off[k][0]) && in01(p.sample_off[k][1]);
+        }
+        svo::BeamParams bp;
+        std::memset(&bp, 0, sizeof bp);
+        if (root && root->boxes && !root->boxes->empty() && offs && beam_camera(p.cam, width, height, &bp)) {
+            if (ctx->boxes_id != root->boxes_id) {   // the device copy of this pool's splat list
+                const size_t nb = root->boxes->size();
+                HIP_TRY(hipDeviceSynchronize());   // launches on any stream may still read the old one
+                if (ctx->boxes_cap < nb) {
+                    if (ctx->d_boxes) hipFree(ctx->d_boxes);
+    if (ctx->count_ts) hipFree(ctx->count_ts);
+                    ctx->d_boxes = nullptr;
+                    ctx->boxes_cap = 0;
+                    HIP_TRY(hipMalloc(&ctx->d_boxes, nb * sizeof(uint2)));
+                    ctx->boxes_cap = nb;
+                }
+                HIP_TRY(hipMemcpy(ctx->d_boxes, root->boxes->data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
+                ctx->n_boxes = (uint32_t)nb;
+                ctx->boxes_id = root->boxes_id;
+            }
+            const int tx = (width + 7) / 8, ty = (height + 7) / 8, sx = (width + 63) / 64, sy = (height + 63) / 64;
+            const size_t need = (size_t)tx * ty + (size_t)sx * sy + 1;
+            // the stream's own buffer; an instrumented launch (no scheduling state) the shared scratch
+            float *&buf = q ? q->tile_start : ctx->count_ts;
+            size_t &cap = q ? q->ts_cap : ctx->count_ts_cap;
+            if (!q) {
+                rc = order_scratch(ctx, s);
+                if (rc) return rc;
+            }
+            if (cap < need) {
+                HIP_TRY(hipDeviceSynchronize());   // a pending launch may still read the old buffer
+                if (buf) hipFree(buf);
+                buf = nullptr;
+                cap = 0;
+                HIP_TRY(hipMalloc(&buf, need * sizeof(float)));
+                cap = need;
+            }
+            HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(buf), 0x7F800000, need, s));   // +inf
+            bp.boxes = ctx->d_boxes;
+            bp.n_boxes = ctx->n_boxes;
+            bp.tile_start = buf;
+            bp.tiles_x = tx;
+            bp.tiles_y = ty;
+            bp.super_x = sx;
+            bp.super_y = sy;
+            bp.super_off = tx * ty;
+            bp.global_off = tx * ty + sx * sy;
+            bp.width = width;
+            bp.height = height;
+            hipError_t eb = svo::launch_beam_splat(bp, s);
+            if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
+            p.tile_start = buf;
+            p.ts_tiles_x = tx;
+            p.ts_super_x = sx;
+            p.ts_super_off = bp.super_off;
+            p.ts_global_off = bp.global_off;
+            p.lat = 0;   // the beam walk is a form of the lean loop
+        }
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (!p.out.fetches) {
@@ -1301,6 +1496,7 @@ int destroy_single(svo_ctx *ctx) {
     for (Sched &q : ctx->sched) {
         free_sched(q);
         if (q.seg_hint) hipFree(q.seg_hint);
+        if (q.tile_start) hipFree(q.tile_start);
         if (q.done) hipEventDestroy(q.done);
         for (int r = 0; r < Sched::STATS_RING; ++r)
             if (q.stats_ev[r]) hipEventDestroy(q.stats_ev[r]);
@@ -1318,6 +1514,8 @@ int destroy_single(svo_ctx *ctx) {
     for (auto &ev : ctx->timing_free) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     if (ctx->switch_event) hipEventDestroy(ctx->switch_event);
     if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
+    if (ctx->d_boxes) hipFree(ctx->d_boxes);
+    if (ctx->count_ts) hipFree(ctx->count_ts);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return SVO_OK;
@@ -1383,6 +1581,8 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_SEG_ALL")) ctx->seg_all = std::atoi(k) == 8 ? 8 : std::atoi(k) != 0 ? 4 : 0;
     if (const char *k = std::getenv("SVO_SEG_SCRAMBLE")) ctx->seg_scramble = (uint32_t)std::strtoul(k, nullptr, 10);
     if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
+    if (const char *k = std::getenv("SVO_BEAM")) ctx->beam = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_BEAM_BACK")) ctx->beam_back = std::max(0, std::atoi(k));
     if (e != hipSuccess) {
         destroy_single(ctx);
         return fail(SVO_ERR_HIP, std::string("svo_create: ") + hipGetErrorString(e));
@@ -1903,7 +2103,7 @@ int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode, const
 
 int svo_set_options(svo_ctx *ctx, uint32_t options) {
     if (!ctx) return fail(SVO_ERR_ARG, "null context");
-    if (options & ~(uint32_t)(SVO_OPT_SHADOW_RAYS | SVO_OPT_KERNEL_TIMING)) return fail(SVO_ERR_ARG, "unknown option bits");
+    if (options & ~(uint32_t)(SVO_OPT_SHADOW_RAYS | SVO_OPT_KERNEL_TIMING | SVO_OPT_COUNT_BEAM)) return fail(SVO_ERR_ARG, "unknown option bits");
     for (svo_ctx *m : ctx->members) m->options = options;
     ctx->options = options;
     return SVO_OK;

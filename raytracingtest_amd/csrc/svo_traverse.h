@@ -121,6 +121,14 @@ struct LaunchParams {
     uint16_t *part_cost;
     uint32_t seg_scramble;     // tests (env SVO_SEG_SCRAMBLE): != 0 replaces every start by a hash of
                                // (pixel, this value) -- unordered, NaN, +-inf, outside the cube
+    // Beam starts (null: none).  tile_start[ty * ts_tiles_x + tx] for the 8x8 tile
+    // (tx, ty) of the FULL frame (global rows), tile_start[ts_super_off + sy * ts_super_x + sx] for
+    // its 64x64 super tile and tile_start[ts_global_off]: the minimum is a lower bound of the
+    // distance (SVO-space t) at which any primary ray through the tile, at any pixel offset in
+    // [0, 1], can first hit a voxel (beam_splat_kernel).  A primary ray starts there, minus a
+    // rounding margin, in trace_seg's exact skip form.
+    const float *tile_start;
+    int ts_tiles_x, ts_super_x, ts_super_off, ts_global_off;
 };
 
 constexpr int SEG_KMAX = 8;                 // segments per ray: 4 (a lane quad) or 8, by cost class
@@ -184,6 +192,24 @@ inline int order_strips_grid(int n_tiles, int seg_cap, int kmax) { return n_tile
 inline size_t order_strips_entries(int n_tiles, int seg_cap, int kmax = SEG_KMAX) {
     return (size_t)order_strips_grid(n_tiles, seg_cap, kmax) + 36;
 }
+
+// Beam starts of one launch: every box of the pool's splat list (the nodes at
+// the splat depth and the leaves above it, svo_rt.hip build_beam_boxes) is projected onto the
+// screen, and its distance from the camera min-ed into every 8x8 tile its projection touches
+// (a 64x64 super tile or the one global word when it touches more than 16).  tile_start must be
+// +inf-filled before (tiles_x * tiles_y + super_x * super_y + 1 floats).
+struct BeamParams {
+    const uint2 *boxes;    // (x | y << 16, z | depth << 16): box [1 + i 2^-depth, 1 + (i + 1) 2^-depth]^3
+    uint32_t n_boxes;
+    float *tile_start;
+    int tiles_x, tiles_y, super_x, super_y, super_off, global_off;
+    int width, height;
+    float org[3];          // camera origin in SVO space, bit-identical to the render's
+    float minv[9];         // row-major inverse of M: unnormalised ray direction = M (fx, fy, 1), fx, fy
+                           // continuous pixel coordinates (pixel x, offset o: fx = x + o)
+    float plane[4][3];     // the view frustum's side planes through the camera, normals pointing in
+};
+hipError_t launch_beam_splat(const BeamParams &b, hipStream_t stream);
 
 // Progressive accumulation (AddShader blend) of an RGBA32F sample frame.
 hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32_t sample, int num_cus,

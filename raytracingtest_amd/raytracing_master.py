@@ -120,6 +120,11 @@ class RaytracingMaster:
         reference's commented-out test, RaytraceCompute.compute:105-112)."""
         self._set_option(_lib.SVO_OPT_SHADOW_RAYS, enable)
 
+    def set_count_beam(self, enable=True):
+        """SVO_OPT_COUNT_BEAM: count_fetches_device counts the fetches of the walk the render runs
+        (from the beam start) instead of the reference's walk from the cube entry."""
+        self._set_option(_lib.SVO_OPT_COUNT_BEAM, enable)
+
     def set_kernel_timing(self, enable=True):
         """Bracket the primary-ray kernel of every launch with HIP events
         (measurement only; read with kernel_time())."""

@@ -1,0 +1,184 @@
+"""GPU parity of the beam starts (svo_kernel.hip beam_splat_kernel + trace_beam).
+
+Every primary ray of a tree pool starts at its tile's lower bound of the hit t (the distance to
+the nearest box of the pool's splat list whose projection touches the tile) instead of the cube
+entry, in trace_seg's exact skip form.  The records must stay bit-identical to the oracle's
+IntersectSVO (NVIDIASVO.compute:57-198): checked for the survey poses, cameras inside and far
+outside the cube, axis-aligned and very wide views, jittered pixel offsets at the ends of [0, 1],
+the samples-in-flight launch, a band of a split frame, every splat depth from the leaves up, and
+both stack modes.
+"""
+import numpy as np
+import pytest
+
+from raytracingtest_amd import RaytracingMaster
+from raytracingtest_amd.builder import build_menger
+from raytracingtest_amd.camera import CAMERAS, Camera, main_light, overview_camera
+
+from test_gpu_frame import _bufs, _check, _oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    t = pytest.importorskip("torch")
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+@pytest.fixture(scope="module")
+def c3_svo():
+    from bench import CONFIGS
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    cfg = CONFIGS["C3"]
+    return build_sampler_svo(cfg["sampler"], cfg["max_level"], device=0)
+
+
+def _cams():
+    return {
+        "flyover": CAMERAS["flyover"](),
+        "main": CAMERAS["main"](),
+        "overview": CAMERAS["overview"](),
+        "terrain": CAMERAS["terrain"](),
+        # inside the cube below the terrain surface (the camera within a splat box: the global word)
+        "buried": overview_camera((3.0, -20.0, 2.0), (0.0, -25.0, 20.0)),
+        # looking straight along +z and straight down: rays parallel to an axis plane (|coef| = inf)
+        "axis_z": overview_camera((0.25, 4.0, -31.0), (0.25, 4.0, 10.0)),
+        "down": overview_camera((0.0, 40.0, 0.0), (0.0, -10.0, 0.0)),
+        # far outside the cube, and a 160-degree view inside it
+        "far": overview_camera((300.0, 200.0, -500.0), (0.0, 0.0, 0.0)),
+        "wide": Camera(position=(1.0, 1.0, 1.0), fov=160.0),
+    }
+
+
+def _render(torch, m, w, h, mode, keys=("hits", "rgba", "position", "voxel")):
+    b = _bufs(torch, w * h)
+    m.render_frame(w, h, stack_mode=mode, **{k: v.data_ptr() for k, v in b.items() if k in keys})
+    m.synchronize()
+    return b
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_beam_starts_match_oracle_c3_poses(torch, oracle_mod, c3_svo, mode):
+    """The C3 terrain pool (depth 10), nine poses, two frames each: every record equals the oracle's."""
+    w, h = 640, 360
+    m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+    try:
+        m.SetSVOBuffer(c3_svo)
+        for name, cam in _cams().items():
+            m.UpdateShaderParameters(cam, w, h)
+            ref_hits, ref_rgba, ref_pos, ref_vox = _oracle(oracle_mod, c3_svo, cam, w, h, mode)
+            for _ in range(2):
+                b = _render(torch, m, w, h, mode)
+                try:
+                    _check(b, oracle_mod, ref_hits, ref_rgba, ref_pos, ref_vox, keys=("hits", "rgba", "position", "voxel"))
+                except AssertionError as e:
+                    raise AssertionError(f"pose {name}: {e}") from None
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("back", ["0", "1", "4", "9"])
+def test_every_splat_depth_matches_oracle(torch, oracle_mod, monkeypatch, c3_svo, back):
+    """Boxes from the leaves themselves (0) up to depth 1 (9): the bound only gets looser."""
+    monkeypatch.setenv("SVO_BEAM_BACK", back)
+    w, h = 480, 270
+    m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+    try:
+        m.SetSVOBuffer(c3_svo)
+        for name in ("flyover", "main", "buried"):
+            cam = _cams()[name]
+            m.UpdateShaderParameters(cam, w, h)
+            ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, c3_svo, cam, w, h, 0)
+            b = _render(torch, m, w, h, 0, keys=("hits", "rgba"))
+            _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("off", [(0.0, 0.0), (1.0, 1.0), (0.999, 0.001), (0.5, 0.5)])
+def test_pixel_offsets_at_the_ends_of_the_range(torch, oracle_mod, c3_svo, off):
+    """_PixelOffset anywhere in [0, 1] (RaytracingMaster.cs:35): the splat covers a tile's whole
+    pixel area, so the bound holds for every offset."""
+    w, h = 480, 270
+    cam = CAMERAS["flyover"]()
+    m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+    try:
+        m.SetSVOBuffer(c3_svo)
+        m.UpdateShaderParameters(cam, w, h, pixel_offset=off)
+        ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, c3_svo, cam, w, h, 0, off=off)
+        b = _render(torch, m, w, h, 0, keys=("hits", "rgba"))
+        _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+    finally:
+        m.close()
+
+
+def test_beam_on_and_off_give_identical_frames(torch, monkeypatch, c3_svo):
+    """The full C3 bench frame (1920x1080, flyover and Main.unity poses): the beam-started launch and
+    the continuous one write the same bytes in every output."""
+    w, h = 1920, 1080
+    out = {}
+    for beam in ("1", "0"):
+        monkeypatch.setenv("SVO_BEAM", beam)
+        m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+        try:
+            m.SetSVOBuffer(c3_svo)
+            for name in ("flyover", "main"):
+                m.UpdateShaderParameters(CAMERAS[name](), w, h)
+                for _ in range(3):   # the order settles; every frame must match
+                    b = _render(torch, m, w, h, 0, keys=("hits", "rgba", "rgba8", "position", "voxel"))
+                    out.setdefault((beam, name), []).append({k: v.cpu().numpy().tobytes() for k, v in b.items()})
+        finally:
+            m.close()
+    for name in ("flyover", "main"):
+        for on, off in zip(out[("1", name)], out[("0", name)]):
+            for k in on:
+                assert on[k] == off[k], f"{name}: output {k} differs with beam starts"
+
+
+def test_menger_and_text_pools(torch, oracle_mod, text_svo):
+    """Other trees: the C2 Menger sponge (leaves at every depth of its holes) and the reference's
+    Text fixture, in both stack modes."""
+    for svo, (w, h) in ((build_menger(8), (480, 272)), (text_svo, (256, 256))):
+        m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+        try:
+            m.SetSVOBuffer(svo)
+            for cam in (overview_camera(), CAMERAS["main"]()):
+                for mode in (0, 1):
+                    m.UpdateShaderParameters(cam, w, h)
+                    ref_hits, ref_rgba, ref_pos, ref_vox = _oracle(oracle_mod, svo, cam, w, h, mode)
+                    b = _render(torch, m, w, h, mode)
+                    _check(b, oracle_mod, ref_hits, ref_rgba, ref_pos, ref_vox,
+                           keys=("hits", "rgba", "position", "voxel"))
+        finally:
+            m.close()
+
+
+def test_beam_band_and_samples(torch, oracle_mod, c3_svo):
+    """Rank 2's band of a 4-way 8-row split (global rows index the full-frame bound) and a
+    four-sample launch with jittered offsets (every sample's rays share the tile bound)."""
+    from test_gpu_frame import _oracle_accumulated
+    w, h = 640, 360
+    cam = CAMERAS["flyover"]()
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, c3_svo, cam, w, h, 0)
+    ys = np.concatenate([np.arange(y0, min(y0 + 8, h)) for y0 in range(16, h, 32)])
+    m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+    try:
+        m.SetSVOBuffer(c3_svo)
+        m.UpdateShaderParameters(cam, w, h)
+        b = _bufs(torch, len(ys) * w)
+        m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(), band=(8, 2, 4))
+        m.synchronize()
+        _check(b, oracle_mod, ref_hits.reshape(h, w)[ys].reshape(-1), ref_rgba.reshape(h, w, 4)[ys].reshape(-1, 4),
+               keys=("hits", "rgba"))
+        offs = np.array([[0.1, 0.9], [0.7, 0.3], [0.0, 1.0], [0.55, 0.45]], np.float32)
+        acc = torch.zeros((h * w * 4,), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        m.render_samples(w, h, offs, 0, acc.data_ptr())
+        m.synchronize()
+        want = _oracle_accumulated(oracle_mod, c3_svo, cam, w, h, offs)
+        assert acc.cpu().numpy().tobytes() == want.astype(np.float32).tobytes(), "accumulation differs"
+    finally:
+        m.close()

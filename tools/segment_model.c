@@ -58,7 +58,7 @@ static int seg_trace(const orc_svo *svo, const float o[3], const float d[3], int
     if (t_entry_out) *t_entry_out = t_min;
     if (t_exit_out) *t_exit_out = t_max;
     if (!skip_form) t_min = fmaxf(t_min, t_start);   /* descent form: start at t_k */
-    int armed = armed0;
+    int armed = armed0 == 2 ? t_min >= t_start : armed0;   /* 2: armed at the entry if it lies past t_k */
     if (armed_at) *armed_at = 0;
     uint32_t parent = 0, cd = 0, first = 0;
     int cached = 0, idx = 0;
@@ -307,4 +307,194 @@ void segm_run(const orc_svo *svo, const orc_camera *cam, int w, int h, int mode,
     j.bounds = bounds; j.fin = fin; j.seg_iters = seg_iters; j.iters = iters; j.mism = mism;
     atomic_init(&j.next, 0);
     go(&j, nthreads);
+}
+
+/* ---- beam starts (model of a per-tile conservative start, round 5) ----
+ * For each tile x tile block of pixels: the cone around the block's rays (shared pinhole origin)
+ * and a best-first search over the octree for the nearest box that the cone touches and that is
+ * a leaf voxel or a node at scale <= cut_scale.  Its Euclidean distance from the origin is a lower
+ * bound of every block ray's hit t (t is SVO-space distance: NVIDIASVO.compute:15-19 with a unit
+ * direction).  The rays then start there (seg_trace's exact skip form, armed at the first event
+ * at or past the start). */
+typedef struct { float dist; uint32_t node; float lo[3]; int scale; int term; } bnode;
+
+static void heap_push(bnode *hp, int *n, bnode v) {
+    int i = (*n)++;
+    while (i > 0) { int p = (i - 1) / 2; if (hp[p].dist <= v.dist) break; hp[i] = hp[p]; i = p; }
+    hp[i] = v;
+}
+static bnode heap_pop(bnode *hp, int *n) {
+    bnode top = hp[0], last = hp[--*n];
+    int i = 0;
+    for (;;) {
+        int c = 2 * i + 1;
+        if (c >= *n) break;
+        if (c + 1 < *n && hp[c + 1].dist < hp[c].dist) ++c;
+        if (hp[c].dist >= last.dist) break;
+        hp[i] = hp[c]; i = c;
+    }
+    hp[i] = last;
+    return top;
+}
+static float box_dist(const float o[3], const float lo[3], float size) {
+    float s = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+        float a = lo[k] - o[k], b = o[k] - (lo[k] + size);
+        float m = a > b ? a : b;
+        if (m > 0.0f) s += m * m;
+    }
+    return sqrtf(s);
+}
+static int cone_hits(const float o[3], const float ax[3], float alpha, const float lo[3], float size) {
+    float c[3], v[3];
+    for (int k = 0; k < 3; ++k) { c[k] = lo[k] + 0.5f * size; v[k] = c[k] - o[k]; }
+    float r = 0.8660254f * size * 1.0001f;
+    float L = sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (L <= r) return 1;
+    float ct = (v[0] * ax[0] + v[1] * ax[1] + v[2] * ax[2]) / L;
+    if (ct > 1.0f) ct = 1.0f;
+    if (ct < -1.0f) ct = -1.0f;
+    return acosf(ct) <= alpha + asinf(r / L) + 1e-5f;
+}
+
+typedef struct {
+    const orc_svo *svo; const orc_camera *cam; int w, h, tile, cut; float *tb; uint32_t *pops;
+    int pop_budget, heap_cap;     /* 0: unbounded */
+    atomic_long next;
+} beam_job;
+
+/* drop the farthest entry of a binary min-heap (a leaf position holds it) */
+static float heap_drop_far(bnode *hp, int *n) {
+    int far = *n / 2;
+    for (int i = *n / 2; i < *n; ++i) if (hp[i].dist > hp[far].dist) far = i;
+    float d = hp[far].dist;
+    bnode last = hp[--*n];
+    if (far < *n) {   /* re-insert `last` at `far` (sift up; it came from the last leaf) */
+        int i = far;
+        while (i > 0) { int q = (i - 1) / 2; if (hp[q].dist <= last.dist) break; hp[i] = hp[q]; i = q; }
+        hp[i] = last;
+    }
+    return d;
+}
+
+static void beam_tile(beam_job *j, long t) {
+    const int tx = j->w / j->tile;
+    const int bx = (int)(t % tx) * j->tile, by = (int)(t / tx) * j->tile;
+    float o[3], ax[3] = {0, 0, 0}; static __thread float d[4096][3];
+    int n = 0;
+    for (int y = 0; y < j->tile; ++y)
+        for (int x = 0; x < j->tile; ++x, ++n) {
+            orc_camera_ray(j->cam, (uint32_t)(bx + x), (uint32_t)(by + y), j->w, j->h, o, d[n]);
+            for (int k = 0; k < 3; ++k) ax[k] += d[n][k];
+        }
+    float L = sqrtf(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+    for (int k = 0; k < 3; ++k) ax[k] /= L;
+    float cmin = 1.0f;
+    for (int i = 0; i < n; ++i) {
+        float c = d[i][0] * ax[0] + d[i][1] * ax[1] + d[i][2] * ax[2];
+        if (c < cmin) cmin = c;
+    }
+    const float alpha = acosf(cmin > 1.0f ? 1.0f : cmin) * 1.001f + 1e-6f;
+    const float os[3] = { o[0] * (1.0f / 32.0f) + 1.5f, o[1] * (1.0f / 32.0f) + 1.5f, o[2] * (1.0f / 32.0f) + 1.5f };
+    static __thread bnode hp[1 << 20];
+    int hn = 0;
+    uint32_t pops = 0;
+    bnode root = { box_dist(os, (float[3]){1, 1, 1}, 1.0f), 0, {1, 1, 1}, S_MAX, 0 };
+    float tb = INFINITY, dropped = INFINITY;
+    if (cone_hits(os, ax, alpha, root.lo, 1.0f)) heap_push(hp, &hn, root);
+    while (hn > 0) {
+        if (j->pop_budget && (int)pops >= j->pop_budget) { tb = hp[0].dist; break; }
+        bnode b = heap_pop(hp, &hn);
+        ++pops;
+        if (b.term) { tb = b.dist; break; }
+        uint64_t nd = b.node < j->svo->n_nodes ? j->svo->nodes[b.node] : 0;
+        uint32_t cd = (uint32_t)nd, first = (uint32_t)(nd >> 32);
+        float half = ldexpf(1.0f, b.scale - 1 - S_MAX);
+        for (int c = 0; c < 8; ++c) {
+            if (!((cd >> (15 - c)) & 1)) continue;
+            int hb = c ^ 7;
+            bnode ch;
+            for (int k = 0; k < 3; ++k) ch.lo[k] = b.lo[k] + (((hb >> k) & 1) ? half : 0.0f);
+            if (!cone_hits(os, ax, alpha, ch.lo, half)) continue;
+            int leaf = !((cd >> (7 - c)) & 1);
+            ch.scale = b.scale - 1;
+            ch.node = leaf ? 0 : first + (uint32_t)__builtin_popcount((cd << c) & 0x7Fu);
+            ch.term = leaf || ch.scale <= j->cut;
+            ch.dist = box_dist(os, ch.lo, half);
+            if (hn < (1 << 20)) heap_push(hp, &hn, ch);
+            if (j->heap_cap && hn > j->heap_cap) { float d = heap_drop_far(hp, &hn); if (d < dropped) dropped = d; }
+        }
+    }
+    j->tb[t] = tb < dropped ? tb : dropped;
+    j->pops[t] = pops;
+}
+static void *beam_worker(void *arg) {
+    beam_job *j = (beam_job *)arg;
+    const long n = (long)(j->w / j->tile) * (long)(j->h / j->tile);
+    for (;;) {
+        long t = atomic_fetch_add(&j->next, 1);
+        if (t >= n) break;
+        beam_tile(j, t);
+    }
+    return NULL;
+}
+void segm_beam(const orc_svo *svo, const orc_camera *cam, int w, int h, int tile, int cut_scale, int nthreads,
+               float *tb, uint32_t *pops, int pop_budget, int heap_cap) {
+    beam_job j;
+    memset(&j, 0, sizeof j);
+    j.pop_budget = pop_budget; j.heap_cap = heap_cap;
+    j.svo = svo; j.cam = cam; j.w = w; j.h = h; j.tile = tile; j.cut = cut_scale; j.tb = tb; j.pops = pops;
+    atomic_init(&j.next, 0);
+    pthread_t th[64];
+    if (nthreads > 64) nthreads = 64;
+    int started = 0;
+    for (int i = 1; i < nthreads; ++i)
+        if (pthread_create(&th[started], NULL, beam_worker, &j) == 0) ++started;
+    beam_worker(&j);
+    for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+}
+
+/* Every pixel traced once from its start (skip form, armed at the entry when it lies past the
+ * start): iterations and a mismatch flag against the continuous oracle. */
+typedef struct {
+    const orc_svo *svo; const orc_camera *cam; int w, h, mode; const float *start;
+    uint32_t *it_cont, *it_beam; uint8_t *mism; atomic_long next;
+} brun_job;
+static void *brun_worker(void *arg) {
+    brun_job *j = (brun_job *)arg;
+    const long n = (long)j->w * j->h;
+    for (;;) {
+        long lo = atomic_fetch_add(&j->next, 1) * 1024;
+        if (lo >= n) break;
+        long hi = lo + 1024 < n ? lo + 1024 : n;
+        for (long i = lo; i < hi; ++i) {
+            float o[3], d[3];
+            orc_camera_ray(j->cam, (uint32_t)(i % j->w), (uint32_t)(i / j->w), j->w, j->h, o, d);
+            orc_hit ref, got;
+            uint32_t nc = 0, nb = 0;
+            orc_intersect(j->svo, o, d, j->mode, &ref, NULL, NULL, &nc);
+            memset(&got, 0, sizeof got);
+            int r = seg_trace(j->svo, o, d, j->mode, j->start[i], INFINITY, 2, &got, &nb, NULL, NULL, NULL, 0, 1, NULL, NULL);
+            if (r == 0) { got.parent = 0xFFFFFFFFu; got.hit_idx = 0; got.hit_scale = 0; got.t = INFINITY; }
+            j->it_cont[i] = nc; j->it_beam[i] = nb;
+            j->mism[i] = !(got.parent == ref.parent && got.hit_idx == ref.hit_idx && got.hit_scale == ref.hit_scale &&
+                           fb(got.t) == fb(ref.t));
+        }
+    }
+    return NULL;
+}
+void segm_beam_run(const orc_svo *svo, const orc_camera *cam, int w, int h, int mode, const float *start, int nthreads,
+                   uint32_t *it_cont, uint32_t *it_beam, uint8_t *mism) {
+    brun_job j;
+    memset(&j, 0, sizeof j);
+    j.svo = svo; j.cam = cam; j.w = w; j.h = h; j.mode = mode; j.start = start;
+    j.it_cont = it_cont; j.it_beam = it_beam; j.mism = mism;
+    atomic_init(&j.next, 0);
+    pthread_t th[64];
+    if (nthreads > 64) nthreads = 64;
+    int started = 0;
+    for (int i = 1; i < nthreads; ++i)
+        if (pthread_create(&th[started], NULL, brun_worker, &j) == 0) ++started;
+    brun_worker(&j);
+    for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
 }
