@@ -875,9 +875,11 @@ __device__ __forceinline__ void trace_seg(const LaunchParams &p, FRay &r, uint2 
 // as without a beam.  Returns -inf without beam starts.
 __device__ __forceinline__ float beam_start(const LaunchParams &p, const FRay &f, int x, int gy) {
     if (!p.tile_start) return -__builtin_inff();
-    float d = p.tile_start[(gy >> 3) * p.ts_tiles_x + (x >> 3)];
-    d = fminf(d, p.tile_start[p.ts_super_off + (gy >> 6) * p.ts_super_x + (x >> 6)]);
-    d = fminf(d, p.tile_start[p.ts_global_off]);
+    // an entry of this launch's generation holds its distance, any other is +inf (beam_splat_kernel)
+    const unsigned long long k = min(min(p.tile_start[(gy >> 3) * p.ts_tiles_x + (x >> 3)],
+                                         p.tile_start[p.ts_super_off + (gy >> 6) * p.ts_super_x + (x >> 6)]),
+                                     p.tile_start[p.ts_global_off]);
+    const float d = (uint32_t)(k >> 32) == ~p.ts_gen ? __uint_as_float((uint32_t)k) : __builtin_inff();
     const float m = (2.0f * (fabsf(f.cx) + fabsf(f.cy) + fabsf(f.cz)) + fabsf(f.bx) + fabsf(f.by) + fabsf(f.bz)) *
                     0x1p-20f;
     const float s = d * (1.0f - 0x1p-16f) - m;
@@ -2141,13 +2143,28 @@ hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
 // the edges crossing that plane add their crossing points).  A box a tile's rays miss only costs
 // that tile a lower start; a box they can reach is never left out, so every tile's value is <=
 // the hit t of each of its rays (exact).
-__device__ __forceinline__ void beam_min(float *a, float v) {
-    if (__float_as_uint(v) < __float_as_uint(*a)) atomicMin(reinterpret_cast<unsigned int *>(a), __float_as_uint(v));
+// Entries are 64-bit keys (~gen << 32 | distance bits): a launch's keys are below every older
+// launch's, so one atomic min both replaces a stale entry and keeps the nearest box -- no fill
+// pass; a reader takes an entry of another generation as +inf.  The list is in Morton order, so
+// a workgroup's boxes cover a compact patch of the screen: their tiles are min-ed in an LDS window
+// first and each touched tile costs one global atomic per workgroup (device-scope atomics from
+// every XCD to one address serialise: one atomic per box-tile pair took 72 us per C3 frame).
+constexpr int SPLAT_THREADS = 512, SPLAT_WIN = 8192;
+
+// no read first: a returning load before each atomic put a full memory round trip into every
+// iteration of the flush loop (24 us per C3 frame); the atomic alone returns nothing to wait for
+__device__ __forceinline__ void beam_min(unsigned long long *a, unsigned long long key, uint32_t diag = 0) {
+    if (!(diag & 1)) atomicMin(a, key);
 }
 
-__global__ __launch_bounds__(256) void beam_splat_kernel(BeamParams b) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= b.n_boxes) return;
+// One box of the splat list: kind 0 (no ray reaches it), 1 (tiles [tx0, tx1] x [ty0, ty1]), 2 (the
+// super tiles over them) or 3 (the global word), and its distance from the camera.
+__device__ __forceinline__ void beam_box(const BeamParams &b, uint32_t i, int &kind, int &tx0, int &ty0, int &tx1,
+                                         int &ty1, float &dist) {
+    kind = 0;
+    tx0 = ty0 = 0;
+    tx1 = ty1 = -1;
+    dist = 0.0f;
     const uint2 e = b.boxes[i];
     const int dep = (int)(e.y >> 16);
     const float size = __uint_as_float((uint32_t)(127 - dep) << 23);   // 2^-depth
@@ -2160,17 +2177,19 @@ __global__ __launch_bounds__(256) void beam_splat_kernel(BeamParams b) {
         const float m = fmaxf(fmaxf(rel[k], -(rel[k] + size)), 0.0f);   // gap to the box along axis k
         d2 += m * m;
     }
-    const float dist = sqrtf(d2);
+    dist = __builtin_amdgcn_sqrtf(d2);   // 1 ulp: inside the render's 2^-16 margin
     // outside a side plane of the view frustum (the planes sit a pixel outside the frame): no ray
     const float span = fabsf(rel[0]) + fabsf(rel[1]) + fabsf(rel[2]) + 3.0f * size;
+    bool in = true;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const float *n = b.plane[j];
         const float top = n[0] * rel[0] + n[1] * rel[1] + n[2] * rel[2] +
                           size * (fmaxf(n[0], 0.0f) + fmaxf(n[1], 0.0f) + fmaxf(n[2], 0.0f));
-        if (top < -1e-5f * span) return;
+        in = in && !(top < -1e-5f * span);
     }
-    // corners in (fx, fy, 1)-space: q = Minv (P - o), linear in the corner
+    // the box's corners in (fx, fy, 1)-space, q = Minv (P - o), by increments; its projection is the
+    // hull of the corners' (qx / qz, qy / qz) when every corner lies in front of the camera
     float q0[3], g[3][3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -2178,56 +2197,155 @@ __global__ __launch_bounds__(256) void beam_splat_kernel(BeamParams b) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) g[k][r] = b.minv[3 * r + k] * size;
     }
-    float qx[8], qy[8], qz[8], zmax = -__builtin_inff();
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        qx[c] = q0[0] + ((c & 1) ? g[0][0] : 0.0f) + ((c & 2) ? g[1][0] : 0.0f) + ((c & 4) ? g[2][0] : 0.0f);
-        qy[c] = q0[1] + ((c & 1) ? g[0][1] : 0.0f) + ((c & 2) ? g[1][1] : 0.0f) + ((c & 4) ? g[2][1] : 0.0f);
-        qz[c] = q0[2] + ((c & 1) ? g[0][2] : 0.0f) + ((c & 2) ? g[1][2] : 0.0f) + ((c & 4) ? g[2][2] : 0.0f);
-        zmax = fmaxf(zmax, qz[c]);
-    }
-    if (!(zmax > 0.0f)) return;   // wholly behind the camera
-    float* const ts = b.tile_start;
-    if (dist <= 1e-3f * size) {   // the camera at the box: every ray
-        beam_min(ts + b.global_off, dist);
-        return;
-    }
-    const float eps = zmax * 1e-5f;
+    float zmin = __builtin_inff(), zmax = -__builtin_inff();
     float x0 = __builtin_inff(), x1 = -__builtin_inff(), y0 = __builtin_inff(), y1 = -__builtin_inff();
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        if (qz[c] > eps) {
-            const float fx = qx[c] / qz[c], fy = qy[c] / qz[c];
-            x0 = fminf(x0, fx); x1 = fmaxf(x1, fx); y0 = fminf(y0, fy); y1 = fmaxf(y1, fy);
-        }
+        const float qx = q0[0] + ((c & 1) ? g[0][0] : 0.0f) + ((c & 2) ? g[1][0] : 0.0f) + ((c & 4) ? g[2][0] : 0.0f);
+        const float qy = q0[1] + ((c & 1) ? g[0][1] : 0.0f) + ((c & 2) ? g[1][1] : 0.0f) + ((c & 4) ? g[2][1] : 0.0f);
+        const float qz = q0[2] + ((c & 1) ? g[0][2] : 0.0f) + ((c & 2) ? g[1][2] : 0.0f) + ((c & 4) ? g[2][2] : 0.0f);
+        zmin = fminf(zmin, qz);
+        zmax = fmaxf(zmax, qz);
+        const float rz = __builtin_amdgcn_rcpf(qz);   // 1 ulp: far inside the pixel margin below
+        x0 = fminf(x0, qx * rz); x1 = fmaxf(x1, qx * rz);
+        y0 = fminf(y0, qy * rz); y1 = fmaxf(y1, qy * rz);
+    }
+    in = in && zmax > 0.0f;   // else wholly behind the camera
+    if (in && dist <= 1e-3f * size) {   // the camera at the box: every ray
+        kind = 3;
+    } else if (in && zmin > 1e-5f * zmax) {   // wholly in front: the corners' hull (x0 .. y1 above)
+    } else if (in) {
+        // across the camera plane (rare: near the camera): the corners in front of q_z = eps and the
+        // crossing points of the edges through that plane
+        float qx[8], qy[8], qz[8];
 #pragma unroll
-        for (int bit = 1; bit < 8; bit <<= 1) {   // the 12 edges (c, c | bit), c without bit
-            if (c & bit) continue;
-            const int d = c | bit;
-            if ((qz[c] > eps) == (qz[d] > eps)) continue;
-            const float s = (eps - qz[c]) / (qz[d] - qz[c]);
-            const float fx = (qx[c] + s * (qx[d] - qx[c])) / eps, fy = (qy[c] + s * (qy[d] - qy[c])) / eps;
-            x0 = fminf(x0, fx); x1 = fmaxf(x1, fx); y0 = fminf(y0, fy); y1 = fmaxf(y1, fy);
+        for (int c = 0; c < 8; ++c) {
+            const float sx = (c & 1) ? size : 0.0f, sy = (c & 2) ? size : 0.0f, sz = (c & 4) ? size : 0.0f;
+            qx[c] = b.minv[0] * (rel[0] + sx) + b.minv[1] * (rel[1] + sy) + b.minv[2] * (rel[2] + sz);
+            qy[c] = b.minv[3] * (rel[0] + sx) + b.minv[4] * (rel[1] + sy) + b.minv[5] * (rel[2] + sz);
+            qz[c] = b.minv[6] * (rel[0] + sx) + b.minv[7] * (rel[1] + sy) + b.minv[8] * (rel[2] + sz);
+        }
+        const float eps = zmax * 1e-5f;
+        x0 = y0 = __builtin_inff();
+        x1 = y1 = -__builtin_inff();
+        for (int c = 0; c < 8; ++c) {
+            if (qz[c] > eps) {
+                const float fx = qx[c] / qz[c], fy = qy[c] / qz[c];
+                x0 = fminf(x0, fx); x1 = fmaxf(x1, fx); y0 = fminf(y0, fy); y1 = fmaxf(y1, fy);
+            }
+            for (int bit = 1; bit < 8; bit <<= 1) {   // the 12 edges (c, c | bit), c without bit
+                if (c & bit) continue;
+                const int d = c | bit;
+                if ((qz[c] > eps) == (qz[d] > eps)) continue;
+                const float s = (eps - qz[c]) / (qz[d] - qz[c]);
+                const float fx = (qx[c] + s * (qx[d] - qx[c])) / eps, fy = (qy[c] + s * (qy[d] - qy[c])) / eps;
+                x0 = fminf(x0, fx); x1 = fmaxf(x1, fx); y0 = fminf(y0, fy); y1 = fmaxf(y1, fy);
+            }
+        }
+        x0 -= fabsf(x0) * 1e-5f; x1 += fabsf(x1) * 1e-5f;   // the corner and clipping roundings
+        y0 -= fabsf(y0) * 1e-5f; y1 += fabsf(y1) * 1e-5f;
+    }
+    if (in && kind == 0) {
+        const float mg = 0.05f;   // pixels: rounding of the projection and of the rays' own u, v
+        x0 -= mg; y0 -= mg; x1 += mg; y1 += mg;
+        if (x1 >= 0.0f && y1 >= 0.0f && x0 <= (float)b.width && y0 <= (float)b.height) {
+            tx0 = (int)(fmaxf(x0, 0.0f) * 0.125f);
+            ty0 = (int)(fmaxf(y0, 0.0f) * 0.125f);
+            tx1 = min((int)(fminf(x1, (float)b.width) * 0.125f), b.tiles_x - 1);
+            ty1 = min((int)(fminf(y1, (float)b.height) * 0.125f), b.tiles_y - 1);
+            if (tx1 >= tx0 && ty1 >= ty0) {
+                const int nt = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+                const int ns = ((tx1 >> 3) - (tx0 >> 3) + 1) * ((ty1 >> 3) - (ty0 >> 3) + 1);
+                kind = nt <= 32 ? 1 : ns <= 32 ? 2 : 3;
+            }
         }
     }
-    const float mg = 0.05f;   // pixels: rounding of the projection and of the rays' own u, v
-    x0 -= mg; y0 -= mg; x1 += mg; y1 += mg;
-    if (!(x1 >= 0.0f && y1 >= 0.0f && x0 <= (float)b.width && y0 <= (float)b.height)) return;
-    const int tx0 = (int)(fmaxf(x0, 0.0f) * 0.125f), ty0 = (int)(fmaxf(y0, 0.0f) * 0.125f);
-    const int tx1 = min((int)(fminf(x1, (float)b.width) * 0.125f), b.tiles_x - 1);
-    const int ty1 = min((int)(fminf(y1, (float)b.height) * 0.125f), b.tiles_y - 1);
-    if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) <= 32) {
-        for (int ty = ty0; ty <= ty1; ++ty)
-            for (int tx = tx0; tx <= tx1; ++tx) beam_min(ts + ty * b.tiles_x + tx, dist);
-        return;
+}
+
+constexpr int SPLAT_PER = 1;   // boxes per thread (4: 14.9 us per C3 frame against 8.9 with 1)
+
+__global__ __launch_bounds__(SPLAT_THREADS) void beam_splat_kernel(BeamParams b) {
+    __shared__ uint32_t win[SPLAT_WIN];
+    __shared__ int rect[4];
+    const unsigned long long gen = (unsigned long long)(~b.gen) << 32;
+    unsigned long long *const ts = b.tile_start;
+    int kind[SPLAT_PER], tx0[SPLAT_PER], ty0[SPLAT_PER], tx1[SPLAT_PER], ty1[SPLAT_PER];
+    float dist[SPLAT_PER];
+    const uint32_t base = blockIdx.x * (SPLAT_THREADS * SPLAT_PER) + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < SPLAT_PER; ++k) {
+        const uint32_t i = base + k * SPLAT_THREADS;
+        kind[k] = 0;
+        if (i < b.n_boxes) beam_box(b, i, kind[k], tx0[k], ty0[k], tx1[k], ty1[k], dist[k]);
     }
-    const int sx0 = tx0 >> 3, sx1 = tx1 >> 3, sy0 = ty0 >> 3, sy1 = ty1 >> 3;
-    if ((sx1 - sx0 + 1) * (sy1 - sy0 + 1) <= 32) {
-        for (int sy = sy0; sy <= sy1; ++sy)
-            for (int sx = sx0; sx <= sx1; ++sx) beam_min(ts + b.super_off + sy * b.super_x + sx, dist);
-        return;
+    // the workgroup's tile window: reduced across the wave first (every lane on the same 4 LDS words
+    // serialises: ~8 us per C3 frame), then one LDS atomic per wave
+    if (threadIdx.x == 0) {
+        rect[0] = rect[1] = 0x7FFFFFFF;
+        rect[2] = rect[3] = -1;
     }
-    beam_min(ts + b.global_off, dist);
+    __syncthreads();
+    {
+        int a0 = 0x7FFFFFFF, a1 = 0x7FFFFFFF, a2 = -1, a3 = -1;
+#pragma unroll
+        for (int k = 0; k < SPLAT_PER; ++k)
+            if (kind[k] == 1) {
+                a0 = min(a0, tx0[k]); a1 = min(a1, ty0[k]); a2 = max(a2, tx1[k]); a3 = max(a3, ty1[k]);
+            }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            a0 = min(a0, __shfl_xor(a0, d));
+            a1 = min(a1, __shfl_xor(a1, d));
+            a2 = max(a2, __shfl_xor(a2, d));
+            a3 = max(a3, __shfl_xor(a3, d));
+        }
+        if ((threadIdx.x & 63) == 0 && a2 >= 0) {
+            atomicMin(&rect[0], a0);
+            atomicMin(&rect[1], a1);
+            atomicMax(&rect[2], a2);
+            atomicMax(&rect[3], a3);
+        }
+    }
+    __syncthreads();
+    const int rx0 = rect[0], ry0 = rect[1], rw = rect[2] - rect[0] + 1, rh = rect[3] - rect[1] + 1;
+    const bool lds = rect[2] >= 0 && rw * rh <= SPLAT_WIN;   // workgroup-uniform
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lds)   // rows by wave, columns by lane: no division
+        for (int r = wave; r < rh; r += SPLAT_THREADS / 64)
+            for (int c = lane; c < rw; c += 64) win[r * rw + c] = 0x7F800000u;   // +inf
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SPLAT_PER; ++k) {
+        const unsigned long long key = gen | __float_as_uint(dist[k]);
+        if (kind[k] == 1) {
+            for (int ty = ty0[k]; ty <= ty1[k]; ++ty)
+                for (int tx = tx0[k]; tx <= tx1[k]; ++tx) {
+                    if (lds) {
+                        if (!(b.diag & 2)) atomicMin(&win[(ty - ry0) * rw + (tx - rx0)], __float_as_uint(dist[k]));
+                    } else beam_min(ts + ty * b.tiles_x + tx, key, b.diag);
+                }
+        } else if (kind[k] == 2) {
+            for (int sy = ty0[k] >> 3; sy <= ty1[k] >> 3; ++sy)
+                for (int sx = tx0[k] >> 3; sx <= tx1[k] >> 3; ++sx)
+                    beam_min(ts + b.super_off + sy * b.super_x + sx, key, b.diag);
+        } else if (kind[k] == 3) {
+            beam_min(ts + b.global_off, key, b.diag);
+        }
+    }
+    __syncthreads();
+    if (lds)
+        for (int r = wave; r < rh; r += SPLAT_THREADS / 64)
+            for (int c = lane; c < rw; c += 64) {
+                const uint32_t v = win[r * rw + c];
+                if (v != 0x7F800000u) beam_min(ts + (ry0 + r) * b.tiles_x + rx0 + c, gen | v, b.diag);
+            }
+}
+
+hipError_t launch_beam_splat(const BeamParams &b, hipStream_t stream) {
+    if (b.n_boxes == 0) return hipSuccess;
+    const uint32_t per_wg = SPLAT_THREADS * SPLAT_PER;
+    hipLaunchKernelGGL(beam_splat_kernel, dim3((b.n_boxes + per_wg - 1u) / per_wg), dim3(SPLAT_THREADS), 0, stream, b);
+    return hipGetLastError();
 }
 
 template <int MODE>
@@ -2238,12 +2356,6 @@ static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
         hipLaunchKernelGGL((shadow_tile_kernel<MODE, true>), dim3((unsigned)(bx * by)), dim3(TILE), lds, stream, p, bx);
     else
         hipLaunchKernelGGL((shadow_tile_kernel<MODE>), dim3((unsigned)(bx * by)), dim3(TILE), lds, stream, p, bx);
-    return hipGetLastError();
-}
-
-hipError_t launch_beam_splat(const BeamParams &b, hipStream_t stream) {
-    if (b.n_boxes == 0) return hipSuccess;
-    hipLaunchKernelGGL(beam_splat_kernel, dim3((b.n_boxes + 255u) / 256u), dim3(256), 0, stream, b);
     return hipGetLastError();
 }
 

@@ -119,8 +119,12 @@ struct Sched {
     size_t order_cap = 0;              // order_buf entries allocated
     float4 *seg_hint = nullptr;        // segmented tiles: per pixel the segment starts (svo_traverse.h)
     size_t hint_cap = 0;
-    float *tile_start = nullptr;       // beam starts of this stream's launches (svo_traverse.h)
+    unsigned long long *tile_start = nullptr;   // beam starts of this stream's launches (svo_traverse.h)
     size_t ts_cap = 0;
+    uint32_t ts_gen = 0;               // the generation of the last launch's keys ...
+    unsigned long long ts_view = ~0ull; // ... splatted for this view, splat list and frame size
+    uint64_t ts_boxes = 0;
+    int ts_w = -1, ts_h = -1;
     Geo order_key;                   // the newest build's key (width -1: none)
     Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
@@ -300,8 +304,9 @@ struct svo_ctx {
     size_t boxes_cap = 0;
     uint32_t n_boxes = 0;
     uint64_t boxes_id = 0;           // ... made from the list with this id (0: none)
-    float *count_ts = nullptr;       // beam starts of an instrumented launch (SVO_OPT_COUNT_BEAM)
+    unsigned long long *count_ts = nullptr;   // beam starts of an instrumented launch (SVO_OPT_COUNT_BEAM)
     size_t count_ts_cap = 0;
+    uint32_t count_ts_gen = 0;
     double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold
     int move_every = 4;              // env SVO_MOVE_EVERY: while the camera moves every launch, rebuild the
                                      // order only every k-th launch (see launch; 1 = at every new view).
@@ -521,6 +526,25 @@ std::shared_ptr<const std::vector<uint2>> build_beam_boxes(const uint32_t *lo, c
         cur.swap(nxt);
     }
     if (out->size() >= 0xFFFFFFFFull) return nullptr;
+    // Morton order (coordinates at 16 bits): a splat workgroup's boxes then cover a compact patch
+    // of the screen (svo_kernel.hip beam_splat_kernel's LDS window)
+    auto spread = [](uint64_t v) {
+        v &= 0xFFFFull;
+        v = (v | (v << 16)) & 0x0000FF0000FFull;
+        v = (v | (v << 8)) & 0x00F00F00F00Full;
+        v = (v | (v << 4)) & 0x0C30C30C30C3ull;
+        v = (v | (v << 2)) & 0x249249249249ull;
+        return v;
+    };
+    auto morton = [&](const uint2 &b) {
+        const int sh = 16 - (int)(b.y >> 16);
+        return spread((uint64_t)(b.x & 0xFFFFu) << sh) | spread((uint64_t)(b.x >> 16) << sh) << 1 |
+               spread((uint64_t)(b.y & 0xFFFFu) << sh) << 2;
+    };
+    std::vector<std::pair<uint64_t, uint2>> keyed(out->size());
+    for (size_t i = 0; i < out->size(); ++i) keyed[i] = {morton((*out)[i]), (*out)[i]};
+    std::sort(keyed.begin(), keyed.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    for (size_t i = 0; i < keyed.size(); ++i) (*out)[i] = keyed[i].second;
     return out;
 }
 
@@ -780,11 +804,15 @@ bool beam_camera(const svo::Camera &c, int width, int height, svo::BeamParams *b
         if (!(l > 0.0) || !std::isfinite(l)) return false;
         for (int k = 0; k < 3; ++k) bp->plane[j][k] = (float)(sgn * n[k] / l);
     }
-    for (int r = 0; r < 3; ++r)
+    for (int r = 0; r < 3; ++r) {
+        double a = 0.0;
         for (int k = 0; k < 3; ++k) {
             bp->minv[3 * r + k] = (float)inv[r][k];
             if (!std::isfinite(bp->minv[3 * r + k])) return false;
+            a += std::fabs(inv[r][k]);
         }
+        bp->minv_abs[r] = (float)(a * (1.0 + 1e-6));
+    }
     for (int k = 0; k < 3; ++k) {   // mul4(c2w, (0, 0, 0, 1)) then to_svo, in f32 (both steps exact or one rounding)
         const float w = c.c2w[12 + k];
         if (!std::isfinite(w)) return false;
@@ -1086,8 +1114,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         p.wave_log = ctx->d_wave_log;
     }
     // Beam starts: a tree pool's primary rays start at a per-tile lower bound of
-    // their hit t, splatted from the pool's boxes right before the render, on its stream, every
-    // launch (a function of the camera and the pool only; pixel offsets in [0, 1] are covered).
+    // their hit t, splatted from the pool's boxes right before the render, on its stream.  The
+    // bounds are a function of the camera matrices, the pool and the frame size only (pixel offsets
+    // in [0, 1] are covered), so a launch at the view of this stream's previous one reuses them --
+    // a held view (the reference's accumulating camera) splats once; a moving camera every frame.
     const bool count_beam = p.out.fetches && (ctx->options & SVO_OPT_COUNT_BEAM);
     if (ctx->beam && (q || count_beam) && !p.guard && (!p.out.fetches || count_beam) && ctx->depth_exact) {
         const Upload *root = nullptr;
@@ -1120,24 +1150,33 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             const int tx = (width + 7) / 8, ty = (height + 7) / 8, sx = (width + 63) / 64, sy = (height + 63) / 64;
             const size_t need = (size_t)tx * ty + (size_t)sx * sy + 1;
             // the stream's own buffer; an instrumented launch (no scheduling state) the shared scratch
-            float *&buf = q ? q->tile_start : ctx->count_ts;
+            unsigned long long *&buf = q ? q->tile_start : ctx->count_ts;
             size_t &cap = q ? q->ts_cap : ctx->count_ts_cap;
+            uint32_t &gen = q ? q->ts_gen : ctx->count_ts_gen;
             if (!q) {
                 rc = order_scratch(ctx, s);
                 if (rc) return rc;
             }
-            if (cap < need) {
+            const bool reuse = q && q->ts_view == ctx->view_gen && q->ts_boxes == root->boxes_id && q->ts_w == width &&
+                               q->ts_h == height && cap >= need && gen != 0;
+            if (!reuse && (cap < need || gen == 0xFFFFFFFEu)) {   // (re)filled with all-ones keys: generation 0, stale
                 HIP_TRY(hipDeviceSynchronize());   // a pending launch may still read the old buffer
-                if (buf) hipFree(buf);
-                buf = nullptr;
-                cap = 0;
-                HIP_TRY(hipMalloc(&buf, need * sizeof(float)));
-                cap = need;
+                if (cap < need) {
+                    if (buf) hipFree(buf);
+                    buf = nullptr;
+                    cap = 0;
+                    HIP_TRY(hipMalloc(&buf, need * sizeof(unsigned long long)));
+                    cap = need;
+                }
+                HIP_TRY(hipMemset(buf, 0xFF, cap * sizeof(unsigned long long)));
+                gen = 0;
             }
-            HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(buf), 0x7F800000, need, s));   // +inf
+            if (!reuse) ++gen;
             bp.boxes = ctx->d_boxes;
             bp.n_boxes = ctx->n_boxes;
             bp.tile_start = buf;
+            bp.gen = gen;
+            if (const char *v = std::getenv("SVO_BEAM_DIAG")) bp.diag = (uint32_t)std::atoi(v);   // timing only
             bp.tiles_x = tx;
             bp.tiles_y = ty;
             bp.super_x = sx;
@@ -1146,9 +1185,18 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             bp.global_off = tx * ty + sx * sy;
             bp.width = width;
             bp.height = height;
-            hipError_t eb = svo::launch_beam_splat(bp, s);
-            if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
+            if (!reuse) {
+                hipError_t eb = svo::launch_beam_splat(bp, s);
+                if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
+                if (q) {
+                    q->ts_view = ctx->view_gen;
+                    q->ts_boxes = root->boxes_id;
+                    q->ts_w = width;
+                    q->ts_h = height;
+                }
+            }
             p.tile_start = buf;
+            p.ts_gen = gen;
             p.ts_tiles_x = tx;
             p.ts_super_x = sx;
             p.ts_super_off = bp.super_off;

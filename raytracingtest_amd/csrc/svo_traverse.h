@@ -127,8 +127,11 @@ struct LaunchParams {
     // distance (SVO-space t) at which any primary ray through the tile, at any pixel offset in
     // [0, 1], can first hit a voxel (beam_splat_kernel).  A primary ray starts there, minus a
     // rounding margin, in trace_seg's exact skip form.
-    const float *tile_start;
+    // Entries are keys ~gen << 32 | distance bits (beam_splat_kernel); one of another generation
+    // than ts_gen reads as +inf.
+    const unsigned long long *tile_start;
     int ts_tiles_x, ts_super_x, ts_super_off, ts_global_off;
+    uint32_t ts_gen;
 };
 
 constexpr int SEG_KMAX = 8;                 // segments per ray: 4 (a lane quad) or 8, by cost class
@@ -196,17 +199,21 @@ inline size_t order_strips_entries(int n_tiles, int seg_cap, int kmax = SEG_KMAX
 // Beam starts of one launch: every box of the pool's splat list (the nodes at
 // the splat depth and the leaves above it, svo_rt.hip build_beam_boxes) is projected onto the
 // screen, and its distance from the camera min-ed into every 8x8 tile its projection touches
-// (a 64x64 super tile or the one global word when it touches more than 16).  tile_start must be
-// +inf-filled before (tiles_x * tiles_y + super_x * super_y + 1 floats).
+// (a 64x64 super tile or the one global word when it touches more than 32), as the key
+// ~gen << 32 | distance bits: no fill pass, stale entries lose every min (tiles_x * tiles_y +
+// super_x * super_y + 1 entries; gen > 0, the buffer all-ones when first allocated).
 struct BeamParams {
     const uint2 *boxes;    // (x | y << 16, z | depth << 16): box [1 + i 2^-depth, 1 + (i + 1) 2^-depth]^3
     uint32_t n_boxes;
-    float *tile_start;
+    unsigned long long *tile_start;
+    uint32_t gen;
+    uint32_t diag;         // diagnostics (env SVO_BEAM_DIAG): 1 no global atomics, 2 no LDS window either
     int tiles_x, tiles_y, super_x, super_y, super_off, global_off;
     int width, height;
     float org[3];          // camera origin in SVO space, bit-identical to the render's
     float minv[9];         // row-major inverse of M: unnormalised ray direction = M (fx, fy, 1), fx, fy
                            // continuous pixel coordinates (pixel x, offset o: fx = x + o)
+    float minv_abs[3];     // sum_k |minv[r][k]| per row r, rounded up: a box's half extents in q-space
     float plane[4][3];     // the view frustum's side planes through the camera, normals pointing in
 };
 hipError_t launch_beam_splat(const BeamParams &b, hipStream_t stream);

@@ -46,7 +46,7 @@ def _cams():
         "buried": overview_camera((3.0, -20.0, 2.0), (0.0, -25.0, 20.0)),
         # looking straight along +z and straight down: rays parallel to an axis plane (|coef| = inf)
         "axis_z": overview_camera((0.25, 4.0, -31.0), (0.25, 4.0, 10.0)),
-        "down": overview_camera((0.0, 40.0, 0.0), (0.0, -10.0, 0.0)),
+        "down": overview_camera((0.0, 40.0, 0.0), (0.0, -10.0, 0.5)),
         # far outside the cube, and a 160-degree view inside it
         "far": overview_camera((300.0, 200.0, -500.0), (0.0, 0.0, 0.0)),
         "wide": Camera(position=(1.0, 1.0, 1.0), fov=160.0),
