@@ -485,8 +485,9 @@ def test_loop_form_choice_follows_the_pose(monkeypatch, capfd):
     of the CURRENT camera view: across jumps between unrelated poses of the C3 frame, each
     submitted as a burst of launches with no host sync (the host runs ahead of the GPU),
     every decision taken at a pose uses that pose's own costs -- the sky-heavy overview the
-    latency form, the flyover and Main poses the lean loop.  Reads the
-    library's SVO_LAT_DEBUG trace."""
+    latency form, the flyover and Main poses the lean loop (costs of the walk from
+    the cube entry, SVO_BEAM=0 -- beam starts shorten every wave but the heaviest and make the
+    flyover pose latency-bound too).  Reads the library's SVO_LAT_DEBUG trace."""
     import re
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -494,6 +495,7 @@ def test_loop_form_choice_follows_the_pose(monkeypatch, capfd):
     from raytracingtest_amd.camera import CAMERAS
     from raytracingtest_amd.native_builder import build_sampler_svo
     monkeypatch.setenv("SVO_LAT_DEBUG", "1")
+    monkeypatch.setenv("SVO_BEAM", "0")
     monkeypatch.delenv("SVO_LAT", raising=False)
     monkeypatch.delenv("SVO_LAT_RATIO", raising=False)
     svo = build_sampler_svo(4, 11)   # config C3's pool
