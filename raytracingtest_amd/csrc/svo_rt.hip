@@ -119,12 +119,20 @@ struct Sched {
     size_t order_cap = 0;              // order_buf entries allocated
     float4 *seg_hint = nullptr;        // segmented tiles: per pixel the segment starts (svo_traverse.h)
     size_t hint_cap = 0;
-    unsigned long long *tile_start = nullptr;   // beam starts of this stream's launches (svo_traverse.h)
+    // Beam starts of this stream's launches (svo_traverse.h), double-buffered: the keys of generation
+    // g live in buffer g % 2, splatted on `beam` (its own stream) while the render of g - 1 still runs
+    // on the render stream; the render of g waits for beam_ready, and the splat of g + 2 for ts_read[g % 2]
+    // (the render of g).  A launch at the view of the previous one reuses generation g: no splat, no event.
+    unsigned long long *ts_buf[2] = {};
     size_t ts_cap = 0;
     uint32_t ts_gen = 0;               // the generation of the last launch's keys ...
     unsigned long long ts_view = ~0ull; // ... splatted for this view, splat list and frame size
     uint64_t ts_boxes = 0;
     int ts_w = -1, ts_h = -1;
+    hipStream_t beam = nullptr;
+    hipEvent_t beam_ready = nullptr;
+    hipEvent_t ts_read[2] = {};
+    bool ts_read_valid[2] = {};
     Geo order_key;                   // the newest build's key (width -1: none)
     Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
@@ -419,6 +427,7 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         HIP_TRY(hipEventRecord(pick->done, pick->stream));
         HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
         if (pick->side) HIP_TRY(hipStreamSynchronize(pick->side));   // its order builds (rare: an eviction)
+        if (pick->beam) HIP_TRY(hipStreamSynchronize(pick->beam));   // and beam splats
         reset_builds(*pick);   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
         pick->view_prev = ~0ull;
@@ -1137,7 +1146,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 HIP_TRY(hipDeviceSynchronize());   // launches on any stream may still read the old one
                 if (ctx->boxes_cap < nb) {
                     if (ctx->d_boxes) hipFree(ctx->d_boxes);
-    if (ctx->count_ts) hipFree(ctx->count_ts);
                     ctx->d_boxes = nullptr;
                     ctx->boxes_cap = 0;
                     HIP_TRY(hipMalloc(&ctx->d_boxes, nb * sizeof(uint2)));
@@ -1149,29 +1157,53 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             }
             const int tx = (width + 7) / 8, ty = (height + 7) / 8, sx = (width + 63) / 64, sy = (height + 63) / 64;
             const size_t need = (size_t)tx * ty + (size_t)sx * sy + 1;
-            // the stream's own buffer; an instrumented launch (no scheduling state) the shared scratch
-            unsigned long long *&buf = q ? q->tile_start : ctx->count_ts;
-            size_t &cap = q ? q->ts_cap : ctx->count_ts_cap;
-            uint32_t &gen = q ? q->ts_gen : ctx->count_ts_gen;
-            if (!q) {
+            const bool reuse = q && q->ts_view == ctx->view_gen && q->ts_boxes == root->boxes_id && q->ts_w == width &&
+                               q->ts_h == height && q->ts_cap >= need && q->ts_gen != 0;
+            unsigned long long *buf = nullptr;
+            uint32_t gen = 0;
+            hipStream_t bs = s;   // the splat's stream
+            if (q) {
+                if (!q->beam) {
+                    HIP_TRY(hipStreamCreateWithFlags(&q->beam, hipStreamNonBlocking));
+                    HIP_TRY(hipEventCreateWithFlags(&q->beam_ready, hipEventDisableTiming));
+                    for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&q->ts_read[i], hipEventDisableTiming));
+                }
+                if (!reuse && (q->ts_cap < need || q->ts_gen >= 0xFFFFFFFDu)) {   // all-ones keys: generation 0, stale
+                    HIP_TRY(hipDeviceSynchronize());   // a pending launch or splat may still use the old buffers
+                    for (int i = 0; i < 2; ++i) {
+                        if (q->ts_cap < need) {
+                            if (q->ts_buf[i]) hipFree(q->ts_buf[i]);
+                            q->ts_buf[i] = nullptr;
+                            HIP_TRY(hipMalloc(&q->ts_buf[i], need * sizeof(unsigned long long)));
+                        }
+                        q->ts_read_valid[i] = false;
+                    }
+                    q->ts_cap = std::max(q->ts_cap, need);
+                    for (int i = 0; i < 2; ++i) HIP_TRY(hipMemset(q->ts_buf[i], 0xFF, q->ts_cap * sizeof(unsigned long long)));
+                    q->ts_gen = 0;
+                }
+                if (!reuse) ++q->ts_gen;
+                gen = q->ts_gen;
+                buf = q->ts_buf[gen & 1];
+                bs = q->beam;
+            } else {   // an instrumented launch: the shared scratch, in stream order
                 rc = order_scratch(ctx, s);
                 if (rc) return rc;
-            }
-            const bool reuse = q && q->ts_view == ctx->view_gen && q->ts_boxes == root->boxes_id && q->ts_w == width &&
-                               q->ts_h == height && cap >= need && gen != 0;
-            if (!reuse && (cap < need || gen == 0xFFFFFFFEu)) {   // (re)filled with all-ones keys: generation 0, stale
-                HIP_TRY(hipDeviceSynchronize());   // a pending launch may still read the old buffer
-                if (cap < need) {
-                    if (buf) hipFree(buf);
-                    buf = nullptr;
-                    cap = 0;
-                    HIP_TRY(hipMalloc(&buf, need * sizeof(unsigned long long)));
-                    cap = need;
+                if (ctx->count_ts_cap < need || ctx->count_ts_gen >= 0xFFFFFFFDu) {
+                    HIP_TRY(hipDeviceSynchronize());
+                    if (ctx->count_ts_cap < need) {
+                        if (ctx->count_ts) hipFree(ctx->count_ts);
+                        ctx->count_ts = nullptr;
+                        ctx->count_ts_cap = 0;
+                        HIP_TRY(hipMalloc(&ctx->count_ts, need * sizeof(unsigned long long)));
+                        ctx->count_ts_cap = need;
+                    }
+                    HIP_TRY(hipMemset(ctx->count_ts, 0xFF, ctx->count_ts_cap * sizeof(unsigned long long)));
+                    ctx->count_ts_gen = 0;
                 }
-                HIP_TRY(hipMemset(buf, 0xFF, cap * sizeof(unsigned long long)));
-                gen = 0;
+                gen = ++ctx->count_ts_gen;
+                buf = ctx->count_ts;
             }
-            if (!reuse) ++gen;
             bp.boxes = ctx->d_boxes;
             bp.n_boxes = ctx->n_boxes;
             bp.tile_start = buf;
@@ -1186,9 +1218,18 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             bp.width = width;
             bp.height = height;
             if (!reuse) {
-                hipError_t eb = svo::launch_beam_splat(bp, s);
+                const int bi = (int)(gen & 1);
+                // on the beam stream, after every render that read this buffer (generation gen - 2 and
+                // older: all enqueued before the event recorded when generation gen - 1 began)
+                if (q && q->ts_read_valid[bi]) HIP_TRY(hipStreamWaitEvent(bs, q->ts_read[bi], 0));
+                hipError_t eb = svo::launch_beam_splat(bp, bs);
                 if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
                 if (q) {
+                    HIP_TRY(hipEventRecord(q->beam_ready, bs));
+                    // every render of generation gen - 1 is on s already: the other buffer's readers
+                    HIP_TRY(hipEventRecord(q->ts_read[bi ^ 1], s));
+                    q->ts_read_valid[bi ^ 1] = true;
+                    HIP_TRY(hipStreamWaitEvent(s, q->beam_ready, 0));
                     q->ts_view = ctx->view_gen;
                     q->ts_boxes = root->boxes_id;
                     q->ts_w = width;
@@ -1211,6 +1252,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     }
     hipError_t e = svo::launch_render(p, stack_mode, s, ev0, ev1);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
+
     // refresh: a new geometry, every order_every-th launch while costs can drift, a change of
     // render mode, and a camera move -- right after the first launch at a view the camera then
     // holds (that launch still uses the old order, a permutation of the same tiles, placement
@@ -1544,7 +1586,15 @@ int destroy_single(svo_ctx *ctx) {
     for (Sched &q : ctx->sched) {
         free_sched(q);
         if (q.seg_hint) hipFree(q.seg_hint);
-        if (q.tile_start) hipFree(q.tile_start);
+        if (q.beam) {
+            hipStreamSynchronize(q.beam);
+            hipStreamDestroy(q.beam);
+        }
+        for (int i = 0; i < 2; ++i) {
+            if (q.ts_buf[i]) hipFree(q.ts_buf[i]);
+            if (q.ts_read[i]) hipEventDestroy(q.ts_read[i]);
+        }
+        if (q.beam_ready) hipEventDestroy(q.beam_ready);
         if (q.done) hipEventDestroy(q.done);
         for (int r = 0; r < Sched::STATS_RING; ++r)
             if (q.stats_ev[r]) hipEventDestroy(q.stats_ev[r]);
@@ -2270,6 +2320,8 @@ int svo_forget_stream(svo_ctx *ctx, void *stream) {
         if (!q.used || q.stream != s) continue;
         // the set's buffers stay allocated for the next stream; only the stream is forgotten
         if (q.side) HIP_TRY(hipStreamSynchronize(q.side));
+        if (q.beam) HIP_TRY(hipStreamSynchronize(q.beam));
+        q.ts_read_valid[0] = q.ts_read_valid[1] = false;   // recorded on s, whose renders are all done
         q.used = false;
         q.stream = nullptr;
         reset_builds(q);
