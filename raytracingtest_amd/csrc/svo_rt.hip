@@ -119,20 +119,12 @@ struct Sched {
     size_t order_cap = 0;              // order_buf entries allocated
     float4 *seg_hint = nullptr;        // segmented tiles: per pixel the segment starts (svo_traverse.h)
     size_t hint_cap = 0;
-    // Beam starts of this stream's launches (svo_traverse.h), double-buffered: the keys of generation
-    // g live in buffer g % 2, splatted on `beam` (its own stream) while the render of g - 1 still runs
-    // on the render stream; the render of g waits for beam_ready, and the splat of g + 2 for ts_read[g % 2]
-    // (the render of g).  A launch at the view of the previous one reuses generation g: no splat, no event.
-    unsigned long long *ts_buf[2] = {};
+    unsigned long long *tile_start = nullptr;   // beam starts of this stream's launches (svo_traverse.h)
     size_t ts_cap = 0;
     uint32_t ts_gen = 0;               // the generation of the last launch's keys ...
     unsigned long long ts_view = ~0ull; // ... splatted for this view, splat list and frame size
     uint64_t ts_boxes = 0;
     int ts_w = -1, ts_h = -1;
-    hipStream_t beam = nullptr;
-    hipEvent_t beam_ready = nullptr;
-    hipEvent_t ts_read[2] = {};
-    bool ts_read_valid[2] = {};
     Geo order_key;                   // the newest build's key (width -1: none)
     Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
@@ -315,7 +307,8 @@ struct svo_ctx {
     unsigned long long *count_ts = nullptr;   // beam starts of an instrumented launch (SVO_OPT_COUNT_BEAM)
     size_t count_ts_cap = 0;
     uint32_t count_ts_gen = 0;
-    double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold
+    double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold ...
+    double seg_ratio = 0.28;         // env SVO_SEG_RATIO: ... and the same with beam starts (class table only)
     int move_every = 4;              // env SVO_MOVE_EVERY: while the camera moves every launch, rebuild the
                                      // order only every k-th launch (see launch; 1 = at every new view).
                                      // C3 pan: 118.8 us per frame at 1, 110.7 at 4, 111.9 at 8
@@ -427,7 +420,6 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         HIP_TRY(hipEventRecord(pick->done, pick->stream));
         HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
         if (pick->side) HIP_TRY(hipStreamSynchronize(pick->side));   // its order builds (rare: an eviction)
-        if (pick->beam) HIP_TRY(hipStreamSynchronize(pick->beam));   // and beam splats
         reset_builds(*pick);   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
         pick->view_prev = ~0ull;
@@ -1033,6 +1025,15 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // (SVO_SEG unset: exactly when the launch is latency-bound, i.e. its heaviest chain and not
     // its issued work bounds it -- a strong split's band).
     const int mode_now = p.shadows | (stack_mode << 2);
+    // whether this launch's primary rays get beam starts (the test of the beam block below, less the
+    // per-launch camera checks)
+    bool beam_planned = ctx->beam && q && !p.guard && !p.out.fetches && ctx->depth_exact;
+    if (beam_planned) {
+        bool boxes = false;
+        for (const Upload &u : ctx->uploads)
+            if (u.offset == 0) boxes = u.boxes && !u.boxes->empty();
+        beam_planned = boxes;
+    }
     p.lat = 0;
     bool latency_bound = false;
     const bool have_order = q && [&] { Geo g = q->order_key; g.seg = g.kpack = 0; return g == key; }();
@@ -1064,7 +1065,12 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                     }
                     const size_t lds = (size_t)p.slots * svo::TILE * sizeof(uint2);
                     const double slots = (double)ctx->num_cus * (double)std::min<size_t>(32, (160 * 1024) / lds);
-                    q->lat_cache = m > 0 && (double)t < ctx->lat_ratio * slots * (double)m ? 1 : 0;
+                    // with beam starts the rule picks only the class table (the loop stays lean); measured
+                    // boundary 0.28: C3 bands at N = 2 (flyover 0.18, terrain-facing 0.23, Main.unity 0.27)
+                    // run faster with the latency table, the flyover frame (0.30, 0.30-0.33 panning),
+                    // terrain-facing (0.45) and Main.unity (0.49) with the issue table
+                    const double ratio = beam_planned ? ctx->seg_ratio : ctx->lat_ratio;
+                    q->lat_cache = m > 0 && (double)t < ratio * slots * (double)m ? 1 : 0;
                     q->lat_key = q->stats_key[r];
                     q->lat_view = q->stats_view[r];
                     q->lat_mode = q->stats_mode[r];
@@ -1097,6 +1103,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             if (q->build_key[i] == okey && (use < 0 || q->build_at[i] > q->build_at[use])) use = i;
         }
         p.tile_order = use >= 0 ? q->order_buf[use] : nullptr;
+        if (std::getenv("SVO_ORDER_DEBUG"))   // diagnostics: the order and class table each launch takes
+            std::fprintf(stderr, "svo order: launch %lld view %llu latency %d kpack %x use %d built_at %lld/%lld keys %d/%d\n",
+                         n, ctx->view_gen, (int)latency_bound, okey.kpack, use, q->build_at[0], q->build_at[1],
+                         (int)(q->build_key[0] == okey), (int)(q->build_key[1] == okey));
         if (p.tile_order && okey.seg) {   // the order lists quarter entries: the segmented kernel
             p.seg = okey.seg;
             p.seg_kmax = svo::seg_kmax_of(okey.kpack);
@@ -1157,53 +1167,29 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             }
             const int tx = (width + 7) / 8, ty = (height + 7) / 8, sx = (width + 63) / 64, sy = (height + 63) / 64;
             const size_t need = (size_t)tx * ty + (size_t)sx * sy + 1;
-            const bool reuse = q && q->ts_view == ctx->view_gen && q->ts_boxes == root->boxes_id && q->ts_w == width &&
-                               q->ts_h == height && q->ts_cap >= need && q->ts_gen != 0;
-            unsigned long long *buf = nullptr;
-            uint32_t gen = 0;
-            hipStream_t bs = s;   // the splat's stream
-            if (q) {
-                if (!q->beam) {
-                    HIP_TRY(hipStreamCreateWithFlags(&q->beam, hipStreamNonBlocking));
-                    HIP_TRY(hipEventCreateWithFlags(&q->beam_ready, hipEventDisableTiming));
-                    for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&q->ts_read[i], hipEventDisableTiming));
-                }
-                if (!reuse && (q->ts_cap < need || q->ts_gen >= 0xFFFFFFFDu)) {   // all-ones keys: generation 0, stale
-                    HIP_TRY(hipDeviceSynchronize());   // a pending launch or splat may still use the old buffers
-                    for (int i = 0; i < 2; ++i) {
-                        if (q->ts_cap < need) {
-                            if (q->ts_buf[i]) hipFree(q->ts_buf[i]);
-                            q->ts_buf[i] = nullptr;
-                            HIP_TRY(hipMalloc(&q->ts_buf[i], need * sizeof(unsigned long long)));
-                        }
-                        q->ts_read_valid[i] = false;
-                    }
-                    q->ts_cap = std::max(q->ts_cap, need);
-                    for (int i = 0; i < 2; ++i) HIP_TRY(hipMemset(q->ts_buf[i], 0xFF, q->ts_cap * sizeof(unsigned long long)));
-                    q->ts_gen = 0;
-                }
-                if (!reuse) ++q->ts_gen;
-                gen = q->ts_gen;
-                buf = q->ts_buf[gen & 1];
-                bs = q->beam;
-            } else {   // an instrumented launch: the shared scratch, in stream order
+            // the stream's own buffer; an instrumented launch (no scheduling state) the shared scratch
+            unsigned long long *&buf = q ? q->tile_start : ctx->count_ts;
+            size_t &cap = q ? q->ts_cap : ctx->count_ts_cap;
+            uint32_t &gen = q ? q->ts_gen : ctx->count_ts_gen;
+            if (!q) {
                 rc = order_scratch(ctx, s);
                 if (rc) return rc;
-                if (ctx->count_ts_cap < need || ctx->count_ts_gen >= 0xFFFFFFFDu) {
-                    HIP_TRY(hipDeviceSynchronize());
-                    if (ctx->count_ts_cap < need) {
-                        if (ctx->count_ts) hipFree(ctx->count_ts);
-                        ctx->count_ts = nullptr;
-                        ctx->count_ts_cap = 0;
-                        HIP_TRY(hipMalloc(&ctx->count_ts, need * sizeof(unsigned long long)));
-                        ctx->count_ts_cap = need;
-                    }
-                    HIP_TRY(hipMemset(ctx->count_ts, 0xFF, ctx->count_ts_cap * sizeof(unsigned long long)));
-                    ctx->count_ts_gen = 0;
-                }
-                gen = ++ctx->count_ts_gen;
-                buf = ctx->count_ts;
             }
+            const bool reuse = q && q->ts_view == ctx->view_gen && q->ts_boxes == root->boxes_id && q->ts_w == width &&
+                               q->ts_h == height && cap >= need && gen != 0;
+            if (!reuse && (cap < need || gen == 0xFFFFFFFEu)) {   // (re)filled with all-ones keys: generation 0, stale
+                HIP_TRY(hipDeviceSynchronize());   // a pending launch may still read the old buffer
+                if (cap < need) {
+                    if (buf) hipFree(buf);
+                    buf = nullptr;
+                    cap = 0;
+                    HIP_TRY(hipMalloc(&buf, need * sizeof(unsigned long long)));
+                    cap = need;
+                }
+                HIP_TRY(hipMemset(buf, 0xFF, cap * sizeof(unsigned long long)));
+                gen = 0;
+            }
+            if (!reuse) ++gen;
             bp.boxes = ctx->d_boxes;
             bp.n_boxes = ctx->n_boxes;
             bp.tile_start = buf;
@@ -1218,18 +1204,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             bp.width = width;
             bp.height = height;
             if (!reuse) {
-                const int bi = (int)(gen & 1);
-                // on the beam stream, after every render that read this buffer (generation gen - 2 and
-                // older: all enqueued before the event recorded when generation gen - 1 began)
-                if (q && q->ts_read_valid[bi]) HIP_TRY(hipStreamWaitEvent(bs, q->ts_read[bi], 0));
-                hipError_t eb = svo::launch_beam_splat(bp, bs);
+                hipError_t eb = svo::launch_beam_splat(bp, s);
                 if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
                 if (q) {
-                    HIP_TRY(hipEventRecord(q->beam_ready, bs));
-                    // every render of generation gen - 1 is on s already: the other buffer's readers
-                    HIP_TRY(hipEventRecord(q->ts_read[bi ^ 1], s));
-                    q->ts_read_valid[bi ^ 1] = true;
-                    HIP_TRY(hipStreamWaitEvent(s, q->beam_ready, 0));
                     q->ts_view = ctx->view_gen;
                     q->ts_boxes = root->boxes_id;
                     q->ts_w = width;
@@ -1252,7 +1229,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     }
     hipError_t e = svo::launch_render(p, stack_mode, s, ev0, ev1);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("render launch: ") + hipGetErrorString(e));
-
     // refresh: a new geometry, every order_every-th launch while costs can drift, a change of
     // render mode, and a camera move -- right after the first launch at a view the camera then
     // holds (that launch still uses the old order, a permutation of the same tiles, placement
@@ -1586,15 +1562,7 @@ int destroy_single(svo_ctx *ctx) {
     for (Sched &q : ctx->sched) {
         free_sched(q);
         if (q.seg_hint) hipFree(q.seg_hint);
-        if (q.beam) {
-            hipStreamSynchronize(q.beam);
-            hipStreamDestroy(q.beam);
-        }
-        for (int i = 0; i < 2; ++i) {
-            if (q.ts_buf[i]) hipFree(q.ts_buf[i]);
-            if (q.ts_read[i]) hipEventDestroy(q.ts_read[i]);
-        }
-        if (q.beam_ready) hipEventDestroy(q.beam_ready);
+        if (q.tile_start) hipFree(q.tile_start);
         if (q.done) hipEventDestroy(q.done);
         for (int r = 0; r < Sched::STATS_RING; ++r)
             if (q.stats_ev[r]) hipEventDestroy(q.stats_ev[r]);
@@ -1679,6 +1647,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_SEG_ALL")) ctx->seg_all = std::atoi(k) == 8 ? 8 : std::atoi(k) != 0 ? 4 : 0;
     if (const char *k = std::getenv("SVO_SEG_SCRAMBLE")) ctx->seg_scramble = (uint32_t)std::strtoul(k, nullptr, 10);
     if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
+    if (const char *k = std::getenv("SVO_SEG_RATIO")) ctx->seg_ratio = std::atof(k);
     if (const char *k = std::getenv("SVO_BEAM")) ctx->beam = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_BEAM_BACK")) ctx->beam_back = std::max(0, std::atoi(k));
     if (e != hipSuccess) {
@@ -2320,8 +2289,6 @@ int svo_forget_stream(svo_ctx *ctx, void *stream) {
         if (!q.used || q.stream != s) continue;
         // the set's buffers stay allocated for the next stream; only the stream is forgotten
         if (q.side) HIP_TRY(hipStreamSynchronize(q.side));
-        if (q.beam) HIP_TRY(hipStreamSynchronize(q.beam));
-        q.ts_read_valid[0] = q.ts_read_valid[1] = false;   // recorded on s, whose renders are all done
         q.used = false;
         q.stream = nullptr;
         reset_builds(q);

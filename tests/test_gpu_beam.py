@@ -182,3 +182,34 @@ def test_beam_band_and_samples(torch, oracle_mod, c3_svo):
         assert acc.cpu().numpy().tobytes() == want.astype(np.float32).tobytes(), "accumulation differs"
     finally:
         m.close()
+
+
+def test_views_and_held_bursts_without_host_sync(torch, oracle_mod, c3_svo):
+    """Beam starts are double-buffered and splatted on their own stream while the previous render
+    runs (svo_rt.hip launch): a sequence of view changes and held-view bursts submitted with no host
+    synchronisation -- each frame into its own buffers -- must give every frame its own view's
+    records (a splat overwriting a buffer a queued render still reads would not)."""
+    from raytracingtest_amd.camera import FLYOVER_EYE, FLYOVER_TARGET
+    w, h = 640, 360
+    views = []
+    for i in range(4):
+        a = 0.05 * i
+        eye = (FLYOVER_EYE[0] + 4.0 * np.sin(a), FLYOVER_EYE[1] - 2.0 * i, FLYOVER_EYE[2] + 4.0 * (1.0 - np.cos(a)))
+        views.append(overview_camera(eye, FLYOVER_TARGET))
+    refs = [_oracle(oracle_mod, c3_svo, cam, w, h, 0)[:2] for cam in views]
+    seq = [0, 0, 0, 1, 2, 2, 3, 0, 0, 1, 1, 1, 1, 2, 3, 3, 0]
+    m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+    try:
+        m.SetSVOBuffer(c3_svo)
+        outs = [_bufs(torch, w * h) for _ in seq]   # (each fill synchronises the device: all before)
+        for v, b in zip(seq, outs):
+            m.UpdateShaderParameters(views[v], w, h)
+            m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr())
+        m.synchronize()
+        for k, (v, b) in enumerate(zip(seq, outs)):
+            try:
+                _check(b, oracle_mod, refs[v][0], refs[v][1], keys=("hits", "rgba"))
+            except AssertionError as e:
+                raise AssertionError(f"frame {k} (view {v}): {e}") from None
+    finally:
+        m.close()

@@ -21,6 +21,9 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--cycle", type=int, default=0,
+                    help="diagnostics: cycle through the first k views of the pan (a new view per frame, "
+                         "views repeating) instead of panning on")
     a = ap.parse_args()
     import torch
     from bench import CONFIGS
@@ -67,7 +70,7 @@ def main():
             t0 = time.perf_counter()
             for k in range(a.frames):
                 if name == "moving":
-                    set_view(k + 1)
+                    set_view(k % a.cycle + 1 if a.cycle else k + 1)
                 render()
             t_host = time.perf_counter() - t0
             torch.cuda.synchronize()
@@ -76,7 +79,7 @@ def main():
             rm.kernel_time()
             for k in range(a.frames):
                 if name == "moving":
-                    set_view(k + 1)
+                    set_view(k % a.cycle + 1 if a.cycle else k + 1)
                 render()
             kms, n = rm.kernel_time()
             rm.set_kernel_timing(False)
