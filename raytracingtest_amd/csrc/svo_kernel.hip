@@ -1727,7 +1727,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
                                                                      uint32_t *__restrict__ order, int n, int tiles_x,
                                                                      uint32_t *stats, int seg_cap,
                                                                      const uint16_t *__restrict__ part_cost,
-                                                                     int seg_kpack) {
+                                                                     int seg_kpack, int spread) {
     __shared__ uint32_t red[ORDER_THREADS / 64], red_sum[ORDER_THREADS / 64];
     constexpr int NC = 6;
     __shared__ uint32_t cnt[NC], base[NC + 1], rank[NC], segs[NC];
@@ -1755,6 +1755,22 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         if (w.r >= tiles_y) { w.r -= tiles_y; w.c += 1; }
     };
     auto tile_of = [&](const Walk &w) { return w.r * tiles_x + strip_col(x, w.c); };
+    // spread (a moving camera: the costs are a few frames old and the heavy tiles have drifted by up to
+    // a tile on screen): a tile's class is that of the heaviest of it and its 8 neighbours
+    auto class_cost = [&](const Walk &w) -> uint32_t {
+        const int col = strip_col(x, w.c);
+        if (!spread) return cost_at(w.r * tiles_x + col);
+        uint32_t m = 0;
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int r = w.r + dy;
+            if (r < 0 || r >= tiles_y) continue;
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int c = col + dx;
+                if (c >= 0 && c < tiles_x) m = max(m, cost_at(r * tiles_x + c));
+            }
+        }
+        return m;
+    };
     uint32_t mx = 0, sum = 0;
     for (Walk w = start(); w.e < len; next(w)) {
         const uint32_t k = cost_at(tile_of(w));
@@ -1789,7 +1805,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     auto cls = [mx](uint32_t k) {
         return 8 * k >= 7 * mx ? 0 : 4 * k >= 3 * mx ? 1 : 2 * k >= mx ? 2 : 4 * k >= mx ? 3 : 8 * k >= mx ? 4 : 5;
     };
-    for (Walk w = start(); w.e < len; next(w)) atomicAdd(&cnt[cls(cost_at(tile_of(w)))], 1u);
+    for (Walk w = start(); w.e < len; next(w)) atomicAdd(&cnt[cls(class_cost(w))], 1u);
     __syncthreads();
     const int G = 8 * L;   // the grid, and where the class ends go
     if (tid == 0) {
@@ -1811,7 +1827,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     __syncthreads();
     for (Walk w = start(); w.e < len; next(w)) {
         const int t = tile_of(w);
-        const int c = cls(cost_at(t));
+        const int c = cls(class_cost(w));
         const uint32_t r = atomicAdd(&rank[c], 1u);
         const uint32_t kc = (uint32_t)(seg_kpack >> (4 * c)) & 15u;
         if (r < segs[c]) {
@@ -1827,7 +1843,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
 }
 
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
-                               uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_kpack) {
+                               uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_kpack, int spread) {
     if (n_tiles <= 0) return hipSuccess;
     if (seg_cap > 0 && (n_tiles / tiles_x) * tiles_x != n_tiles) return hipErrorInvalidValue;
     for (int c = 0; c < 6; ++c) {
@@ -1837,7 +1853,7 @@ hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tile
     if (seg_cap > 0 && ((size_t)order_strips_grid(n_tiles, seg_cap, seg_kmax_of(seg_kpack)) >> 28) != 0)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
-                       stats, seg_cap, part_cost, seg_kpack);
+                       stats, seg_cap, part_cost, seg_kpack, spread);
     return hipGetLastError();
 }
 

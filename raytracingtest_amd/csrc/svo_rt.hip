@@ -308,6 +308,7 @@ struct svo_ctx {
     size_t count_ts_cap = 0;
     uint32_t count_ts_gen = 0;
     double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold ...
+    int spread = 1;                  // env SVO_SPREAD=0: a moving camera's order classes tiles by their own costs only
     double seg_ratio = 0.28;         // env SVO_SEG_RATIO: ... and the same with beam starts (class table only)
     int move_every = 4;              // env SVO_MOVE_EVERY: while the camera moves every launch, rebuild the
                                      // order only every k-th launch (see launch; 1 = at every new view).
@@ -1236,6 +1237,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // move_every-th launch: each build is an order kernel plus an event on the render stream, and
     // the last few frames' costs order a slowly moving view almost as well as its own
     bool refresh = false;
+    bool moving_build = false;   // the build follows a launch at a new view (a moving camera)
     if (q && p.tile_cost) {
         const unsigned long long n = q->launches++;   // (p.tile_cost is cost_buf[n % 2])
         const bool moving = q->view_prev != ctx->view_gen;   // a new view since this stream's last launch
@@ -1247,6 +1249,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         refresh = q->order_key != okey || (n % ctx->order_every == 0 && drift) || q->built_mode != mode_now ||
                   (q->built_view != ctx->view_gen && (!moving || n - q->last_build >= (unsigned long long)ctx->move_every));
         if (refresh) q->last_build = n;
+        moving_build = moving;
     }
     if (refresh) {   // the launch after next at this geometry dispatches the heaviest tiles first
         const int r = q->stats_head;
@@ -1257,7 +1260,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         HIP_TRY(hipEventRecord(q->render_done, s));
         HIP_TRY(hipStreamWaitEvent(q->side, q->render_done, 0));
         e = p.xcd_remap == 2 ? svo::launch_order_strips(p.tile_cost, q->order_buf[bi], n_tiles, (width + 7) / 8, q->side,
-                                                        st16, okey.seg, p.part_cost, okey.kpack)
+                                                        st16, okey.seg, p.part_cost, okey.kpack,
+                                                        moving_build && ctx->spread ? 1 : 0)
                              : svo::launch_order_tiles(p.tile_cost, q->order_buf[bi], n_tiles, q->side, st16);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         HIP_TRY(hipEventRecord(q->build_ev[bi], q->side));
@@ -1648,6 +1652,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_SEG_SCRAMBLE")) ctx->seg_scramble = (uint32_t)std::strtoul(k, nullptr, 10);
     if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
     if (const char *k = std::getenv("SVO_SEG_RATIO")) ctx->seg_ratio = std::atof(k);
+    if (const char *k = std::getenv("SVO_SPREAD")) ctx->spread = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_BEAM")) ctx->beam = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_BEAM_BACK")) ctx->beam_back = std::max(0, std::atoi(k));
     if (e != hipSuccess) {
