@@ -631,10 +631,18 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// acc_x: out.accum[i].x when out.accum is set, loaded by the caller before its trace (the line then
-// waits in L2 for the epilogue's read instead of costing every wave an HBM round trip at its end:
-// the S = 1 samples route took 1.15x the render kernel's time without it)
-__device__ __forceinline__ void store_outputs(const Outputs &out, size_t i, const Record &o, float acc_x = 0.0f) {
+// The one-sample route's read of the accumulation (0 elsewhere; a non-temporal load measured 3 %
+// slower).
+__device__ __forceinline__ float4 accum_load(const LaunchParams &p, size_t i) {
+    if (!p.out.accum) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    return p.out.accum[i];
+}
+
+// d0: out.accum[i] when out.accum is set, loaded by the caller right after its trace and before
+// `record`, so its memory latency overlaps the attachment fetch of the shading instead of following
+// it (loaded before the trace it would hold up the first trip: loads retire in order)
+__device__ __forceinline__ void store_outputs(const Outputs &out, size_t i, const Record &o,
+                                              float4 d0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f)) {
     // the words as scalars first: vectors built straight from the array kept it in private memory
     // in render_seg_kernel
     const uint32_t w0 = o.w[0], w1 = o.w[1], w2 = o.w[2], w3 = o.w[3], w4 = o.w[4], w5 = o.w[5];
@@ -651,9 +659,8 @@ __device__ __forceinline__ void store_outputs(const Outputs &out, size_t i, cons
         __builtin_nontemporal_store(f32x4{o.rgb[0], o.rgb[1], o.rgb[2], 1.0f}, reinterpret_cast<f32x4 *>(out.rgba + i));
     float dr = o.rgb[0], dg = o.rgb[1], db = o.rgb[2];   // the colour the display words carry
     if (out.accum) {   // accumulate_kernel's blend (AddShader.shader:44-47), the Result alpha is a
-        const float4 d0 = out.accum[i];
         const float a = out.acc_a, b = out.acc_b;
-        dr = o.rgb[0] * a + acc_x * b;   // == d0.x (the same word, read earlier)
+        dr = o.rgb[0] * a + d0.x * b;
         dg = o.rgb[1] * a + d0.y * b;
         db = o.rgb[2] * a + d0.z * b;
         const float dw = a * a + d0.w * b;
@@ -965,7 +972,6 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
     uint2 *stk = stk_base + lane;
     uint32_t t0 = 0;
     if (!COUNT && p.wave_log) t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    const float acc_x = !COUNT && p.out.accum ? p.out.accum[out_index(p, lr, gy, x)].x : 0.0f;
     FRay f;
     to_fray(r, f);
     LeanDiag dg;
@@ -986,6 +992,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
         p.out.fetches[(size_t)lr * (size_t)p.width + (size_t)x] = r.fetches;
         return;
     }
+    const float4 acc = accum_load(p, out_index(p, lr, gy, x));
     Record o;
     record(p, r, x, gy, o);
     int trips = f.trips;
@@ -1030,7 +1037,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
         w[6] = dg.fetch_trips;
         w[7] = dg.pop_trips;
     }
-    store_outputs(p.out, out_index(p, lr, gy, x), o, acc_x);
+    store_outputs(p.out, out_index(p, lr, gy, x), o, acc);
     if (p.wave_log && lane == 0) p.wave_log[WAVE_LOG_WORDS * (size_t)blockIdx.x + 9] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 }
 
@@ -1145,7 +1152,6 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
     const bool have = hint8[0] == hint8[0];                        // NaN: none yet
     const float t_start = seg_start(p, hint8, have, hi, e0, t_entry, t_exit);
     const float t_stop = seg_start(p, hint8, have, hi, e1, t_entry, t_exit);
-    const float acc_x = p.out.accum ? p.out.accum[out_index(p, lr, gy, x)].x : 0.0f;
     uint32_t n_lane, armed_at;
     bool stopped;
     trace_seg<MODE, FA>(p, f, stk, k == 0 ? bs : t_start, t_stop, k == 0 && r.t_min >= bs, n_lane, armed_at,
@@ -1185,9 +1191,10 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
         }
     }
     if (!writer || !inside) return;
+    const float4 acc = accum_load(p, out_index(p, lr, gy, x));
     Record o;
     record(p, r, x, gy, o);
-    store_outputs(p.out, out_index(p, lr, gy, x), o, acc_x);
+    store_outputs(p.out, out_index(p, lr, gy, x), o, acc);
 }
 
 template <int MODE, bool FA, bool LAT>
@@ -1218,13 +1225,13 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
             camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
             setup_ray(org, dir, r);
         }
-        const float acc_x = p.out.accum ? p.out.accum[out_index(p, lr, gy, x)].x : 0.0f;
         FRay f;
         to_fray(r, f);
         if (LAT) trace_lat<MODE>(p, f, stk);
         else if (p.tile_start) trace_beam<MODE, FA>(p, f, stk, beam_start(p, f, x, gy));
         else trace_lean<MODE, false, false, FA>(p, f, stk);
         from_fray(f, r);
+        const float4 acc = accum_load(p, out_index(p, lr, gy, x));
         Record o;
         record(p, r, x, gy, o);
         if (p.out.hitmask) {
@@ -1232,7 +1239,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
             if (lane == 0) p.out.hitmask[t] = hm;
         }
         if (p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, (int)(SEG_COST_FLAG - 1));
-        store_outputs(p.out, out_index(p, lr, gy, x), o, acc_x);
+        store_outputs(p.out, out_index(p, lr, gy, x), o, acc);
         return;
     }
     if (code <= 4) seg_part<MODE, FA, 4>(p, stk_base, t, code - 1, bx, by);

@@ -1071,7 +1071,13 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                     // run faster with the latency table, the flyover frame (0.30, 0.30-0.33 panning),
                     // terrain-facing (0.45) and Main.unity (0.49) with the issue table
                     const double ratio = beam_planned ? ctx->seg_ratio : ctx->lat_ratio;
-                    q->lat_cache = m > 0 && (double)t < ratio * slots * (double)m ? 1 : 0;
+                    // hysteresis of 15 % around it once this geometry and mode have a decision: costs
+                    // measured under one class table (or with jittered rays) move T a little, and a
+                    // flip near the boundary costs more than either table (the next launches find no
+                    // order built for the other table's class layout)
+                    const bool prior = q->lat_key == q->stats_key[r] && q->lat_mode == q->stats_mode[r];
+                    const double bound = !prior ? ratio : q->lat_cache ? ratio * 1.15 : ratio / 1.15;
+                    q->lat_cache = m > 0 && (double)t < bound * slots * (double)m ? 1 : 0;
                     q->lat_key = q->stats_key[r];
                     q->lat_view = q->stats_view[r];
                     q->lat_mode = q->stats_mode[r];
@@ -1103,14 +1109,24 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             }
             if (q->build_key[i] == okey && (use < 0 || q->build_at[i] > q->build_at[use])) use = i;
         }
+        if (use < 0) {   // none for this class table yet: the newest at this geometry, with its own table
+            for (int i = 0; i < 2; ++i) {
+                if (q->build_at[i] < 0 || q->build_at[i] > n - 2) continue;
+                Geo g = q->build_key[i];
+                if (g.seg && !seg_cap) continue;   // part entries only where this launch may segment
+                g.seg = g.kpack = 0;
+                if (g == key && (use < 0 || q->build_at[i] > q->build_at[use])) use = i;
+            }
+        }
         p.tile_order = use >= 0 ? q->order_buf[use] : nullptr;
         if (std::getenv("SVO_ORDER_DEBUG"))   // diagnostics: the order and class table each launch takes
             std::fprintf(stderr, "svo order: launch %lld view %llu latency %d kpack %x use %d built_at %lld/%lld keys %d/%d\n",
                          n, ctx->view_gen, (int)latency_bound, okey.kpack, use, q->build_at[0], q->build_at[1],
                          (int)(q->build_key[0] == okey), (int)(q->build_key[1] == okey));
-        if (p.tile_order && okey.seg) {   // the order lists quarter entries: the segmented kernel
-            p.seg = okey.seg;
-            p.seg_kmax = svo::seg_kmax_of(okey.kpack);
+        const Geo &bk = use >= 0 ? q->build_key[use] : okey;   // the class layout the order was built with
+        if (p.tile_order && bk.seg) {   // the order lists part entries: the segmented kernel
+            p.seg = bk.seg;
+            p.seg_kmax = svo::seg_kmax_of(bk.kpack);
             p.seg_hint = q->seg_hint;
             if (ctx->seg_scramble) p.seg_scramble = ctx->seg_scramble * 0x9E3779B9u + ++ctx->seg_launches;
         }
