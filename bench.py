@@ -358,10 +358,14 @@ def main():
                          "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
                          "kernel_ms_events": round(m["kern_ms_events"], 4),
                          "event_floor_ms": round(m["floor_ms"], 4),
+                         "kernel_ms_bracket_minus_floor": round(m["kern_ms_bracket"], 4),
+                         "gpu_span_ms_per_step": round(m["span_ms"], 4),
                          "kernel_ms_le_step": bool(kern_ms <= ms_per_step),
-                         "kernel": "render_seg_kernel / render_tile_kernel (the primary-ray launch; library HIP events "
-                                   "around that kernel alone, K steps after the timed region, minus event_floor_ms: "
-                                   "the same event pair around a one-element kernel on the same stream)",
+                         "kernel": "render_seg_kernel / render_tile_kernel (the primary-ray launch). N = 1: kernel_ms = "
+                                   "the timed region's GPU span per step (one HIP event pair around the K launches on "
+                                   "their stream; they run back to back and nothing else runs there at a held view); "
+                                   "kernel_ms_events: library events around each launch (K more steps), which add the "
+                                   "bracket's marker processing; N > 1: kernel_ms = kernel_ms_events - event_floor_ms",
                          "bound_note": "dependent node-fetch chain at 8 waves/SIMD (DESIGN.md 5.1); frac is the "
                                        "metric's algorithmic-bytes fraction of HBM peak, hbm_frac the PMC fabric "
                                        "bytes' (FETCH_SIZE x2 + WRITE_SIZE), l2_frac algorithmic bytes vs L2 peak",
@@ -490,12 +494,18 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     step_events = os.environ.get("SVO_STEP_EVENTS", "0") != "0"
+    # one event pair around the whole timed region on the launch stream: with one GPU the K launches
+    # run back to back, so its span / K is the render kernel's mean duration with no per-launch
+    # bracket (a bracket around each launch adds ~5 us of marker processing to what it times)
+    span0, span1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    span0.record(stream)
     for i in range(args.steps):
         if step_events:
             ev[i][0].record(stream)
         step()
         if step_events:
             ev[i][1].record(stream)
+    span1.record(stream)
     drain()   # the last frame's assemble (each step assembles the previous frame)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -520,7 +530,12 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     # the event pair's own cost (the bracketed kernel read longer than the step
     # it belongs to): the same two hipEventRecords around a one-element kernel on the same stream
     floor_ms = event_floor_ms(stream, dev)
-    kern_ms = max(kern_ms_events - floor_ms, 1e-6)
+    kern_ms_bracket = max(kern_ms_events - floor_ms, 1e-6)
+    span_ms = span0.elapsed_time(span1) / args.steps
+    # N = 1: the timed region's GPU span per launch (only the render kernel runs on the stream at a
+    # held view: the beam splat and the order builds happened in the warmup); N > 1: the bracketed
+    # kernel (the steps also hold the gather)
+    kern_ms = span_ms if gather is None else kern_ms_bracket
     host_hits = (hits if gather is None else gather.local_hits()).cpu().numpy().view(_lib.HIT_DTYPE)
     n_hit = int(np.count_nonzero(host_hits["flags"] & 1))
     F_ref = int(fetch[:n_px].to(torch.int64).sum().item())
@@ -547,7 +562,8 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
                 band=band,
                 deal_info=deal_info, payload_choice=payload_choice, bytes_per_launch=bytes_per_launch,
                 elapsed=elapsed, kern_ms=kern_ms, kern_ms_max=kern_ms_max, stages=stages, frame_check=frame_check,
-                per_rank=per_rank, step_ms=step_ms, step=step, kern_ms_events=kern_ms_events, floor_ms=floor_ms)
+                per_rank=per_rank, step_ms=step_ms, step=step, kern_ms_events=kern_ms_events, floor_ms=floor_ms,
+                kern_ms_bracket=kern_ms_bracket, span_ms=span_ms)
 
 
 def event_floor_ms(stream, dev, n=200):
@@ -1393,13 +1409,13 @@ def samples_in_flight(rm, W, H, args, dev, stream, sizes=(1, 2, 4, 8), floor_ms=
             step()
         torch.cuda.synchronize(dev)
         ms = (time.perf_counter() - t) / args.steps * 1e3
-        rm.set_kernel_timing(True)
-        rm.kernel_time()
-        for _ in range(args.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):   # the GPU span per launch, as the render kernel's kernel_ms
             step()
-        kern, _ = rm.kernel_time()
-        rm.set_kernel_timing(False)
-        kern = max(kern - floor_ms, 1e-6)   # the event pair's own cost, as the render kernel's
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        kern = e0.elapsed_time(e1) / args.steps
         out[str(S)] = {"ms_per_step": round(ms, 4), "kernel_ms": round(kern, 4),
                        "Mrays_per_s": round(S * W * H / (ms * 1e-3) / 1e6, 2),
                        "kernel_Mrays_per_s": round(S * W * H / (kern * 1e-3) / 1e6, 2)}
@@ -1411,8 +1427,8 @@ def strong_split_bands(rm, W, H, args, dev, stream, hits, rgba, kern_ms, floor_m
     """One-GPU rehearsal of the metric's frame split over N GPUs: every rank's
     round-robin 8-row band of the same frame rendered alone on this GPU (the launch each GPU of an
     N-way split runs, segmented heavy tiles and loop form chosen by the library as there), its
-    render-kernel time (library events minus the event floor, median of `timed` launches after a
-    warmup), and the predicted N-GPU speed-up of the one-sample frame = this run's kernel_ms over
+    GPU time per launch (one event pair around `timed` back-to-back launches after a warmup, as the
+    one-GPU kernel_ms), and the predicted N-GPU speed-up of the one-sample frame = this run's kernel_ms over
     the slowest rank's band.  The RCCL gather and display-rank assemble are not in it (they
     overlap the next frame's render)."""
     import torch
@@ -1424,14 +1440,15 @@ def strong_split_bands(rm, W, H, args, dev, stream, hits, rgba, kern_ms, floor_m
             for _ in range(30):
                 rm.render_frame(W, H, hits=hits.data_ptr(), rgba=None if rgba is None else rgba.data_ptr(),
                                 stack_mode=args.stack_mode, band=band, stream=stream.cuda_stream)
-            rm.set_kernel_timing(True)
-            rm.kernel_time()
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
             for _ in range(timed):
                 rm.render_frame(W, H, hits=hits.data_ptr(), rgba=None if rgba is None else rgba.data_ptr(),
                                 stack_mode=args.stack_mode, band=band, stream=stream.cuda_stream)
-            t = rm.stage_times()
-            rm.set_kernel_timing(False)
-            per.append(max(float(np.median(t)) - floor_ms, 1e-6))
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            per.append(e0.elapsed_time(e1) / timed)
         torch.cuda.synchronize(dev)
         out[str(N)] = {"band_kernel_ms_per_rank": [round(x, 4) for x in per], "slowest_rank_ms": round(max(per), 4),
                        "predicted_speedup": round(kern_ms / max(per), 3)}

@@ -19,17 +19,21 @@ import shutil
 import sys
 
 
-def per_kernel(path, name_sub="render_tile_kernel"):
+def per_kernel(path):
+    """Mean counters per launch of the primary-ray kernel: render_seg_kernel (the cost-ordered launch,
+    every launch once an order exists) and render_tile_kernel without the instrumented and the fused
+    shadow-ray instantiations."""
     vals = {}
     with open(path) as fh:
         for r in csv.DictReader(fh):
             name = r["Kernel_Name"]
-            if name_sub not in name:
+            if "render_tile_kernel" not in name and "render_seg_kernel" not in name:
                 continue
             targs = [a.strip() for a in name[name.index("<") + 1:name.index(">")].split(",")]
-            if len(targs) > 1 and targs[1] == "true":   # the instrumented (fetch-counting) launch
+            tile = "render_tile_kernel" in name
+            if tile and len(targs) > 1 and targs[1] == "true":   # the instrumented (fetch-counting) launch
                 continue
-            if len(targs) > 3 and targs[3] == "true":   # the fused shadow-ray launches (c3_plus_shadow_ray)
+            if tile and len(targs) > 3 and targs[3] == "true":   # the fused shadow-ray launches (c3_plus_shadow_ray)
                 continue
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
@@ -52,7 +56,7 @@ def main():
     write_b = write.get("WRITE_SIZE", 0.0) * 1024
     hit, miss = l2.get("TCC_HIT_sum", 0.0), l2.get("TCC_MISS_sum", 0.0)
     summary = {
-        "kernel": "render_tile_kernel (hlsl stack, no fetch counting)",
+        "kernel": "render_seg_kernel / render_tile_kernel (hlsl stack, no fetch counting)",
         "workload": lines[0]["config"]["workload"] if lines else None,
         "fetch_bytes_raw": fetch_b,
         "write_bytes": write_b,
