@@ -185,10 +185,10 @@ def test_beam_band_and_samples(torch, oracle_mod, c3_svo):
 
 
 def test_views_and_held_bursts_without_host_sync(torch, oracle_mod, c3_svo):
-    """Beam starts are double-buffered and splatted on their own stream while the previous render
-    runs (svo_rt.hip launch): a sequence of view changes and held-view bursts submitted with no host
-    synchronisation -- each frame into its own buffers -- must give every frame its own view's
-    records (a splat overwriting a buffer a queued render still reads would not)."""
+    """Beam starts are re-splatted on the launch stream at each view change and reused while the
+    view is held (svo_rt.hip launch): a sequence of view changes and held-view bursts submitted with
+    no host synchronisation -- each frame into its own buffers -- must give every frame its own
+    view's records (a splat racing a queued render that still reads the old bound would not)."""
     from raytracingtest_amd.camera import FLYOVER_EYE, FLYOVER_TARGET
     w, h = 640, 360
     views = []
