@@ -147,6 +147,7 @@ struct Sched {
     unsigned long long stats_view[STATS_RING] = {};
     int stats_mode[STATS_RING] = {};
     int stats_head = 0;                  // the slot the next build writes
+    bool relayout_pending = false;       // a launch ran in an order of another class layout (see launch)
     int lat_cache = 0;                   // the decision of the last completed build ...
     bool lat_short = false;              // ... and whether its heaviest tile's chain was short
     Geo lat_key;                         // ... made at this geometry / view / mode (width -1: none)
@@ -310,6 +311,7 @@ struct svo_ctx {
     uint32_t count_ts_gen = 0;
     double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold ...
     int spread = 1;                  // env SVO_SPREAD=0: a moving camera's order classes tiles by their own costs only
+    int relayout = 1;                // env SVO_RELAYOUT=0: keep an order built from costs of another class layout
     int seg_min_chain = 160;         // env SVO_SEG_MIN_CHAIN: a latency-bound launch whose heaviest tile costs fewer
                                      // trips takes the latency form, unsegmented, without beam starts
     double seg_ratio = 0.28;         // env SVO_SEG_RATIO: ... and the same with beam starts (class table only)
@@ -1094,6 +1096,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             latency_bound = q->lat_key == key && q->lat_mode == mode_now && q->lat_cache;
         }
     }
+    int used_kpack = 0;   // the class layout of the order this launch dispatches in
     if (q) {   // the order this launch dispatches in: with segmented heavy tiles if so decided
         okey = key;
         // a latency-bound launch whose heaviest chain is short (C1, C2: 76 and 111 trips) runs faster in
@@ -1132,6 +1135,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                          n, ctx->view_gen, (int)latency_bound, okey.kpack, use, q->build_at[0], q->build_at[1],
                          (int)(q->build_key[0] == okey), (int)(q->build_key[1] == okey));
         const Geo &bk = use >= 0 ? q->build_key[use] : okey;   // the class layout the order was built with
+        used_kpack = bk.kpack;
         if (p.tile_order && bk.seg) {   // the order lists part entries: the segmented kernel
             p.seg = bk.seg;
             p.seg_kmax = svo::seg_kmax_of(bk.kpack);
@@ -1269,8 +1273,16 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         // pixel offset, a new light or pool, per-launch sample offsets): a held view with nothing
         // else changed records the same costs every launch, so its order stays exact
         const bool drift = q->built_cost != ctx->cost_gen || p.samples != 0 || jittered;
-        refresh = q->order_key != okey || (n % ctx->order_every == 0 && drift) || q->built_mode != mode_now ||
+        // a launch dispatched in an order of another class layout (the first at a new class table)
+        // recorded its costs under that layout: the next build at this table comes from a launch in
+        // its own layout (C3 N = 2 band: 0.059 ms with the first build kept, 0.050 with its own)
+        const bool relayout = ctx->relayout && p.tile_order && (p.seg != okey.seg || (okey.seg && p.seg_kmax != svo::seg_kmax_of(okey.kpack))
+                                               || used_kpack != okey.kpack);
+        if (relayout) q->relayout_pending = true;
+        const bool own_layout = !relayout && q->relayout_pending;
+        refresh = q->order_key != okey || (n % ctx->order_every == 0 && drift) || q->built_mode != mode_now || own_layout ||
                   (q->built_view != ctx->view_gen && (!moving || n - q->last_build >= (unsigned long long)ctx->move_every));
+        if (own_layout) q->relayout_pending = false;
         if (refresh) q->last_build = n;
         moving_build = moving;
     }
@@ -1676,6 +1688,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
     if (const char *k = std::getenv("SVO_SEG_RATIO")) ctx->seg_ratio = std::atof(k);
     if (const char *k = std::getenv("SVO_SPREAD")) ctx->spread = std::atoi(k) != 0;
+    if (const char *k = std::getenv("SVO_RELAYOUT")) ctx->relayout = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SEG_MIN_CHAIN")) ctx->seg_min_chain = std::max(0, std::atoi(k));
     if (const char *k = std::getenv("SVO_BEAM")) ctx->beam = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_BEAM_BACK")) ctx->beam_back = std::max(0, std::atoi(k));
