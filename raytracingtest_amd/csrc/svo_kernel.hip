@@ -735,7 +735,24 @@ __device__ __forceinline__ size_t out_index(const LaunchParams &p, int lr, int g
 // and no per-lane trip bookkeeping.
 // COUNT: per-lane descriptor fetches in r.fetches, with the HLSL re-fetch of a zero descriptor
 // (trace_lean's COUNT form; svo_count_fetches under SVO_OPT_COUNT_BEAM).
-template <int MODE, bool FETCH_ALL, bool SEGS = true, bool COUNT = false>
+// Lanes k of each KG-lane segment group (lanes KG r .. KG r + KG - 1 = ray r) that have a lane
+// j < k of their group in m: an exclusive prefix OR inside the groups, on the wave's lane mask.
+template <int KG>
+__device__ __forceinline__ lmask after_in_group(lmask m) {
+    constexpr lmask NOT0 = KG == 4 ? 0xEEEEEEEEEEEEEEEEull : 0xFEFEFEFEFEFEFEFEull;   // not a group's lane 0
+    m |= (m << 1) & NOT0;
+    m |= (m << 2) & (KG == 4 ? 0xCCCCCCCCCCCCCCCCull : 0xFCFCFCFCFCFCFCFCull);
+    if (KG == 8) m |= (m << 4) & 0xF0F0F0F0F0F0F0F0ull;
+    return (m << 1) & NOT0;
+}
+
+// KG (segmented parts: the group size K): a segment whose group has an earlier segment that ended
+// holding the record (a hit or the cube exit, not a STOP) ends too -- the record is that earlier
+// segment's whatever it would find (the first segment that did not stop), and its trips, stack and
+// state are never read (seg_part: only segments up to the record holder's feed the rebalance and
+// the tile cost).  Saves the walk of the segments past a hit that comes before their stored starts
+// (a jittered sample, a moving camera: the starts are one frame old).
+template <int MODE, bool FETCH_ALL, bool SEGS = true, bool COUNT = false, int KG = 0>
 __device__ __forceinline__ void trace_seg(const LaunchParams &p, FRay &r, uint2 *__restrict__ stk, float t_start,
                                           float t_stop, bool armed0, uint32_t &n_lane, uint32_t &armed_at,
                                           bool &stopped_lane) {
@@ -744,7 +761,7 @@ __device__ __forceinline__ void trace_seg(const LaunchParams &p, FRay &r, uint2 
     for (int s = 0; s < slots; ++s) stk[s * STRIDE] = make_uint2(0u, 0u);
     const int scale_lo = S_MAX - slots;
     lmask act = LM_OF(true);
-    lmask armed = LM_OF(armed0), stopped = 0, cached = 0;
+    lmask armed = LM_OF(armed0), stopped = 0, cached = 0, recs = 0;
     const int oct = r.octant_mask | 16;
     int sh = r.idx ^ oct;
     const uint32_t stk_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2 *)stk;
@@ -862,6 +879,10 @@ __device__ __forceinline__ void trace_seg(const LaunchParams &p, FRay &r, uint2 
             if (SEGS && LM_ON(fin)) n_lane = (uint32_t)it;
             stopped |= stop;                             // STOP before the cube exit of the same trip
             act &= ~fin;
+            if (KG > 1) {                                // the group's later segments: nothing to find
+                recs |= fin & ~stop;
+                act &= ~after_in_group<KG>(recs);
+            }
         }
         asm volatile("s_cmp_lt_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(go) : "s"(it), "n"(MAX_ITERS), "s"(act) : "scc");
     } while (go != 0);
@@ -1147,14 +1168,14 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
     // the pixel's starts at fractions e / 8 of its trace (8 floats: e = 1..7 + spare); segment k of
     // K runs from fraction k / K to (k + 1) / K
     const size_t hi = (size_t)lr * (size_t)p.width + (size_t)x;
-    float *hint8 = reinterpret_cast<float *>(p.seg_hint + 2 * hi);
+    float *hint8 = p.seg_hint ? reinterpret_cast<float *>(p.seg_hint + 2 * hi) : nullptr;   // null: even splits
     const int e0 = k * (SEG_KMAX / K), e1 = e0 + SEG_KMAX / K;   // 0 and 8: none
-    const bool have = hint8[0] == hint8[0];                        // NaN: none yet
+    const bool have = hint8 && hint8[0] == hint8[0];               // NaN: none yet
     const float t_start = seg_start(p, hint8, have, hi, e0, t_entry, t_exit);
     const float t_stop = seg_start(p, hint8, have, hi, e1, t_entry, t_exit);
     uint32_t n_lane, armed_at;
     bool stopped;
-    trace_seg<MODE, FA>(p, f, stk, k == 0 ? bs : t_start, t_stop, k == 0 && r.t_min >= bs, n_lane, armed_at,
+    trace_seg<MODE, FA, true, false, K>(p, f, stk, k == 0 ? bs : t_start, t_stop, k == 0 && r.t_min >= bs, n_lane, armed_at,
                         stopped);
     from_fray(f, r);
     // the record holder: the first segment that did not stop (the last one never stops)
@@ -1166,7 +1187,7 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
     tot += (uint32_t)__shfl_xor((int)tot, 1);
     tot += (uint32_t)__shfl_xor((int)tot, 2);
     if (K == 8) tot += (uint32_t)__shfl_xor((int)tot, 4);
-    seg_rebalance(stk_base, t_entry, t_start, t_end, c, fsel, K, (float)tot, hint8, inside);
+    seg_rebalance(stk_base, t_entry, t_start, t_end, c, fsel, K, (float)tot, hint8, inside && hint8);
     if (p.tile_cost) {
         uint32_t m = inside ? tot : 0u;
         for (int d = K; d < TILE; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));

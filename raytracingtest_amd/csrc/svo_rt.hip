@@ -310,6 +310,14 @@ struct svo_ctx {
     size_t count_ts_cap = 0;
     uint32_t count_ts_gen = 0;
     double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold ...
+    // the stored segment starts are those of the pixel's ray in the previous launch: of another
+    // sub-pixel ray after a jittered launch, of another view while the camera moves.  Such a launch
+    // splits its segments evenly from the beam start instead (segments past an earlier segment's
+    // record end early; trace_seg): C3 one-sample route 94.6 against 97.9 us (overview 84.3 / 88.8),
+    // a slow pan 91.2 / 93.0 us (profiles/r05_stale_starts.txt).  1: the stored starts, 0 (jittered
+    // launches only): no segments
+    int seg_move = 2;                // env SVO_SEG_MOVE: a launch at a new view
+    int seg_jitter = 2;              // env SVO_SEG_JITTER: a jittered launch (the one-sample samples route)
     int spread = 1;                  // env SVO_SPREAD=0: a moving camera's order classes tiles by their own costs only
     int relayout = 1;                // env SVO_RELAYOUT=0: keep an order built from costs of another class layout
     int seg_min_chain = 160;         // env SVO_SEG_MIN_CHAIN: a latency-bound launch whose heaviest tile costs fewer
@@ -1102,7 +1110,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         // a latency-bound launch whose heaviest chain is short (C1, C2: 76 and 111 trips) runs faster in
         // the latency form without segments or beam starts (C2 0.041 against 0.047 ms, C1 0.025 / 0.031)
         const bool short_chains = latency_bound && !ctx->seg_all && q->lat_short;
-        okey.kpack = ctx->seg_all ? ctx->seg_all * 0x111111 : short_chains ? 0
+        okey.kpack = ctx->seg_all ? ctx->seg_all * 0x111111 : short_chains || (jittered && ctx->seg_jitter == 0) ? 0
                    : latency_bound ? ctx->seg_kpack_lat : ctx->seg_kpack_issue;
         okey.seg = seg_cap && okey.kpack ? seg_cap : 0;
         if (!okey.seg) okey.kpack = 0;
@@ -1139,7 +1147,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         if (p.tile_order && bk.seg) {   // the order lists part entries: the segmented kernel
             p.seg = bk.seg;
             p.seg_kmax = svo::seg_kmax_of(bk.kpack);
-            p.seg_hint = q->seg_hint;
+            const bool even = (jittered && ctx->seg_jitter == 2) || (q->view_prev != ctx->view_gen && ctx->seg_move == 2);
+            p.seg_hint = even ? nullptr : q->seg_hint;
             if (ctx->seg_scramble) p.seg_scramble = ctx->seg_scramble * 0x9E3779B9u + ++ctx->seg_launches;
         }
     }
@@ -1687,6 +1696,8 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     if (const char *k = std::getenv("SVO_SEG_SCRAMBLE")) ctx->seg_scramble = (uint32_t)std::strtoul(k, nullptr, 10);
     if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
     if (const char *k = std::getenv("SVO_SEG_RATIO")) ctx->seg_ratio = std::atof(k);
+    if (const char *k = std::getenv("SVO_SEG_JITTER")) ctx->seg_jitter = std::atoi(k);
+    if (const char *k = std::getenv("SVO_SEG_MOVE")) ctx->seg_move = std::atoi(k);
     if (const char *k = std::getenv("SVO_SPREAD")) ctx->spread = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_RELAYOUT")) ctx->relayout = std::atoi(k) != 0;
     if (const char *k = std::getenv("SVO_SEG_MIN_CHAIN")) ctx->seg_min_chain = std::max(0, std::atoi(k));

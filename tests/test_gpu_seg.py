@@ -82,10 +82,13 @@ def test_c3_heavy_tiles_segmented_full_frame(torch, oracle_mod, monkeypatch, c3_
     _frames(torch, oracle_mod, c3_svo, [CAMERAS["flyover"]()], w, h, mode, n_frames=6, keys=("hits", "rgba"))
 
 
-def test_c3_segmented_moving_camera(torch, oracle_mod, monkeypatch, c3_svo):
-    """A pan (a new view per frame, starts carried over from the previous view), then held."""
+@pytest.mark.parametrize("seg_move", ["1", "2"])
+def test_c3_segmented_moving_camera(torch, oracle_mod, monkeypatch, c3_svo, seg_move):
+    """A pan (a new view per frame: even splits by default, under SVO_SEG_MOVE=1 the starts carried
+    over from the previous view), then held."""
     monkeypatch.setenv("SVO_SEG_ISSUE", "488")
     monkeypatch.setenv("SVO_MOVE_EVERY", "1")
+    monkeypatch.setenv("SVO_SEG_MOVE", seg_move)
     from raytracingtest_amd.camera import FLYOVER_EYE, FLYOVER_TARGET
     w, h = 1920, 1080
     cams = []
@@ -94,6 +97,34 @@ def test_c3_segmented_moving_camera(torch, oracle_mod, monkeypatch, c3_svo):
         eye = (FLYOVER_EYE[0] + 2.0 * np.sin(a), FLYOVER_EYE[1], FLYOVER_EYE[2] + 2.0 * (1.0 - np.cos(a)))
         cams.append(overview_camera(eye, FLYOVER_TARGET))
     _frames(torch, oracle_mod, c3_svo, cams, w, h, 0, n_frames=2, keys=("hits", "rgba"))
+
+
+@pytest.mark.parametrize("jit", ["1", "2"])
+def test_c3_segmented_jittered_one_sample_launches(torch, oracle_mod, monkeypatch, c3_svo, jit):
+    """svo_render_samples one sample per launch (the one-sample route: the render launch with the
+    blend in its store epilogue), a new jittered offset every launch, on the C3 frame whose heavy
+    tiles are segmented once the order exists -- from even splits (the default), or under
+    SVO_SEG_JITTER=1 from the starts another sub-pixel ray stored, with the segments past an earlier segment's record
+    ended early: the accumulation equals the oracle's renders + orc_accumulate, bit for bit."""
+    from raytracingtest_amd.camera import jitter_offsets
+    from test_gpu_frame import _oracle_accumulated
+    monkeypatch.setenv("SVO_SEG_JITTER", jit)
+    w, h = 1920, 1080
+    cam = CAMERAS["flyover"]()
+    offs = jitter_offsets(6)
+    want = _oracle_accumulated(oracle_mod, c3_svo, cam, w, h, offs)
+    m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+    try:
+        m.SetSVOBuffer(c3_svo)
+        m.UpdateShaderParameters(cam, w, h)
+        acc = torch.zeros((w * h * 4,), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        for k in range(len(offs)):
+            m.render_samples(w, h, offs[k:k + 1], k, acc.data_ptr())
+        m.synchronize()
+        assert acc.cpu().numpy().tobytes() == want.astype(np.float32).tobytes(), "accumulation differs"
+    finally:
+        m.close()
 
 
 @pytest.mark.parametrize("mode,k", [(0, 4), (1, 4), (0, 8)])
