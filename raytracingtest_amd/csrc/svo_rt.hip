@@ -150,6 +150,7 @@ struct Sched {
     bool relayout_pending = false;       // a launch ran in an order of another class layout (see launch)
     int lat_cache = 0;                   // the decision of the last completed build ...
     bool lat_short = false;              // ... and whether its heaviest tile's chain was short
+    bool lat_thin = false;               // ... and whether its work was thin against that chain (SVO_SEG_THIN)
     Geo lat_key;                         // ... made at this geometry / view / mode (width -1: none)
     unsigned long long lat_view = 0;
     int lat_mode = -1;
@@ -296,6 +297,11 @@ struct svo_ctx {
     int seg_kpack_lat = 0x444;       // env SVO_SEG_LAT=<hex>: the K of each cost class (nibble c: class c, >= 7/8,
                                      // 3/4, 1/2, 1/4, 1/8 of the max, rest; 0 none, 4 or 8) in a latency-bound launch
     int seg_kpack_issue = 0x4;       // env SVO_SEG_ISSUE=<hex>: the same in an issue-bound launch
+    int seg_kpack_thin = 0x888;      // env SVO_SEG_THIN=<hex>: ... and in a latency-bound launch whose summed trips
+    double thin_ratio = 0.083;       // are below SVO_SEG_THIN_RATIO x slots x its heaviest tile's: C3 8-way bands
+                                     // (flyover 0.045, Main.unity 0.079) and the overview frame (0.063) run faster
+                                     // with every heavy class in eighths, the flyover 4-way band (0.087) with 444
+                                     // (profiles/r05_thin_ab.json)
     int seg_cap = 96;                // env SVO_SEG_CAP: at most this many segmented tiles per XCD
     int seg_all = 0;                 // env SVO_SEG_ALL=4|8 (tests; 1 = 4): every tile segmented with that K
     uint32_t seg_scramble = 0;       // env SVO_SEG_SCRAMBLE=<seed> (tests): arbitrary segment starts
@@ -1092,12 +1098,17 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                     const double bound = !prior ? ratio : q->lat_cache ? ratio * 1.15 : ratio / 1.15;
                     q->lat_cache = m > 0 && (double)t < bound * slots * (double)m ? 1 : 0;
                     q->lat_short = m < (uint32_t)ctx->seg_min_chain;
+                    // far fewer summed trips than resident slots x the heaviest chain (a band of an 8-way
+                    // split): the chain alone bounds the launch and eight segments shorten it most
+                    const double thin = !prior ? ctx->thin_ratio : q->lat_thin ? ctx->thin_ratio * 1.15 : ctx->thin_ratio / 1.15;
+                    q->lat_thin = q->lat_cache && (double)t < thin * slots * (double)m;
                     q->lat_key = q->stats_key[r];
                     q->lat_view = q->stats_view[r];
                     q->lat_mode = q->stats_mode[r];
                     if (std::getenv("SVO_LAT_DEBUG"))   // diagnostics: the decision and its inputs
-                        std::fprintf(stderr, "svo lat: view %llu T %llu M %u slots %.0f -> %s\n", q->lat_view,
-                                     (unsigned long long)t, m, slots, q->lat_cache ? "latency" : "lean");
+                        std::fprintf(stderr, "svo lat: view %llu T %llu M %u slots %.0f ratio %.4f -> %s%s\n", q->lat_view,
+                                     (unsigned long long)t, m, slots, m ? (double)t / (slots * (double)m) : 0.0,
+                                     q->lat_cache ? "latency" : "lean", q->lat_thin ? " thin" : "");
                 }
                 break;
             }
@@ -1111,7 +1122,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         // the latency form without segments or beam starts (C2 0.041 against 0.047 ms, C1 0.025 / 0.031)
         const bool short_chains = latency_bound && !ctx->seg_all && q->lat_short;
         okey.kpack = ctx->seg_all ? ctx->seg_all * 0x111111 : short_chains || (jittered && ctx->seg_jitter == 0) ? 0
-                   : latency_bound ? ctx->seg_kpack_lat : ctx->seg_kpack_issue;
+                   : latency_bound ? (q->lat_thin ? ctx->seg_kpack_thin : ctx->seg_kpack_lat) : ctx->seg_kpack_issue;
         okey.seg = seg_cap && okey.kpack ? seg_cap : 0;
         if (!okey.seg) okey.kpack = 0;
         // the newest build it follows by >= 2 launches (Sched): a build that launch n - 2 was
@@ -1691,6 +1702,8 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     };
     ctx->seg_kpack_lat = kpack_env("SVO_SEG_LAT", ctx->seg_kpack_lat);
     ctx->seg_kpack_issue = kpack_env("SVO_SEG_ISSUE", ctx->seg_kpack_issue);
+    ctx->seg_kpack_thin = kpack_env("SVO_SEG_THIN", ctx->seg_kpack_thin);
+    if (const char *k = std::getenv("SVO_SEG_THIN_RATIO")) ctx->thin_ratio = std::atof(k);
     if (const char *k = std::getenv("SVO_SEG_CAP")) ctx->seg_cap = std::max(1, std::atoi(k));
     if (const char *k = std::getenv("SVO_SEG_ALL")) ctx->seg_all = std::atoi(k) == 8 ? 8 : std::atoi(k) != 0 ? 4 : 0;
     if (const char *k = std::getenv("SVO_SEG_SCRAMBLE")) ctx->seg_scramble = (uint32_t)std::strtoul(k, nullptr, 10);

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--variants", default="off,auto",
                     help="comma list of: off (SVO_SEG=0), auto (the library's defaults), or '+'-joined "
-                         "l<hex> (SVO_SEG_LAT: K per cost class, class 0 in the low nibble), i<hex> (SVO_SEG_ISSUE) "
+                         "l<hex> (SVO_SEG_LAT: K per cost class, class 0 in the low nibble), i<hex> (SVO_SEG_ISSUE), t<hex> (SVO_SEG_THIN), "
                          "nobeam (SVO_BEAM=0) and norelayout (SVO_RELAYOUT=0)")
     ap.add_argument("--cap", default=None, help="SVO_SEG_CAP")
     ap.add_argument("--cameras", default=None, help="comma list (default: --camera)")
@@ -45,7 +45,7 @@ def main():
     cams = (a.cameras or a.camera).split(",")
     for rnd in range(a.rounds):
         for name in a.variants.split(","):
-            for k in ("SVO_SEG", "SVO_SEG_LAT", "SVO_SEG_ISSUE", "SVO_SEG_CAP", "SVO_BEAM", "SVO_RELAYOUT"):
+            for k in ("SVO_SEG", "SVO_SEG_LAT", "SVO_SEG_ISSUE", "SVO_SEG_CAP", "SVO_BEAM", "SVO_RELAYOUT", "SVO_SEG_THIN"):
                 os.environ.pop(k, None)
             for part in name.split("+"):
                 if part == "off":
@@ -54,6 +54,8 @@ def main():
                     os.environ["SVO_SEG_LAT"] = part[1:]
                 elif part.startswith("i"):     # i<hex>: SVO_SEG_ISSUE, the same for issue-bound launches
                     os.environ["SVO_SEG_ISSUE"] = part[1:]
+                elif part.startswith("t"):     # t<hex>: SVO_SEG_THIN, the table of thin latency-bound launches
+                    os.environ["SVO_SEG_THIN"] = part[1:]
                 elif part == "nobeam":         # SVO_BEAM=0: rays from the cube entry
                     os.environ["SVO_BEAM"] = "0"
                 elif part == "norelayout":     # SVO_RELAYOUT=0: keep the first order built at a new class table
