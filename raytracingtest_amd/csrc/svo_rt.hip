@@ -1099,9 +1099,11 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                     q->lat_cache = m > 0 && (double)t < bound * slots * (double)m ? 1 : 0;
                     q->lat_short = m < (uint32_t)ctx->seg_min_chain;
                     // far fewer summed trips than resident slots x the heaviest chain (a band of an 8-way
-                    // split): the chain alone bounds the launch and eight segments shorten it most
-                    const double thin = !prior ? ctx->thin_ratio : q->lat_thin ? ctx->thin_ratio * 1.15 : ctx->thin_ratio / 1.15;
-                    q->lat_thin = q->lat_cache && (double)t < thin * slots * (double)m;
+                    // split): the chain alone bounds the launch and eight segments shorten it most.  No
+                    // hysteresis: the second build at a new geometry reads costs of the fallback order's
+                    // layout (C3 Main.unity 8-way band: 0.118 once, 0.079 from then on), and a sticky
+                    // decision would keep that transient (0.0417 ms against 0.0378 with eighths)
+                    q->lat_thin = q->lat_cache && (double)t < ctx->thin_ratio * slots * (double)m;
                     q->lat_key = q->stats_key[r];
                     q->lat_view = q->stats_view[r];
                     q->lat_mode = q->stats_mode[r];
