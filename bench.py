@@ -362,8 +362,9 @@ def main():
                          "gpu_span_ms_per_step": round(m["span_ms"], 4),
                          "kernel_ms_le_step": bool(kern_ms <= ms_per_step),
                          "kernel": "render_seg_kernel / render_tile_kernel (the primary-ray launch). N = 1: kernel_ms = "
-                                   "the timed region's GPU span per step (one HIP event pair around the K launches on "
-                                   "their stream; they run back to back and nothing else runs there at a held view); "
+                                   "the timed region's GPU span per launch (one HIP event pair around launches 2..K on "
+                                   "their stream, from the end of the first so the host's first-launch latency is not "
+                                   "in it; they run back to back and nothing else runs there at a held view); "
                                    "kernel_ms_events: library events around each launch (K more steps), which add the "
                                    "bracket's marker processing; N > 1: kernel_ms = kernel_ms_events - event_floor_ms",
                          "bound_note": "dependent node-fetch chain at 8 waves/SIMD (DESIGN.md 5.1); frac is the "
@@ -494,17 +495,23 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     step_events = os.environ.get("SVO_STEP_EVENTS", "0") != "0"
-    # one event pair around the whole timed region on the launch stream: with one GPU the K launches
-    # run back to back, so its span / K is the render kernel's mean duration with no per-launch
-    # bracket (a bracket around each launch adds ~5 us of marker processing to what it times)
+    # one event pair on the launch stream around launches 2..K of the timed region: with one GPU they
+    # run back to back, so the span / (K - 1) is the render kernel's mean duration with no per-launch
+    # bracket (a bracket around each launch adds ~5 us of marker processing to what it times).  The
+    # pair starts at the end of the first launch: the GPU idles from the synchronize until the host's
+    # first launch arrives (~140 us under rocprofv3), which would otherwise be spread over the K steps
     span0, span1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    span0.record(stream)
+    span_n = args.steps - 1 if args.steps > 1 else 1
+    if args.steps == 1:
+        span0.record(stream)
     for i in range(args.steps):
         if step_events:
             ev[i][0].record(stream)
         step()
         if step_events:
             ev[i][1].record(stream)
+        if i == 0 and args.steps > 1:
+            span0.record(stream)
     span1.record(stream)
     drain()   # the last frame's assemble (each step assembles the previous frame)
     torch.cuda.synchronize(dev)
@@ -531,7 +538,7 @@ def measure_frame(args, rm, W, H, rank, world, dev, stream, dist):
     # it belongs to): the same two hipEventRecords around a one-element kernel on the same stream
     floor_ms = event_floor_ms(stream, dev)
     kern_ms_bracket = max(kern_ms_events - floor_ms, 1e-6)
-    span_ms = span0.elapsed_time(span1) / args.steps
+    span_ms = span0.elapsed_time(span1) / span_n
     # N = 1: the timed region's GPU span per launch (only the render kernel runs on the stream at a
     # held view: the beam splat and the order builds happened in the warmup); N > 1: the bracketed
     # kernel (the steps also hold the gather)
