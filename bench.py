@@ -107,7 +107,14 @@ def parse():
                    help="N = 1: skip the figures reported beside value (other camera poses, frames in flight, "
                         "host path); profiling runs use it so every render_tile_kernel launch is the value's "
                         "workload, one frame at a time")
+    p.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
+                   help="svo_config field for the context (include/svo_rt.h; A/B runs): the policy only, every "
+                        "setting renders the same frames")
     a = p.parse_args()
+    a.svo_config = {}
+    for kv in a.set:
+        k, v = kv.split("=", 1)
+        a.svo_config[k] = float(v) if "." in v else int(v, 0)
     cfg = CONFIGS[a.config]
     for k in ("width", "height", "max_level", "sampler", "camera", "stack_mode"):
         if getattr(a, k) is None:
@@ -211,7 +218,7 @@ def main():
     if mode == "multidevice":
         return bench_multidevice(args, svo, cam, W, H, scaling, build_s)
 
-    rm = RaytracingMaster(device=dev.index, capacity_nodes=n_nodes)
+    rm = RaytracingMaster(device=dev.index, capacity_nodes=n_nodes, config=args.svo_config)
     rm.SetSVOBuffer(svo)
     rm.UpdateShaderParameters(cam, W, H)
     if args.shadows:
@@ -305,6 +312,9 @@ def main():
                if world == 1 and args.steps > 0 and args.extras and not args.shadows else None)
     split = (strong_split_bands(rm, W, H, args, dev, stream, hits, rgba, kern_ms, m["floor_ms"])
              if world == 1 and args.steps > 0 and args.extras and not args.shadows else None)
+    dropin = pan = None
+    if world == 1 and args.steps > 0 and args.extras and not args.shadows:
+        dropin, pan = dropin_loop_rates(rm, W, H, args, dev, stream)
     poses = None
     if world == 1 and args.extras and args.svo != "menger":
         poses = extra_poses(rm, args, W, H, hits, rgba, sptr, dev)
@@ -341,7 +351,7 @@ def main():
             "dtype": "f32",
             "data": ("synthetic: 256^3 Menger sponge surface SVO (SURVEY.md 8(d) C2)" if args.svo == "menger" else
                      "synthetic: Custom1 OpenSimplex(seed 7) terrain SVO built on-GPU by the NaiveCreator restatement"),
-            "config": {"workload": workload,
+            "config": {"workload": workload, "svo_config": args.svo_config or "defaults",
                        "svo_nodes": n_nodes, "svo_format": "V%d" % svo.format, "svo_leaves": getattr(svo, "n_leaves", None),
                        "build_s": round(build_s, 2), "stack_mode": "hlsl" if args.stack_mode == 0 else "exact",
                        "svo_replica": None if world == 1 else ("rccl_broadcast_from_rank0" if args.replica == "broadcast"
@@ -422,6 +432,9 @@ def main():
                 "note": "value overlaps the gather of frame k with the render of frame k+1; render_only_Mrays is "
                         "the frame's rays over the slowest rank's render kernel alone; gather/assemble from a "
                         "serialized pass (events on the gather stream)"}
+        if dropin:
+            out["dropin_loop"] = dropin
+            out["pan"] = pan
         if poses:
             out["extra_poses"] = poses
         if host_path:
@@ -1167,7 +1180,7 @@ def bench_multidevice(args, svo, cam, W, H, scaling, build_s):
     from raytracingtest_amd import RaytracingMaster, _lib
     from raytracingtest_amd import distributed as D
     n = args.gpus
-    rm = RaytracingMaster(devices=args.device_list, capacity_nodes=len(svo))
+    rm = RaytracingMaster(devices=args.device_list, capacity_nodes=len(svo), config=args.svo_config)
     rm.SetSVOBuffer(svo)
     dev0 = torch.device("cuda", args.device_list[0])
     s = torch.cuda.Stream(dev0)
@@ -1494,6 +1507,120 @@ def host_path_rates(rm, W, H, args, n=5):
         out[name]["note"] = ("each call returns the previous frame's pinned pixels (D2H overlapping the next "
                              "render); the caller's own copy of them is not included")
     return out
+
+
+def dropin_loop_rates(rm, W, H, args, dev, stream, frames=300):
+    """The drop-in's own frame loop, measured beside `value` (which repeats one
+    frame at pixel offset (0.5, 0.5)).  RaytracingMaster.OnRenderImage draws a fresh
+    _PixelOffset = (Random.value, Random.value) every frame (RaytracingMaster.cs:35), blends the
+    sample in with _Sample = _currentSample (:70-73) and restarts the blend whenever the camera moves
+    (:44-47); the C# shim does the same through svo_render_progressive_async (RGB24).  Three loops:
+      fixed   -- held view, offset (0.5, 0.5) every frame (value's ray set);
+      jitter  -- held view, a new seeded offset every frame (the `dropin_loop` key);
+      pan     -- a new view AND a new offset every frame, _currentSample 0 each time (the `pan` key;
+                 camera.pan_cameras: the pose's eye circling by 2 mrad per frame).
+    Each loop is timed twice: (1) the plugin's pipelined progressive entry point on the host clock
+    (render + AddShader blend + RGB24 pack + D2H of the previous frame into pinned memory, the call
+    the shim makes per frame) and, with the library's per-launch events, its render kernel; (2) the
+    render alone through svo_render_device on the bench stream with value's outputs (hit record +
+    RGBA32F), its GPU span per frame over launches 2..K exactly as value's kernel_ms (the beam splat of
+    a new view runs on that stream and is in the pan's span; the order builds run beside it)."""
+    import torch
+    from raytracingtest_amd import _lib
+    from raytracingtest_amd.camera import column_major, jitter_offsets, main_light, pan_cameras
+    L = _lib.lib()
+    offs = jitter_offsets(frames + 64)
+    light = np.ascontiguousarray(main_light(), np.float32)
+    cams = pan_cameras(args.camera, frames + 64)
+    views = []
+    for c in cams:
+        c2w, ip = c.uniforms(W, H)
+        views.append((column_major(c2w), column_major(ip)))
+    hits = torch.empty(W * H * 24, dtype=torch.uint8, device=dev)
+    rgba = torch.empty(W * H * 4, dtype=torch.float32, device=dev)
+    sptr = stream.cuda_stream
+
+    def set_cam(kind, k):
+        c, p = views[k if kind == "pan" else 0]
+        ox, oy = (0.5, 0.5) if kind == "fixed" else (float(offs[k, 0]), float(offs[k, 1]))
+        _lib.check(L.svo_set_camera(rm._ctx, c.ctypes.data, p.ctypes.data, ox, oy, light.ctypes.data), "svo_set_camera")
+
+    ptr = ctypes.c_void_p()
+    state = {"sample": 0}
+
+    def progressive(kind, k):
+        set_cam(kind, k)
+        s = 0 if kind == "pan" else state["sample"]
+        _lib.check(L.svo_render_progressive_async(rm._ctx, W, H, args.stack_mode, s, _lib.PIXELS_RGB8,
+                                                  ctypes.byref(ptr)), "svo_render_progressive_async")
+        state["sample"] = s + 1
+
+    def device(kind, k):
+        set_cam(kind, k)
+        rm.render_device(W, H, rgba_ptr=rgba.data_ptr(), hits_ptr=hits.data_ptr(), stack_mode=args.stack_mode,
+                         stream=sptr)
+
+    out = {}
+    for kind in ("fixed", "jitter", "pan"):
+        state["sample"] = 0
+        r = {}
+        # (1) the pipelined drop-in call, host clock; then its render kernel by the library's events
+        for k in range(30):
+            progressive(kind, k)
+        _lib.check(L.svo_progressive_last(rm._ctx, ctypes.byref(ptr)), "svo_progressive_last")
+        t = time.perf_counter()
+        for k in range(frames):
+            progressive(kind, k)
+        _lib.check(L.svo_progressive_last(rm._ctx, ctypes.byref(ptr)), "svo_progressive_last")
+        ms = (time.perf_counter() - t) / frames * 1e3
+        rm.set_kernel_timing(True)
+        rm.kernel_time()
+        for k in range(frames):
+            progressive(kind, k)
+        kev, n = rm.kernel_time()
+        rm.set_kernel_timing(False)
+        _lib.check(L.svo_progressive_last(rm._ctx, ctypes.byref(ptr)), "svo_progressive_last")
+        r["progressive_async_rgb24"] = {"ms_per_frame": round(ms, 4), "Mrays_per_s": round(W * H / (ms * 1e-3) / 1e6, 1),
+                                        "kernel_ms_events": round(kev, 4)}
+        # (2) the render alone, value's method
+        for k in range(30):
+            device(kind, k)
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for k in range(frames):
+            device(kind, k)
+            if k == 0:
+                e0.record(stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t) / frames * 1e3
+        span = e0.elapsed_time(e1) / (frames - 1)
+        r["render_device"] = {"ms_per_frame": round(ms, 4), "kernel_ms": round(span, 4),
+                              "Mrays_per_s": round(W * H / (span * 1e-3) / 1e6, 1)}
+        out[kind] = r
+    # leave the context at the bench pose, offset (0.5, 0.5)
+    set_cam("fixed", 0)
+    f, j, p = out["fixed"], out["jitter"], out["pan"]
+    ratio = lambda a, b: round(a / b, 4)   # noqa: E731
+    dropin = {"frames": frames, "fixed_offset": f, "jittered": j,
+              "kernel_vs_fixed_offset": ratio(j["render_device"]["kernel_ms"], f["render_device"]["kernel_ms"]),
+              "kernel_events_vs_fixed_offset": ratio(j["progressive_async_rgb24"]["kernel_ms_events"],
+                                                     f["progressive_async_rgb24"]["kernel_ms_events"]),
+              "Mrays_per_s": j["render_device"]["Mrays_per_s"],
+              "note": "svo_render_progressive_async RGB24 (the C# shim's per-frame call) with a new seeded "
+                      "_PixelOffset per frame at a held view; kernel_ms = render_device span per frame under the "
+                      "same jitter (value's method); fixed_offset = the same loops at (0.5, 0.5)"}
+    pan = {"frames": frames, "moving": p,
+           "frame_vs_held": ratio(p["render_device"]["ms_per_frame"], j["render_device"]["ms_per_frame"]),
+           "kernel_vs_held": ratio(p["render_device"]["kernel_ms"], j["render_device"]["kernel_ms"]),
+           "progressive_frame_vs_held": ratio(p["progressive_async_rgb24"]["ms_per_frame"],
+                                              j["progressive_async_rgb24"]["ms_per_frame"]),
+           "Mrays_per_s": p["render_device"]["Mrays_per_s"],
+           "note": "the same loops with a new view every frame (eye circling the pose by 2 mrad per frame, "
+                   "camera.pan_cameras) and _currentSample reset each frame; *_vs_held against the jittered "
+                   "held view (dropin_loop)"}
+    return dropin, pan
 
 
 def extra_poses(rm, args, W, H, hits, rgba, sptr, dev):

@@ -15,10 +15,16 @@
  *  - one context is driven from one host thread at a time; its asynchronous
  *    entry points take any hipStream_t, and renders on different streams run
  *    concurrently (per-stream dispatch-order state).
- *  - a caller stream handed to a context stays alive until svo_forget_stream,
- *    svo_synchronize or svo_destroy of that context: the context may later
- *    record an event on it (when a fifth stream takes its dispatch-order state
- *    over, or another stream takes the host-path scratch).
+ *  - a caller stream handed to a context may be destroyed after
+ *    svo_forget_stream(ctx, stream), svo_synchronize(ctx) or svo_destroy(ctx):
+ *    until one of them, the context may record an event on it (when a fifth
+ *    stream takes its dispatch-order state over, or another stream takes the
+ *    host-path scratch).  After svo_synchronize no work is pending anywhere, so
+ *    the context records nothing on a stream it saw before that call.
+ *  - policy (dispatch order, loop form, segmented rays, beam starts, shadow and
+ *    readback forms) is one svo_config per context, svo_set_config; no
+ *    environment variable changes what the library computes or how (four
+ *    diagnostic switches only add traces and timing aids: INTEGRATION.md).
  */
 #ifndef SVO_RT_H
 #define SVO_RT_H
@@ -102,6 +108,61 @@ typedef struct svo_frame {
     int layout;
 } svo_frame;
 
+/* Render policy of a context (ABI 10) -- the plugin's counterpart of RaytracingMaster's
+ * Inspector fields (RaytracingMaster.cs:16-18): every switch that chooses HOW a frame is
+ * traced.  None changes a result: every combination renders bit-identical frames (the GPU
+ * suite runs the oracle comparison under each); they move only time.  Versioned by size: a
+ * caller sets `size` = sizeof(svo_config) as it was compiled, svo_set_config reads the fields
+ * that fit in it and keeps the context's values of any later ones, svo_get_config writes at
+ * most `size` bytes.  svo_get_config(NULL, cfg) gives the defaults below.  Hex tables: one
+ * nibble per cost class (lowest = heaviest: >= 7/8, 3/4, 1/2, 1/4, 1/8 of the heaviest tile,
+ * rest), each 0 (whole tiles), 4 or 8 (t-segments per ray). */
+#define SVO_CONFIG_VERSION 1
+typedef struct svo_config {
+    uint32_t size;               /* sizeof(svo_config) as compiled by the caller */
+    uint32_t version;            /* SVO_CONFIG_VERSION (written by svo_get_config) */
+    /* dispatch order */
+    int32_t  tile_order;         /* 1: heaviest cost class first, from earlier launches' tile costs; 0: strip order */
+    int32_t  xcd_strips;         /* 1: tile columns dealt to the 8 XCDs in interleaved strips; 0: raster */
+    int32_t  issue_priority;     /* 1: s_setprio 3/2/1 by cost class */
+    int32_t  order_every;        /* >= 1: rebuild the order every k-th launch while costs drift (32) */
+    int32_t  move_every;         /* >= 1: while the camera moves, rebuild every k-th launch (4) */
+    int32_t  move_spread;        /* 1: a moving camera's order classes a tile by its 3x3 neighbourhood (1) */
+    int32_t  relayout;           /* 1: rebuild once in a new class table's own layout (1) */
+    int32_t  fetch_all;          /* -1: by pool size (< 2^24 nodes: 1); 0: fetch on a changed node; 1: every trip */
+    /* loop form */
+    int32_t  loop_form;          /* -1: by the last order build's statistics; 0: lean; 1: latency form */
+    float    lat_ratio;          /* latency-bound when summed trips < ratio x resident waves x heaviest (0.3) */
+    /* segmented rays */
+    int32_t  segments;           /* 1: heavy tiles traced as t-segments by the class tables; 0: never */
+    uint32_t seg_table_latency;  /* class table of a latency-bound launch (0x444) */
+    uint32_t seg_table_issue;    /* ... of an issue-bound launch (0x4) */
+    uint32_t seg_table_thin;     /* ... of a latency-bound launch below seg_thin_ratio (0x888) */
+    float    seg_ratio;          /* the latency-bound boundary with beam starts (0.28) */
+    float    seg_thin_ratio;     /* the thin boundary (0.083) */
+    int32_t  seg_cap;            /* >= 1: segmented tiles per XCD at most (96) */
+    int32_t  seg_min_chain;      /* a latency-bound launch whose heaviest tile has fewer trips: no segments (160) */
+    int32_t  seg_move;           /* starts after a camera move: 1 the stored ones, 2 even split (2) */
+    int32_t  seg_jitter;         /* ... in a jittered launch: 0 no segments, 1 stored, 2 even split (2) */
+    int32_t  seg_all;            /* tests: 0 off, 4 or 8 = every tile segmented with that K */
+    uint32_t seg_scramble;       /* tests: != 0 replaces every start by a hash (unordered, NaN, +-inf) */
+    /* beam starts */
+    int32_t  beam;               /* 1: primary rays start at their tile's splatted lower bound of the hit t */
+    int32_t  beam_back;          /* >= 0: splat the boxes this many levels above the leaves (2) */
+    /* shadow rays (SVO_OPT_SHADOW_RAYS) */
+    int32_t  shadow_form;        /* 0: fused into the primary launch; 1: second pass over tiles; 2: over the
+                                    compacted hit list */
+    int32_t  shadow_order;       /* 1: the two-pass form's tiles in their own cost order */
+    /* host paths */
+    int32_t  readback;           /* svo_render_progressive_async copy: 0 one DMA, 1 kernel push, 2 two DMAs */
+    int32_t  host_copy_threads;  /* svo_render's host copy threads (0: half the hardware threads, <= 16) */
+    /* multi-device contexts (svo_create_multi) */
+    int32_t  sparse_payload;     /* 1: display-only frames travel as sparse hit payloads */
+    int32_t  peer_copy;          /* 1: every member's payload copied instead of pulled over xGMI (tests) */
+} svo_config;
+int svo_get_config(svo_ctx *ctx, svo_config *cfg);
+int svo_set_config(svo_ctx *ctx, const svo_config *cfg);
+
 /* ~ RaytracingMaster.InitializeSVOBuffer (RaytracingMaster.cs:111-116):
  * allocate a node pool of `capacity_nodes` descriptors (+2 attachment words
  * each) on HIP device `device`. */
@@ -118,7 +179,7 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out);
  * dispatches one grid over the whole frame (RaytracingMaster.cs:66-68).
  * Payload transport per member (svo_get_member_link): the display device pulls a
  * member's payload over xGMI when hipDeviceCanAccessPeer allows it; when it does
- * not (or env SVO_PEER_COPY=1 forces it), the member's stream copies the payload
+ * not (or svo_config.peer_copy forces it), the member's stream copies the payload
  * into a buffer on the display device (hipMemcpyPeerAsync) and the assemble
  * reads that copy -- creation no longer fails for lack of peer access. */
 int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes, int band_rows, svo_ctx **out);
@@ -168,11 +229,11 @@ int svo_render(svo_ctx *ctx, int width, int height, int stack_mode,
  * d_hits are device pointers on this context's device (either may be NULL),
  * `band` selects this rank's rows (NULL = all), `stream` is a hipStream_t
  * (NULL = the context's own stream).  Asynchronous: returns after enqueue --
- * with one exception: the automatic loop-form choice (SVO_LAT
- * unset) waits, once per new static view (the second render after a camera move),
+ * with one exception: the automatic loop-form choice (svo_config.loop_form -1,
+ * the default) waits, once per new static view (the second render after a camera move),
  * for the dispatch-order build of the first one, i.e. for up to one frame of
  * already-enqueued work on that stream.  A caller whose stream waits on something
- * the host signals only after this call returns must set SVO_LAT=0 or 1.  The same
+ * the host signals only after this call returns must set loop_form 0 or 1.  The same
  * holds for svo_render_frame and the renders of svo_render. */
 int svo_render_device(svo_ctx *ctx, int width, int height, int stack_mode,
                       const svo_band *band, void *d_rgba, void *d_hits, void *stream);
@@ -247,6 +308,13 @@ int svo_pack_hits(svo_ctx *ctx, int width, int height, const svo_band *band, con
  * (DESIGN.md 3.1d). */
 int svo_count_fetches(svo_ctx *ctx, int width, int height, int stack_mode,
                       const svo_band *band, void *d_fetches, void *stream);
+
+/* Diagnostics (ABI 10): the start of every primary ray's walk under the current camera -- the
+ * beam start of DESIGN.md 3.1d, in SVO-space t (the loop's t_min; the hit record's t is 2048 x
+ * that), one float per pixel of `band`'s rows (band layout), -inf where the ray starts at its cube
+ * entry.  A record is exact iff no hit lies before its start, so start <= the oracle's hit t on
+ * every hit ray is the bound's conservativeness (tests/test_gpu_beam.py).  Asynchronous. */
+int svo_beam_starts(svo_ctx *ctx, int width, int height, const svo_band *band, float *d_starts, void *stream);
 
 /* Render options (bit set).  SVO_OPT_SHADOW_RAYS: after the primary pass,
  * trace one shadow ray per hit toward -_DirectionalLight (SURVEY.md 8(d) C3;

@@ -27,7 +27,7 @@ assert HIT_DTYPE.itemsize == 24
 COMPACT_DTYPE = np.dtype([("parent", "<u4"), ("meta", "<u4"), ("t", "<f4")])   # svo_hit_compact
 assert COMPACT_DTYPE.itemsize == 12
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 # every symbol include/svo_rt.h declares
 EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera", "svo_render",
            "svo_render_device", "svo_count_fetches", "svo_get_info", "svo_synchronize",
@@ -35,7 +35,8 @@ EXPORTS = ("svo_create", "svo_set_buffer", "svo_set_buffer_v2", "svo_set_camera"
            "svo_kernel_time", "svo_create_multi", "svo_num_devices", "svo_get_member", "svo_render_frame",
            "svo_assemble_frame", "svo_stage_time", "svo_render_progressive", "svo_set_band_deal",
            "svo_pack_hits", "svo_get_member_link", "svo_stage_times", "svo_render_samples",
-           "svo_render_progressive_async", "svo_progressive_last", "svo_forget_stream")
+           "svo_render_progressive_async", "svo_progressive_last", "svo_forget_stream", "svo_get_config",
+           "svo_set_config", "svo_beam_starts")
 SVO_OPT_SHADOW_RAYS = 1
 SVO_OPT_KERNEL_TIMING = 2
 SVO_OPT_COUNT_BEAM = 4
@@ -84,6 +85,30 @@ class SvoFrame(ctypes.Structure):
     _fields_ = [("hits", ctypes.c_void_p), ("rgba", ctypes.c_void_p), ("rgba8", ctypes.c_void_p),
                 ("compact", ctypes.c_void_p), ("position", ctypes.c_void_p), ("voxel", ctypes.c_void_p),
                 ("rgb8", ctypes.c_void_p), ("hitmask", ctypes.c_void_p), ("layout", ctypes.c_int)]
+
+
+# svo_config (include/svo_rt.h, ABI 10): the context's render policy, versioned by size
+CONFIG_VERSION = 1
+_i32, _u32, _f32 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_float
+CONFIG_FIELDS = [
+    ("tile_order", _i32), ("xcd_strips", _i32), ("issue_priority", _i32), ("order_every", _i32),
+    ("move_every", _i32), ("move_spread", _i32), ("relayout", _i32), ("fetch_all", _i32),
+    ("loop_form", _i32), ("lat_ratio", _f32),
+    ("segments", _i32), ("seg_table_latency", _u32), ("seg_table_issue", _u32), ("seg_table_thin", _u32),
+    ("seg_ratio", _f32), ("seg_thin_ratio", _f32), ("seg_cap", _i32), ("seg_min_chain", _i32),
+    ("seg_move", _i32), ("seg_jitter", _i32), ("seg_all", _i32), ("seg_scramble", _u32),
+    ("beam", _i32), ("beam_back", _i32),
+    ("shadow_form", _i32), ("shadow_order", _i32),
+    ("readback", _i32), ("host_copy_threads", _i32),
+    ("sparse_payload", _i32), ("peer_copy", _i32)]
+SHADOW_FUSED, SHADOW_TILES, SHADOW_LIST = 0, 1, 2   # svo_config.shadow_form
+
+
+class SvoConfig(ctypes.Structure):
+    _fields_ = [("size", _u32), ("version", _u32)] + CONFIG_FIELDS
+
+    def to_dict(self):
+        return {name: getattr(self, name) for name, _ in CONFIG_FIELDS}
 
 
 class SvoError(RuntimeError):
@@ -139,6 +164,9 @@ def lib():
         "svo_pack_hits": [vp, i, i, ctypes.POINTER(SvoBand), vp, vp, vp],
         "svo_synchronize": [vp],
         "svo_forget_stream": [vp, vp],
+        "svo_get_config": [vp, ctypes.POINTER(SvoConfig)],
+        "svo_set_config": [vp, ctypes.POINTER(SvoConfig)],
+        "svo_beam_starts": [vp, i, i, ctypes.POINTER(SvoBand), vp, vp],
         "svo_destroy": [vp],
         "svo_last_error": [],
         "svo_abi_version": [],
@@ -153,6 +181,14 @@ def lib():
         fn.restype = ctypes.c_char_p if name == "svo_last_error" else i
     _lib = L
     return L
+
+
+def default_config():
+    """svo_get_config(NULL): the library's defaults, as a dict of svo_config fields."""
+    c = SvoConfig()
+    c.size = ctypes.sizeof(SvoConfig)
+    check(lib().svo_get_config(None, ctypes.byref(c)), "svo_get_config")
+    return c.to_dict()
 
 
 def check(rc, what):

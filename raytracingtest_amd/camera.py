@@ -133,6 +133,24 @@ def column_major(m):
     return np.ascontiguousarray(np.asarray(m, np.float32).T.reshape(-1))
 
 
+def pan_cameras(name, n, step_rad=0.002, radius=3.0):
+    """A slow pan from camera pose `name`: frame k's eye circles the pose's eye in the xz plane by
+    k * step_rad (radius `radius` world units) and looks at the pose's target (overview / flyover /
+    terrain: their look-at target; main: 10 units along its forward axis).  Frame 0 is the pose
+    itself.  The interactive drop-in case: a new view every frame (RaytracingMaster.cs:44-47, 55-74)."""
+    base = CAMERAS[name]()
+    targets = {"overview": OVERVIEW_TARGET, "flyover": FLYOVER_TARGET, "terrain": TERRAIN_TARGET}
+    eye = np.asarray(base.position, float)
+    target = np.asarray(targets[name], float) if name in targets else eye + 10.0 * np.asarray(base.rotation)[:, 2]
+    out = []
+    for k in range(n):
+        a = step_rad * k
+        e = eye + radius * np.array([np.sin(a), 0.0, 1.0 - np.cos(a)])
+        out.append(Camera(position=tuple(e), rotation=look_rotation(target - e), fov=base.fov, near=base.near,
+                          far=base.far))
+    return out
+
+
 def jitter_offsets(n, seed=0x5EED):
     """Seeded _PixelOffset sequence for jittered runs (RaytracingMaster.cs:35 uses Random.value)."""
     rng = np.random.default_rng(seed)

@@ -1089,6 +1089,9 @@ __device__ __forceinline__ void seg_rebalance(uint2 *slot, float t_entry, float 
     const int lane = (int)threadIdx.x, k = lane & (K - 1);
     // a start past the ray's end carries nothing: it sits at the end
     slot[lane] = make_uint2(k <= f ? c : 0u, __float_as_uint(k == 0 ? t_entry : k > f ? t_end : t_start));
+    // lane 0 of each group reads its group's other lanes' entries below: the writes must have landed
+    // (the workgroup is this one wave; the compiler cannot see the cross-lane dependence)
+    __syncthreads();
     if (k != 0 || !store) return;
     if (!(tot > 0.0f)) {   // no information: the next trace splits the cube span evenly
         hint8[0] = __int_as_float(0x7FC00000);
@@ -1170,7 +1173,9 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
     const size_t hi = (size_t)lr * (size_t)p.width + (size_t)x;
     float *hint8 = p.seg_hint ? reinterpret_cast<float *>(p.seg_hint + 2 * hi) : nullptr;   // null: even splits
     const int e0 = k * (SEG_KMAX / K), e1 = e0 + SEG_KMAX / K;   // 0 and 8: none
-    const bool have = hint8 && hint8[0] == hint8[0];               // NaN: none yet
+    // NaN: none yet.  A lane outside the frame (a copy of an edge pixel, which may belong to another
+    // part of this tile traced by another workgroup) takes the even split: it reads no hint
+    const bool have = inside && hint8 && hint8[0] == hint8[0];
     const float t_start = seg_start(p, hint8, have, hi, e0, t_entry, t_exit);
     const float t_stop = seg_start(p, hint8, have, hi, e1, t_entry, t_exit);
     uint32_t n_lane, armed_at;
@@ -2409,9 +2414,30 @@ static hipError_t launch_shadows(const LaunchParams &p, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// svo_beam_starts (diagnostics): every pixel's primary-ray start under the launch's beam starts --
+// beam_start of the ray render_tile_kernel traces (-inf without beam starts), band layout.
+__global__ __launch_bounds__(256) void beam_starts_kernel(LaunchParams p) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)p.width * (size_t)p.local_rows) return;
+    const int x = (int)(i % (size_t)p.width), lr = (int)(i / (size_t)p.width);
+    const int gy = global_row(p, lr);
+    Ray r;
+    float org[3], dir[3];
+    camera_ray(p.cam, p.width, p.height, x, gy, org, dir);
+    setup_ray(org, dir, r);
+    FRay f;
+    to_fray(r, f);
+    p.out.starts[i] = beam_start(p, f, x, gy);
+}
+
 hipError_t launch_render(const LaunchParams &p, int stack_mode, hipStream_t stream, hipEvent_t primary_start,
                          hipEvent_t primary_end) {
     // primary_start / primary_end (nullable): events around the primary-ray kernel only
+    if (p.out.starts) {
+        const size_t n = (size_t)p.width * (size_t)p.local_rows;
+        hipLaunchKernelGGL(beam_starts_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, p);
+        return hipGetLastError();
+    }
     const bool count = p.out.fetches != nullptr;
     hipError_t e = hipSuccess;
     if (primary_start && (e = hipEventRecord(primary_start, stream)) != hipSuccess) return e;

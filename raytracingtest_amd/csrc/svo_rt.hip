@@ -64,9 +64,10 @@ struct Upload {
     int depth;
     bool external;   // has child links outside its own range (sub-SVO linking)
     bool tree;       // every node reached once from the upload's first node (no sharing, no cycles)
-    // beam starts: the splat list of a self-contained tree at offset 0 (null: none)
+    // beam starts: the splat list of a self-contained tree at offset 0, built from the
+    // host arrays at upload (null: none; a pool of several uploads is walked on the device copy)
     std::shared_ptr<const std::vector<uint2>> boxes;
-    uint64_t boxes_id;   // unique per list (the device copy's key)
+    int boxes_back;      // the config's beam_back it was built with
 };
 
 enum { STAGE_KERNEL = 0, STAGE_ASSEMBLE = 1, N_STAGES = 2 };
@@ -94,6 +95,7 @@ constexpr int MAX_SCHED = 4;
 struct Sched {
     hipStream_t stream = nullptr;
     bool used = false;
+    bool idle = false;               // nothing enqueued on `stream` since the last svo_synchronize
     unsigned long long last_use = 0;
     hipEvent_t done = nullptr;       // eviction: recorded on this stream when another takes the set over
     // The dispatch order is built OFF the render stream (round 5): after launch n
@@ -166,6 +168,7 @@ struct Peer {                       // one per member of a multi-device context 
     int accum_w = 0, accum_rows = -1;
     uint64_t accum_deal = 0;             // the band deal its rows belong to
     int link = SVO_LINK_SELF;            // how the payload reaches the display device (svo_get_member_link)
+    int native_link = SVO_LINK_SELF;     // ... without svo_config.peer_copy (what svo_create_multi found)
     void *local[2] = {nullptr, nullptr}; // SVO_LINK_COPY: the payload's copy on the display device
     size_t local_cap = 0;
 };
@@ -242,7 +245,17 @@ struct svo_ctx {
     bool cam_set = false;
     std::vector<Upload> uploads;
     int depth = 0;
-    bool depth_exact = false;        // see recompute_depth
+    bool depth_exact = false;        // see recompute_pool
+    // the splat list of the whole pool (beam starts; null: none) and its unique id
+    std::shared_ptr<const std::vector<uint2>> pool_boxes;
+    uint64_t pool_boxes_id = 0;
+    int pool_boxes_back = -1;
+    // diagnostics (the library's only environment switches, read once at svo_create):
+    // SVO_DEBUG bit 0 the loop-form / class-table decision trace, bit 1 the order each launch
+    // takes; SVO_WAVE_LOG=<file> the per-wave record; SVO_BEAM_DIAG the splat's timing variants
+    int debug = 0;
+    std::string wave_log_path;
+    uint32_t beam_diag = 0;
     // host-path output scratch
     void *d_out_hits = nullptr;
     void *d_shadow_list = nullptr;   // compacted shadow pass: hit masks, offsets, hit list (svo_kernel.hip)
@@ -271,8 +284,9 @@ struct svo_ctx {
     hipStream_t copy_stream = nullptr;
     int pin_w = 0, pin_h = 0, pin_next = 0;
     int pin_format = SVO_PIXELS_RGBA8;   // the slots' pixel format (svo_render_progressive_async)
-    int pin_push = 0;                    // env SVO_PIN_PUSH: 0 hipMemcpyAsync (DMA), 1 a kernel writes the
+    int pin_push = 0;                    // svo_config.readback: 0 hipMemcpyAsync (DMA), 1 a kernel writes the
                                          // mapped pinned buffer, 2 the DMA split over two copy streams
+    int host_copy_threads = 0;           // svo_config.host_copy_threads (0: half the hardware threads)
     hipStream_t copy_stream2 = nullptr;
     hipEvent_t pin_copied2[PIN_SLOTS] = {};
     unsigned long long pin_frames = 0;   // frames enqueued since the slots were (re)allocated
@@ -298,7 +312,7 @@ struct svo_ctx {
                                      // 3/4, 1/2, 1/4, 1/8 of the max, rest; 0 none, 4 or 8) in a latency-bound launch
     int seg_kpack_issue = 0x4;       // env SVO_SEG_ISSUE=<hex>: the same in an issue-bound launch
     int seg_kpack_thin = 0x888;      // env SVO_SEG_THIN=<hex>: ... and in a latency-bound launch whose summed trips
-    double thin_ratio = 0.083;       // are below SVO_SEG_THIN_RATIO x slots x its heaviest tile's: C3 8-way bands
+    float thin_ratio = 0.083f;       // are below SVO_SEG_THIN_RATIO x slots x its heaviest tile's: C3 8-way bands
                                      // (flyover 0.045, Main.unity 0.079) and the overview frame (0.063) run faster
                                      // with every heavy class in eighths, the flyover 4-way band (0.087) with 444
                                      // (profiles/r05_thin_ab.json)
@@ -311,11 +325,11 @@ struct svo_ctx {
     uint2 *d_boxes = nullptr;        // the device copy of the root upload's splat list ...
     size_t boxes_cap = 0;
     uint32_t n_boxes = 0;
-    uint64_t boxes_id = 0;           // ... made from the list with this id (0: none)
+    uint64_t boxes_id = 0;           // ... made from the list with this id (pool_boxes_id; 0: none)
     unsigned long long *count_ts = nullptr;   // beam starts of an instrumented launch (SVO_OPT_COUNT_BEAM)
     size_t count_ts_cap = 0;
     uint32_t count_ts_gen = 0;
-    double lat_ratio = 0.3;          // env SVO_LAT_RATIO: the auto rule's threshold ...
+    float lat_ratio = 0.3f;          // svo_config.lat_ratio: the auto rule's threshold ...
     // the stored segment starts are those of the pixel's ray in the previous launch: of another
     // sub-pixel ray after a jittered launch, of another view while the camera moves.  Such a launch
     // splits its segments evenly from the beam start instead (segments past an earlier segment's
@@ -328,7 +342,7 @@ struct svo_ctx {
     int relayout = 1;                // env SVO_RELAYOUT=0: keep an order built from costs of another class layout
     int seg_min_chain = 160;         // env SVO_SEG_MIN_CHAIN: a latency-bound launch whose heaviest tile costs fewer
                                      // trips takes the latency form, unsegmented, without beam starts
-    double seg_ratio = 0.28;         // env SVO_SEG_RATIO: ... and the same with beam starts (class table only)
+    float seg_ratio = 0.28f;         // svo_config.seg_ratio: ... and the same with beam starts (class table only)
     int move_every = 4;              // env SVO_MOVE_EVERY: while the camera moves every launch, rebuild the
                                      // order only every k-th launch (see launch; 1 = at every new view).
                                      // C3 pan: 118.8 us per frame at 1, 110.7 at 4, 111.9 at 8
@@ -353,7 +367,8 @@ struct svo_ctx {
     int parity = 0;
     int band_rows = 8;
     int deal_cycle = 0;                  // svo_set_band_deal: weighted deal over the members (0: round-robin)
-    int sparse_payload = 0;              // env SVO_SPARSE_PAYLOAD=1: display-only frames travel as sparse parts
+    int sparse_payload = 0;              // svo_config.sparse_payload: display-only frames travel as sparse parts
+    int peer_copy = 0;                   // svo_config.peer_copy: every member's payload copied, not pulled
     uint8_t deal_owner[svo::MAX_CYCLE] = {};
     uint64_t samples_deal = 0;           // the deal of the last svo_render_samples (band accumulations' rows)
     bool samples_deal_set = false;
@@ -436,9 +451,13 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
         // Recorded here, at the rare eviction, not behind every launch: a marker packet
         // between two renders of one stream cost ~2-3 us of GPU time per frame.  The evicted
         // stream is alive: callers keep a stream until svo_forget_stream (svo_rt.h).
-        if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(pick->done, pick->stream));
-        HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
+        // After svo_synchronize nothing is pending there and the stream may be gone (svo_rt.h):
+        // record nothing on it.
+        if (!pick->idle) {
+            if (!pick->done) HIP_TRY(hipEventCreateWithFlags(&pick->done, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(pick->done, pick->stream));
+            HIP_TRY(hipStreamWaitEvent(s, pick->done, 0));
+        }
         if (pick->side) HIP_TRY(hipStreamSynchronize(pick->side));   // its order builds (rare: an eviction)
         reset_builds(*pick);   // built for another stream's frames
         pick->launches = pick->shadow_launches = 0;
@@ -451,6 +470,7 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
     }
     pick->stream = s;
     pick->used = true;
+    pick->idle = false;
     pick->last_use = ++ctx->sched_clock;
     *out = pick;
     return SVO_OK;
@@ -460,7 +480,7 @@ int sched_for(svo_ctx *ctx, hipStream_t s, Sched **out) {
 // number of descriptor levels reachable from the upload's first node.  A
 // breadth-first walk with a seen set: exact for a tree; for a DAG it is the
 // shallowest depth, so such pools are traversed with the full stack
-// (recompute_depth).
+// (recompute_pool walks the whole pool instead).
 int walk_depth(const uint32_t *lo, const uint32_t *first, size_t n, size_t base, size_t pool_n,
                int *depth_out, bool *external_out, bool *tree_out, std::string *err) {
     *tree_out = true;
@@ -498,21 +518,6 @@ int walk_depth(const uint32_t *lo, const uint32_t *first, size_t n, size_t base,
     *depth_out = depth;
     *external_out = external;
     return 0;
-}
-
-void recompute_depth(svo_ctx *ctx) {
-    int root_depth = 0;
-    for (const Upload &u : ctx->uploads)
-        if (u.offset == 0) root_depth = std::max(root_depth, u.depth);
-    // A single self-contained tree at offset 0: every descent path has exactly its
-    // walked depth, so the traversal stack needs depth - 1 slots and cannot overflow
-    // while parents are exact (the kernel may then drop its overflow guard).  Any
-    // other pool -- a DAG (the walk saw a node twice, so its depth is only the
-    // shallowest path), linked sub-pools, several uploads -- gets the full 22-slot
-    // stack of the reference (stack[s_max + 1], NVIDIASVO.compute:13).
-    ctx->depth_exact = ctx->uploads.size() == 1 && ctx->uploads[0].offset == 0 && !ctx->uploads[0].external &&
-                       ctx->uploads[0].tree && root_depth <= 22;
-    ctx->depth = ctx->depth_exact ? root_depth : 22;
 }
 
 // The splat list of a tree: every box a primary ray can first hit a voxel in, at
@@ -578,24 +583,106 @@ int validate_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, siz
     // capacity is legal; the pool is zero-filled at svo_create, so a link into a
     // region not uploaded yet reads empty descriptors
     if (walk_depth(lo, first, n, base, ctx->capacity, &depth, &ext, &tree, &err) != 0) return fail(SVO_ERR_FORMAT, err);
-    *out = Upload{base, n, depth, ext, tree, nullptr, 0};
-    if (base == 0 && tree && !ext && ctx->beam) {
-        static std::atomic<uint64_t> next_id{0};
+    *out = Upload{base, n, depth, ext, tree, nullptr, -1};
+    if (base == 0 && tree && !ext && ctx->beam) {   // the common case: the splat list from the host arrays
         out->boxes = build_beam_boxes(lo, first, n, depth, ctx->beam_back);
-        out->boxes_id = ++next_id;
+        out->boxes_back = ctx->beam_back;
     }
     return SVO_OK;
 }
 
+uint64_t next_boxes_id() {
+    static std::atomic<uint64_t> next_id{0};
+    return ++next_id;
+}
+
+// The pool's traversal facts and its splat list, after every upload and beam config change.
+//  * One self-contained tree uploaded at offset 0 (the reference's SetSVOBuffer(data)): its own
+//    upload walk; the splat list built from its host arrays then.
+//  * Anything else -- a trunk whose leaves link to sub-SVOs uploaded elsewhere (Clipmap.cs:153-169
+//    via SetSVOBuffer(data, offset), RaytracingMaster.cs:118-135), several uploads, a shared
+//    subtree: the pool as the device holds it is walked from the root (node 0) across the uploads.
+//    A child index past the uploaded nodes reads as the zero-filled empty descriptor (no
+//    children).  If every node is reached once, the pool is one tree: its depth is exact (the
+//    stack needs depth - 1 slots and cannot overflow) and its splat list comes from this walk, so
+//    a linked pool gets beam starts too.  A DAG or a pool deeper than 22 levels gets the
+//    reference's full 22-slot stack (stack[s_max + 1], NVIDIASVO.compute:13) and no beam starts.
+int recompute_pool(svo_ctx *ctx) {
+    ctx->depth_exact = false;
+    ctx->depth = 22;
+    std::shared_ptr<const std::vector<uint2>> boxes;
+    const bool simple = ctx->uploads.size() == 1 && ctx->uploads[0].offset == 0 && !ctx->uploads[0].external &&
+                        ctx->uploads[0].tree && ctx->uploads[0].depth <= 22;
+    if (simple) {
+        ctx->depth_exact = true;
+        ctx->depth = ctx->uploads[0].depth;
+        if (ctx->beam && ctx->uploads[0].boxes_back == ctx->beam_back) boxes = ctx->uploads[0].boxes;
+    }
+    const bool have = boxes || !ctx->beam;
+    if ((!simple || !have) && ctx->n_nodes > 0 && ctx->n_nodes < 0xFFFFFFFFull) {
+        // the device copy of the pool (the host arrays of earlier uploads are gone)
+        const size_t n = ctx->n_nodes;
+        std::vector<uint2> pool(n);
+        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(pool.data(), ctx->d_nodes, n * sizeof(uint2), hipMemcpyDeviceToHost));
+        std::vector<uint32_t> lo(n), first(n);
+        for (size_t i = 0; i < n; ++i) {
+            lo[i] = pool[i].x;
+            first[i] = pool[i].y;
+        }
+        if (!simple) {   // breadth-first from the root, every node at most once
+            std::vector<uint8_t> seen(n, 0);
+            std::vector<uint32_t> cur{0}, nxt;
+            seen[0] = 1;
+            int depth = 0, deep = 0;   // levels of uploaded descriptors; the deepest empty child's level
+            bool tree = true;
+            while (!cur.empty() && tree && depth <= 22) {
+                ++depth;
+                nxt.clear();
+                for (uint32_t li : cur) {
+                    const uint32_t m = lo[li] & 0xFFu;
+                    uint32_t rank = 0;
+                    for (int c = 0; c < 8; ++c) {
+                        if (!((m >> c) & 1u)) continue;
+                        const uint64_t child = (uint64_t)first[li] + rank++;
+                        if (child >= n) {   // not uploaded: an empty descriptor one level down
+                            deep = std::max(deep, depth + 1);
+                            continue;
+                        }
+                        if (seen[child]) { tree = false; break; }
+                        seen[child] = 1;
+                        nxt.push_back((uint32_t)child);
+                    }
+                    if (!tree) break;
+                }
+                cur.swap(nxt);
+            }
+            depth = std::max(depth, deep);
+            if (tree && cur.empty() && depth <= 22) {
+                ctx->depth_exact = true;
+                ctx->depth = depth;
+            }
+        }
+        if (ctx->depth_exact && ctx->beam) boxes = build_beam_boxes(lo.data(), first.data(), n, ctx->depth, ctx->beam_back);
+    }
+    if (boxes != ctx->pool_boxes) {
+        ctx->pool_boxes = boxes;
+        ctx->pool_boxes_id = boxes ? next_boxes_id() : 0;
+    }
+    ctx->pool_boxes_back = ctx->beam_back;
+    return SVO_OK;
+}
+
 // Commit an upload's metadata -- only after its device copies have completed.
-void commit_upload(svo_ctx *ctx, const Upload &u) {
+int commit_upload(svo_ctx *ctx, const Upload &u) {
     ctx->uploads.erase(std::remove_if(ctx->uploads.begin(), ctx->uploads.end(),
                                       [&](const Upload &v) { return v.offset == u.offset; }),
                        ctx->uploads.end());
     ctx->uploads.push_back(u);
     ctx->n_nodes = std::max(ctx->n_nodes, u.offset + u.count);
     ++ctx->cost_gen;   // another pool: other costs
-    recompute_depth(ctx);
+    return recompute_pool(ctx);
 }
 
 int ensure_out(svo_ctx *ctx, size_t px) {
@@ -658,7 +745,6 @@ int ensure_pinned(svo_ctx *ctx, int width, int height) {
     if (ctx->copy_stream2) HIP_TRY(hipStreamSynchronize(ctx->copy_stream2));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     free_pinned(ctx);
-    if (const char *v = std::getenv("SVO_PIN_PUSH")) ctx->pin_push = std::atoi(v);
     if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
     if (ctx->pin_push == 2 && !ctx->copy_stream2)
         HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream2, hipStreamNonBlocking));
@@ -929,7 +1015,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     }
     if (p.shadows == 3 && out.hitmask) p.shadows = 1;   // the caller's masks are not a list scratch
     if (p.local_rows == 0) return SVO_OK;
-    if (out.fetches) p.shadows = 0;
+    const bool instr = out.fetches || out.starts;   // instrumented: svo_count_fetches / svo_beam_starts
+    if (instr) p.shadows = 0;
     hipStream_t s = stream ? stream : ctx->stream;
     if ((p.shadows == 1 || p.shadows == 3) && !p.out.hits && !p.out.compact) {   // the second pass reads the records
         int rc2 = ensure_out(ctx, (size_t)(p.out.frame_layout ? height : p.local_rows) * (size_t)width);
@@ -953,7 +1040,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         p.out.hitmask = reinterpret_cast<unsigned long long *>(ctx->d_shadow_list);
     }
     p.prio = ctx->prio;
-    const bool ordered = ctx->tile_order && !p.out.fetches;
+    const bool ordered = ctx->tile_order && !instr;
     const int n_tiles = ((width + 7) / 8) * ((p.local_rows + 7) / 8);
     Geo key;        // the geometry (seg 0): the key of the costs and of the loop-form decision
     Geo okey;       // the order's key: key + the seg_cap its order was built with
@@ -1047,17 +1134,12 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     const int mode_now = p.shadows | (stack_mode << 2);
     // whether this launch's primary rays get beam starts (the test of the beam block below, less the
     // per-launch camera checks)
-    bool beam_planned = ctx->beam && q && !p.guard && !p.out.fetches && ctx->depth_exact;
-    if (beam_planned) {
-        bool boxes = false;
-        for (const Upload &u : ctx->uploads)
-            if (u.offset == 0) boxes = u.boxes && !u.boxes->empty();
-        beam_planned = boxes;
-    }
+    const bool beam_planned = ctx->beam && q && !p.guard && !instr && ctx->depth_exact && ctx->pool_boxes &&
+                              !ctx->pool_boxes->empty();
     p.lat = 0;
     bool latency_bound = false;
     const bool have_order = q && [&] { Geo g = q->order_key; g.seg = g.kpack = 0; return g == key; }();
-    if (!p.guard && p.shadows == 0 && !p.out.fetches && !p.samples && (ctx->lat_mode != 0 || seg_cap)) {
+    if (!p.guard && p.shadows == 0 && !instr && !p.samples && (ctx->lat_mode != 0 || seg_cap)) {
         if (ctx->lat_mode == 1) {
             latency_bound = true;
         } else if (q && q->stats && have_order) {
@@ -1107,10 +1189,11 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                     q->lat_key = q->stats_key[r];
                     q->lat_view = q->stats_view[r];
                     q->lat_mode = q->stats_mode[r];
-                    if (std::getenv("SVO_LAT_DEBUG"))   // diagnostics: the decision and its inputs
-                        std::fprintf(stderr, "svo lat: view %llu T %llu M %u slots %.0f ratio %.4f -> %s%s\n", q->lat_view,
-                                     (unsigned long long)t, m, slots, m ? (double)t / (slots * (double)m) : 0.0,
-                                     q->lat_cache ? "latency" : "lean", q->lat_thin ? " thin" : "");
+                    if (ctx->debug & 1)   // diagnostics (SVO_DEBUG bit 0): the decision and its inputs
+                        std::fprintf(stderr, "svo lat: view %llu T %llu M %u slots %.0f ratio %.6f bound %.6f thin %.6f "
+                                     "beam %d -> %s%s\n", q->lat_view, (unsigned long long)t, m, slots,
+                                     m ? (double)t / (slots * (double)m) : 0.0, bound, (double)ctx->thin_ratio,
+                                     beam_planned ? 1 : 0, q->lat_cache ? "latency" : "lean", q->lat_thin ? " thin" : "");
                 }
                 break;
             }
@@ -1151,7 +1234,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             }
         }
         p.tile_order = use >= 0 ? q->order_buf[use] : nullptr;
-        if (std::getenv("SVO_ORDER_DEBUG"))   // diagnostics: the order and class table each launch takes
+        if (ctx->debug & 2)   // diagnostics (SVO_DEBUG bit 1): the order and class table each launch takes
             std::fprintf(stderr, "svo order: launch %lld view %llu latency %d kpack %x use %d built_at %lld/%lld keys %d/%d\n",
                          n, ctx->view_gen, (int)latency_bound, okey.kpack, use, q->build_at[0], q->build_at[1],
                          (int)(q->build_key[0] == okey), (int)(q->build_key[1] == okey));
@@ -1169,9 +1252,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // the resident waves of the quarters too (C3 flyover bands, profiles/r05b_seg_ab.json: N = 2
     // 0.0804 ms with it against 0.0629 without, N = 4 0.0500 / 0.0457, N = 8 0.0388 / 0.0395)
     p.lat = latency_bound && ctx->lat_mode != 0 && (!p.seg || ctx->lat_mode == 1) ? 1 : 0;
-    const char *log_path = std::getenv("SVO_WAVE_LOG");
+    const char *log_path = ctx->wave_log_path.empty() ? nullptr : ctx->wave_log_path.c_str();
     const size_t n_wave = (size_t)n_tiles;
-    if (log_path && !p.out.fetches) {
+    if (log_path && !instr) {
         if (ctx->wave_log_cap < n_wave) {
             HIP_TRY(hipDeviceSynchronize());
             if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
@@ -1188,11 +1271,10 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // bounds are a function of the camera matrices, the pool and the frame size only (pixel offsets
     // in [0, 1] are covered), so a launch at the view of this stream's previous one reuses them --
     // a held view (the reference's accumulating camera) splats once; a moving camera every frame.
-    const bool count_beam = p.out.fetches && (ctx->options & SVO_OPT_COUNT_BEAM);
-    if (ctx->beam && (q || count_beam) && !p.guard && (!p.out.fetches || count_beam) && ctx->depth_exact && !p.lat) {
-        const Upload *root = nullptr;
-        for (const Upload &u : ctx->uploads)
-            if (u.offset == 0) root = &u;
+    // an instrumented launch with the beam: SVO_OPT_COUNT_BEAM's fetch count, or svo_beam_starts
+    const bool count_beam = (p.out.fetches && (ctx->options & SVO_OPT_COUNT_BEAM)) || p.out.starts;
+    if (ctx->beam && (q || count_beam) && !p.guard && (!instr || count_beam) && ctx->depth_exact && !p.lat) {
+        const std::shared_ptr<const std::vector<uint2>> &boxes = ctx->pool_boxes;
         auto in01 = [](float v) { return v >= 0.0f && v <= 1.0f; };
         bool offs = in01(p.cam.px_off[0]) && in01(p.cam.px_off[1]);
         if (p.samples) {
@@ -1201,9 +1283,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         }
         svo::BeamParams bp;
         std::memset(&bp, 0, sizeof bp);
-        if (root && root->boxes && !root->boxes->empty() && offs && beam_camera(p.cam, width, height, &bp)) {
-            if (ctx->boxes_id != root->boxes_id) {   // the device copy of this pool's splat list
-                const size_t nb = root->boxes->size();
+        if (boxes && !boxes->empty() && offs && beam_camera(p.cam, width, height, &bp)) {
+            if (ctx->boxes_id != ctx->pool_boxes_id) {   // the device copy of this pool's splat list
+                const size_t nb = boxes->size();
                 HIP_TRY(hipDeviceSynchronize());   // launches on any stream may still read the old one
                 if (ctx->boxes_cap < nb) {
                     if (ctx->d_boxes) hipFree(ctx->d_boxes);
@@ -1212,9 +1294,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                     HIP_TRY(hipMalloc(&ctx->d_boxes, nb * sizeof(uint2)));
                     ctx->boxes_cap = nb;
                 }
-                HIP_TRY(hipMemcpy(ctx->d_boxes, root->boxes->data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(ctx->d_boxes, boxes->data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
                 ctx->n_boxes = (uint32_t)nb;
-                ctx->boxes_id = root->boxes_id;
+                ctx->boxes_id = ctx->pool_boxes_id;
             }
             const int tx = (width + 7) / 8, ty = (height + 7) / 8, sx = (width + 63) / 64, sy = (height + 63) / 64;
             const size_t need = (size_t)tx * ty + (size_t)sx * sy + 1;
@@ -1226,7 +1308,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 rc = order_scratch(ctx, s);
                 if (rc) return rc;
             }
-            const bool reuse = q && q->ts_view == ctx->view_gen && q->ts_boxes == root->boxes_id && q->ts_w == width &&
+            const bool reuse = q && q->ts_view == ctx->view_gen && q->ts_boxes == ctx->pool_boxes_id && q->ts_w == width &&
                                q->ts_h == height && cap >= need && gen != 0;
             if (!reuse && (cap < need || gen == 0xFFFFFFFEu)) {   // (re)filled with all-ones keys: generation 0, stale
                 HIP_TRY(hipDeviceSynchronize());   // a pending launch may still read the old buffer
@@ -1245,7 +1327,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             bp.n_boxes = ctx->n_boxes;
             bp.tile_start = buf;
             bp.gen = gen;
-            if (const char *v = std::getenv("SVO_BEAM_DIAG")) bp.diag = (uint32_t)std::atoi(v);   // timing only
+            bp.diag = ctx->beam_diag;   // timing diagnostics only
             bp.tiles_x = tx;
             bp.tiles_y = ty;
             bp.super_x = sx;
@@ -1259,7 +1341,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
                 if (q) {
                     q->ts_view = ctx->view_gen;
-                    q->ts_boxes = root->boxes_id;
+                    q->ts_boxes = ctx->pool_boxes_id;
                     q->ts_w = width;
                     q->ts_h = height;
                 }
@@ -1273,7 +1355,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         }
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    if (!p.out.fetches) {
+    if (!instr) {
         rc = take_events(ctx, STAGE_KERNEL, &ev0, &ev1);
         if (rc) return rc;
     }
@@ -1595,7 +1677,10 @@ int replicate_upload(svo_ctx *g, size_t offset, size_t n) {
     }
     HIP_TRY(hipSetDevice(m0->device));
     HIP_TRY(hipStreamSynchronize(m0->stream));
-    for (size_t i = 1; i < g->members.size(); ++i) commit_upload(g->members[i], u);
+    for (size_t i = 1; i < g->members.size(); ++i) {
+        const int rc = commit_upload(g->members[i], u);
+        if (rc) return rc;
+    }
     return SVO_OK;
 }
 
@@ -1648,11 +1733,191 @@ int destroy_single(svo_ctx *ctx) {
     return SVO_OK;
 }
 
+// ------------------------------------------------------------------ svo_config
+void config_of(const svo_ctx *c, svo_config *o) {
+    svo_config k;
+    std::memset(&k, 0, sizeof k);
+    k.size = sizeof(svo_config);
+    k.version = SVO_CONFIG_VERSION;
+    k.tile_order = c->tile_order;
+    k.xcd_strips = c->xcd_remap == 2 ? 1 : 0;
+    k.issue_priority = c->prio;
+    k.order_every = c->order_every;
+    k.move_every = c->move_every;
+    k.move_spread = c->spread;
+    k.relayout = c->relayout;
+    k.fetch_all = c->fetch_all;
+    k.loop_form = c->lat_mode;
+    k.lat_ratio = c->lat_ratio;
+    k.segments = c->seg_mode;
+    k.seg_table_latency = (uint32_t)c->seg_kpack_lat;
+    k.seg_table_issue = (uint32_t)c->seg_kpack_issue;
+    k.seg_table_thin = (uint32_t)c->seg_kpack_thin;
+    k.seg_ratio = c->seg_ratio;
+    k.seg_thin_ratio = c->thin_ratio;
+    k.seg_cap = c->seg_cap;
+    k.seg_min_chain = c->seg_min_chain;
+    k.seg_move = c->seg_move;
+    k.seg_jitter = c->seg_jitter;
+    k.seg_all = c->seg_all;
+    k.seg_scramble = c->seg_scramble;
+    k.beam = c->beam;
+    k.beam_back = c->beam_back;
+    k.shadow_form = c->shadow_compact ? 2 : c->fused_shadows ? 0 : 1;
+    k.shadow_order = c->shadow_order_enabled;
+    k.readback = c->pin_push;
+    k.host_copy_threads = c->host_copy_threads;
+    k.sparse_payload = c->sparse_payload;
+    k.peer_copy = c->peer_copy;
+    *o = k;
+}
+
+int check_config(const svo_config &k) {
+    auto bit = [](int32_t v) { return v == 0 || v == 1; };
+    auto table = [](uint32_t t) {
+        if (t > 0xFFFFFFu) return false;
+        for (int c = 0; c < 6; ++c) {
+            const uint32_t kc = (t >> (4 * c)) & 15u;
+            if (kc != 0 && kc != 4 && kc != 8) return false;
+        }
+        return true;
+    };
+    auto ratio = [](float r) { return std::isfinite(r) && r >= 0.0f; };
+    const char *bad = !bit(k.tile_order) ? "tile_order" : !bit(k.xcd_strips) ? "xcd_strips"
+                    : !bit(k.issue_priority) ? "issue_priority" : k.order_every < 1 ? "order_every"
+                    : k.move_every < 1 ? "move_every" : !bit(k.move_spread) ? "move_spread"
+                    : !bit(k.relayout) ? "relayout" : k.fetch_all < -1 || k.fetch_all > 1 ? "fetch_all"
+                    : k.loop_form < -1 || k.loop_form > 1 ? "loop_form" : !ratio(k.lat_ratio) ? "lat_ratio"
+                    : !bit(k.segments) ? "segments" : !table(k.seg_table_latency) ? "seg_table_latency"
+                    : !table(k.seg_table_issue) ? "seg_table_issue" : !table(k.seg_table_thin) ? "seg_table_thin"
+                    : !ratio(k.seg_ratio) ? "seg_ratio" : !ratio(k.seg_thin_ratio) ? "seg_thin_ratio"
+                    : k.seg_cap < 1 ? "seg_cap" : k.seg_min_chain < 0 ? "seg_min_chain"
+                    : k.seg_move < 1 || k.seg_move > 2 ? "seg_move" : k.seg_jitter < 0 || k.seg_jitter > 2 ? "seg_jitter"
+                    : k.seg_all != 0 && k.seg_all != 4 && k.seg_all != 8 ? "seg_all" : !bit(k.beam) ? "beam"
+                    : k.beam_back < 0 || k.beam_back > 22 ? "beam_back" : k.shadow_form < 0 || k.shadow_form > 2 ? "shadow_form"
+                    : !bit(k.shadow_order) ? "shadow_order" : k.readback < 0 || k.readback > 2 ? "readback"
+                    : k.host_copy_threads < 0 || k.host_copy_threads > 16 ? "host_copy_threads"
+                    : !bit(k.sparse_payload) ? "sparse_payload" : !bit(k.peer_copy) ? "peer_copy" : nullptr;
+    if (bad) return fail(SVO_ERR_ARG, std::string("svo_config.") + bad + " out of range");
+    return SVO_OK;
+}
+
+// One device's context takes a validated config.  Nothing here changes a result; what holds state
+// built under the old value is rebuilt: the pinned readback slots (their allocation flags follow
+// `readback`), the host copy threads, the pool's splat list (beam, beam_back); and every stream's
+// loop-form / class-table decision is dropped, so the next order build decides under the new rule.
+int apply_config(svo_ctx *c, const svo_config &k) {
+    c->tile_order = k.tile_order;
+    c->xcd_remap = k.xcd_strips ? 2 : 0;
+    c->prio = k.issue_priority;
+    c->order_every = k.order_every;
+    c->move_every = k.move_every;
+    c->spread = k.move_spread;
+    c->relayout = k.relayout;
+    c->fetch_all = k.fetch_all;
+    c->lat_mode = k.loop_form;
+    c->lat_ratio = k.lat_ratio;
+    c->seg_mode = k.segments;
+    c->seg_kpack_lat = (int)k.seg_table_latency;
+    c->seg_kpack_issue = (int)k.seg_table_issue;
+    c->seg_kpack_thin = (int)k.seg_table_thin;
+    c->seg_ratio = k.seg_ratio;
+    c->thin_ratio = k.seg_thin_ratio;
+    c->seg_cap = k.seg_cap;
+    c->seg_min_chain = k.seg_min_chain;
+    c->seg_move = k.seg_move;
+    c->seg_jitter = k.seg_jitter;
+    c->seg_all = k.seg_all;
+    c->seg_scramble = k.seg_scramble;
+    c->shadow_compact = k.shadow_form == 2;
+    c->fused_shadows = k.shadow_form == 0;
+    c->shadow_order_enabled = k.shadow_order;
+    c->sparse_payload = k.sparse_payload;
+    c->peer_copy = k.peer_copy;
+    if (c->pin_push != k.readback) {
+        if (c->h_pin[0]) {
+            HIP_TRY(hipSetDevice(c->device));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            if (c->copy_stream) HIP_TRY(hipStreamSynchronize(c->copy_stream));
+            if (c->copy_stream2) HIP_TRY(hipStreamSynchronize(c->copy_stream2));
+            free_pinned(c);
+        }
+        c->pin_push = k.readback;
+    }
+    if (c->host_copy_threads != k.host_copy_threads) {
+        c->copy_pool.reset();   // idle between calls (svo_render waits for it)
+        c->host_copy_threads = k.host_copy_threads;
+    }
+    const bool boxes = c->beam != k.beam || c->beam_back != k.beam_back;
+    c->beam = k.beam;
+    c->beam_back = k.beam_back;
+    if (boxes && c->n_nodes > 0) {
+        const int rc = recompute_pool(c);
+        if (rc) return rc;
+    }
+    for (Sched &q : c->sched) {
+        q.lat_key = Geo();
+        q.lat_mode = -1;
+    }
+    return SVO_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
-int svo_abi_version(void) { return 9; }
+int svo_get_config(svo_ctx *ctx, svo_config *cfg) {
+    if (!cfg) return fail(SVO_ERR_ARG, "cfg is null");
+    if (cfg->size < 2 * sizeof(uint32_t)) return fail(SVO_ERR_ARG, "svo_config.size must hold at least size and version");
+    static const svo_ctx defaults;
+    svo_config k;
+    config_of(ctx ? ctx : &defaults, &k);
+    const size_t n = std::min<size_t>(cfg->size, sizeof k);
+    k.size = (uint32_t)n;
+    std::memcpy(cfg, &k, n);
+    return SVO_OK;
+}
+
+int svo_set_config(svo_ctx *ctx, const svo_config *cfg) {
+    if (!ctx || !cfg) return fail(SVO_ERR_ARG, "null argument");
+    if (cfg->size < 2 * sizeof(uint32_t)) return fail(SVO_ERR_ARG, "svo_config.size must hold at least size and version");
+    if (cfg->size > sizeof(svo_config))
+        return fail(SVO_ERR_ARG, "svo_config.size " + std::to_string(cfg->size) + " is larger than this library's (" +
+                                     std::to_string(sizeof(svo_config)) + "): a newer ABI");
+    svo_config k;
+    config_of(ctx, &k);   // fields past the caller's size keep the context's values
+    std::memcpy(&k, cfg, cfg->size);
+    k.size = sizeof k;
+    k.version = SVO_CONFIG_VERSION;
+    int rc = check_config(k);
+    if (rc) return rc;
+    if (is_multi(ctx)) {
+        for (svo_ctx *m : ctx->members) {
+            rc = apply_config(m, k);
+            if (rc) return rc;
+        }
+        if (k.peer_copy != ctx->peer_copy) {   // the members' payload routes: frames in flight first
+            for (svo_ctx *m : ctx->members) {
+                HIP_TRY(hipSetDevice(m->device));
+                HIP_TRY(hipDeviceSynchronize());
+            }
+            HIP_TRY(hipSetDevice(ctx->members[0]->device));
+            for (size_t i = 1; i < ctx->peers.size(); ++i)
+                ctx->peers[i].link = k.peer_copy ? SVO_LINK_COPY : ctx->peers[i].native_link;
+        }
+    }
+    return apply_config(ctx, k);
+}
+
+int svo_beam_starts(svo_ctx *ctx, int width, int height, const svo_band *band, float *d_starts, void *stream) {
+    if (!d_starts) return fail(SVO_ERR_ARG, "d_starts is null");
+    if (ctx && is_multi(ctx)) return fail(SVO_ERR_ARG, "beam starts of a member context (svo_get_member)");
+    svo::Outputs o{};
+    o.starts = d_starts;
+    return launch(ctx, width, height, SVO_STACK_HLSL, band, o, reinterpret_cast<hipStream_t>(stream));
+}
+
+int svo_abi_version(void) { return 10; }
 
 const char *svo_last_error(void) { return g_last_error.c_str(); }
 
@@ -1681,43 +1946,10 @@ int svo_create(int device, size_t capacity_nodes, svo_ctx **out) {
     int lds_block = 0;
     if (e == hipSuccess) e = hipDeviceGetAttribute(&lds_block, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
     if (e == hipSuccess && lds_block > 0) ctx->lds_per_block = (size_t)lds_block;
-    if (const char *k = std::getenv("SVO_XCD_REMAP")) ctx->xcd_remap = std::atoi(k) == 0 ? 0 : 2;
-    if (const char *k = std::getenv("SVO_TILE_ORDER")) ctx->tile_order = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_PRIO")) ctx->prio = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_SHADOW_ORDER")) ctx->shadow_order_enabled = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_FETCH_ALL")) ctx->fetch_all = std::atoi(k) != 0 ? 1 : 0;
-    if (const char *k = std::getenv("SVO_FUSED_SHADOWS")) ctx->fused_shadows = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_SHADOW_COMPACT")) ctx->shadow_compact = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_ORDER_EVERY")) ctx->order_every = std::max(1, std::atoi(k));
-    if (const char *k = std::getenv("SVO_MOVE_EVERY")) ctx->move_every = std::max(1, std::atoi(k));
-    if (const char *k = std::getenv("SVO_LAT")) ctx->lat_mode = std::atoi(k) != 0 ? 1 : 0;
-    if (const char *k = std::getenv("SVO_SEG")) ctx->seg_mode = std::atoi(k) != 0 ? 1 : 0;
-    auto kpack_env = [](const char *name, int dflt) {
-        const char *k = std::getenv(name);
-        if (!k) return dflt;
-        const int v = (int)std::strtol(k, nullptr, 16);
-        for (int c = 0; c < 6; ++c) {
-            const int kc = (v >> (4 * c)) & 15;
-            if (kc != 0 && kc != 4 && kc != 8) return dflt;   // not a valid table: the default
-        }
-        return v & 0xFFFFFF;
-    };
-    ctx->seg_kpack_lat = kpack_env("SVO_SEG_LAT", ctx->seg_kpack_lat);
-    ctx->seg_kpack_issue = kpack_env("SVO_SEG_ISSUE", ctx->seg_kpack_issue);
-    ctx->seg_kpack_thin = kpack_env("SVO_SEG_THIN", ctx->seg_kpack_thin);
-    if (const char *k = std::getenv("SVO_SEG_THIN_RATIO")) ctx->thin_ratio = std::atof(k);
-    if (const char *k = std::getenv("SVO_SEG_CAP")) ctx->seg_cap = std::max(1, std::atoi(k));
-    if (const char *k = std::getenv("SVO_SEG_ALL")) ctx->seg_all = std::atoi(k) == 8 ? 8 : std::atoi(k) != 0 ? 4 : 0;
-    if (const char *k = std::getenv("SVO_SEG_SCRAMBLE")) ctx->seg_scramble = (uint32_t)std::strtoul(k, nullptr, 10);
-    if (const char *k = std::getenv("SVO_LAT_RATIO")) ctx->lat_ratio = std::atof(k);
-    if (const char *k = std::getenv("SVO_SEG_RATIO")) ctx->seg_ratio = std::atof(k);
-    if (const char *k = std::getenv("SVO_SEG_JITTER")) ctx->seg_jitter = std::atoi(k);
-    if (const char *k = std::getenv("SVO_SEG_MOVE")) ctx->seg_move = std::atoi(k);
-    if (const char *k = std::getenv("SVO_SPREAD")) ctx->spread = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_RELAYOUT")) ctx->relayout = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_SEG_MIN_CHAIN")) ctx->seg_min_chain = std::max(0, std::atoi(k));
-    if (const char *k = std::getenv("SVO_BEAM")) ctx->beam = std::atoi(k) != 0;
-    if (const char *k = std::getenv("SVO_BEAM_BACK")) ctx->beam_back = std::max(0, std::atoi(k));
+    // diagnostics only (svo_rt.h): traces and timing aids, never a policy
+    if (const char *k = std::getenv("SVO_DEBUG")) ctx->debug = std::atoi(k);
+    if (const char *k = std::getenv("SVO_WAVE_LOG")) ctx->wave_log_path = k;
+    if (const char *k = std::getenv("SVO_BEAM_DIAG")) ctx->beam_diag = (uint32_t)std::atoi(k);
     if (e != hipSuccess) {
         destroy_single(ctx);
         return fail(SVO_ERR_HIP, std::string("svo_create: ") + hipGetErrorString(e));
@@ -1737,7 +1969,6 @@ int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes,
     g->capacity = capacity_nodes;
     g->band_rows = band_rows;
     g->peers.resize(num_devices);
-    if (const char *k = std::getenv("SVO_SPARSE_PAYLOAD")) g->sparse_payload = std::atoi(k) != 0;
     auto bail = [&](int rc) {
         svo_destroy(g);
         return rc;
@@ -1750,31 +1981,29 @@ int svo_create_multi(const int *devices, int num_devices, size_t capacity_nodes,
     }
     // the display device reads every other device's payload over xGMI (peer access);
     // a member it cannot map gets the copy fallback (SVO_LINK_COPY, multi_render).
-    // SVO_PEER_COPY=1 forces the copy for every member but the display device itself
+    // svo_config.peer_copy forces the copy for every member but the display device itself
     // (the one-GPU test of that path: a repeated device index)
-    const char *force = std::getenv("SVO_PEER_COPY");
-    const bool force_copy = force && std::atoi(force) != 0;
     for (int i = 1; i < num_devices; ++i) {
         Peer &pr = g->peers[i];
         if (devices[i] == devices[0]) {
-            pr.link = force_copy ? SVO_LINK_COPY : SVO_LINK_SELF;
+            pr.native_link = pr.link = SVO_LINK_SELF;
             continue;
         }
         int ok = 0;
         hipError_t e = hipDeviceCanAccessPeer(&ok, devices[0], devices[i]);
-        if (e != hipSuccess || !ok || force_copy) {
+        if (e != hipSuccess || !ok) {
             (void)hipGetLastError();
-            pr.link = SVO_LINK_COPY;
+            pr.native_link = pr.link = SVO_LINK_COPY;
             continue;
         }
         hipSetDevice(devices[0]);
         e = hipDeviceEnablePeerAccess(devices[i], 0);
         if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) {
             (void)hipGetLastError();
-            pr.link = SVO_LINK_PEER;
+            pr.native_link = pr.link = SVO_LINK_PEER;
         } else {   // reported as possible, refused when enabled: copy instead
             (void)hipGetLastError();
-            pr.link = SVO_LINK_COPY;
+            pr.native_link = pr.link = SVO_LINK_COPY;
         }
     }
     for (int i = 1; i < num_devices; ++i) {
@@ -1873,8 +2102,7 @@ int svo_set_buffer(svo_ctx *ctx, const int32_t *desc, size_t n_desc, const uint3
     HIP_TRY(hipMemcpyAsync(ctx->d_att + dst_offset, att, n_att * sizeof(uint32_t), hipMemcpyHostToDevice,
                            ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    commit_upload(ctx, u);
-    return SVO_OK;
+    return commit_upload(ctx, u);
 }
 
 int svo_set_buffer_v2(svo_ctx *ctx, const uint64_t *nodes, size_t n_nodes, const uint32_t *att,
@@ -1905,8 +2133,7 @@ int svo_set_buffer_v2(svo_ctx *ctx, const uint64_t *nodes, size_t n_nodes, const
     HIP_TRY(hipMemcpyAsync(ctx->d_att + dst_offset, att, n_att * sizeof(uint32_t), hipMemcpyHostToDevice,
                            ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    commit_upload(ctx, u);
-    return SVO_OK;
+    return commit_upload(ctx, u);
 }
 
 int svo_set_camera(svo_ctx *ctx, const float c2w[16], const float inv_proj[16], float px_off_x,
@@ -2026,8 +2253,7 @@ int svo_render(svo_ctx *ctx, int width, int height, int stack_mode, float *rgba_
         for (int i = 0; i < svo_ctx::STAGE_CHUNKS; ++i)
             HIP_TRY(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
     if (!c->copy_pool) {
-        int n = (int)std::thread::hardware_concurrency() / 2;
-        if (const char *v = std::getenv("SVO_HOST_COPY_THREADS")) n = std::atoi(v);
+        const int n = c->host_copy_threads > 0 ? c->host_copy_threads : (int)std::thread::hardware_concurrency() / 2;
         c->copy_pool.reset(new CopyPool(std::max(1, std::min(n, 16))));
     }
     struct Part { char *dst; const char *dev; char *stage; size_t bytes; };
@@ -2059,6 +2285,12 @@ int svo_render(svo_ctx *ctx, int width, int height, int stack_mode, float *rgba_
         HIP_TRY(hipEventRecord(c->stage_ev[n_chunks], c->stream));
     }
     CopyPool &pool = *c->copy_pool;
+    // every exit waits for the copy threads: none may still write the caller's arrays, or read the
+    // staging, once this call has returned (an error included)
+    struct WaitPool {
+        CopyPool &p;
+        ~WaitPool() { p.wait(); }
+    } wait_pool{pool};
     for (int i = 0; i < n_chunks; ++i) {
         HIP_TRY(hipEventSynchronize(c->stage_ev[i]));
         const size_t lo = (size_t)i * chunk, hi = std::min(total, lo + chunk);
@@ -2067,7 +2299,6 @@ int svo_render(svo_ctx *ctx, int width, int height, int stack_mode, float *rgba_
             for (size_t o = 0; o < n; o += per) pool.submit(q.dst + off + o, q.stage + off + o, std::min(per, n - o));
         });
     }
-    pool.wait();
     return SVO_OK;
 }
 
@@ -2386,6 +2617,12 @@ int svo_synchronize(svo_ctx *ctx) {
     }
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipDeviceSynchronize());   // the context's stream and every caller stream it rendered on
+    // nothing is pending on any stream now, and a caller may destroy its streams (svo_rt.h): the
+    // context records no event on a stream it saw before this point (an eviction of its
+    // dispatch-order set skips the hand-over event; the host-path scratch needs no ordering)
+    for (Sched &q : ctx->sched) q.idle = true;
+    ctx->scratch_valid = false;
+    ctx->scratch_stream = nullptr;
     return SVO_OK;
 }
 

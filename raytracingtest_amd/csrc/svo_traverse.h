@@ -60,6 +60,7 @@ struct Outputs {
     unsigned long long *hitmask;   // per 8x8 tile of the render's rows (band-local tile index
                                    // (lr / 8) * tiles_x + x / 8): the wave's ballot of its hit lanes
     uint32_t *fetches;         // instrumented launch: descriptor fetches per ray
+    float *starts;             // diagnostics (svo_beam_starts): each primary ray's beam start, nothing else
     int frame_layout;          // 1: index by global row (full-frame buffers)
     // one sample blended into an RGBA32F accumulation (svo_render_samples with S = 1: the one-sample
     // launch itself, AddShader's blend in its epilogue): accum = colour * acc_a + accum * acc_b,

@@ -42,9 +42,10 @@ def _frame(hits=None, rgba=None, rgba8=None, compact=None, position=None, voxel=
 
 class RaytracingMaster:
     def __init__(self, device=0, capacity_nodes=REFERENCE_CAPACITY, maxLevel=5, sampleType=4, devices=None,
-                 band_rows=8):
+                 band_rows=8, config=None):
         """devices: list of HIP device indices for a multi-device context (devices[0]
-        displays; an index may repeat); None = the single device `device`."""
+        displays; an index may repeat); None = the single device `device`.
+        config: svo_config fields to set on the new context (set_config)."""
         self.devices = None if devices is None else [int(d) for d in devices]
         self.device = device if devices is None else self.devices[0]
         self.band_rows = int(band_rows)
@@ -56,6 +57,7 @@ class RaytracingMaster:
         self._c2w = None
         self._options = 0               # svo_set_options bits
         self.currentSample = 0          # _currentSample (RaytracingMaster.cs:12)
+        self._config = dict(config or {})
         self.InitializeSVOBuffer()
 
     # ------------------------------------------------------------------ setup
@@ -71,6 +73,30 @@ class RaytracingMaster:
             check(L.svo_create_multi(arr, len(self.devices), self.capacity_nodes, self.band_rows,
                                      ctypes.byref(self._ctx)), "svo_create_multi")
         self._options = 0
+        if self._config:
+            self.set_config(**self._config)
+
+    def get_config(self):
+        """The context's svo_config (render policy) as a dict."""
+        c = _lib.SvoConfig()
+        c.size = ctypes.sizeof(_lib.SvoConfig)
+        check(_lib.lib().svo_get_config(self._ctx, ctypes.byref(c)), "svo_get_config")
+        return c.to_dict()
+
+    def set_config(self, **fields):
+        """Change svo_config fields (include/svo_rt.h; the counterpart of RaytracingMaster's Inspector
+        fields, RaytracingMaster.cs:16-18): the others keep their values.  Policy only -- every
+        setting renders the same frames."""
+        c = _lib.SvoConfig()
+        c.size = ctypes.sizeof(_lib.SvoConfig)
+        check(_lib.lib().svo_get_config(self._ctx, ctypes.byref(c)), "svo_get_config")
+        names = {n for n, _ in _lib.CONFIG_FIELDS}
+        for k, v in fields.items():
+            if k not in names:
+                raise SvoError(f"svo_config has no field {k!r}")
+            setattr(c, k, v)
+        check(_lib.lib().svo_set_config(self._ctx, ctypes.byref(c)), "svo_set_config")
+        self._config.update(fields)
 
     def SetSVOBuffer(self, data=None, offset=0):
         """Upload an SVOData at descriptor `offset`; with no data, build one from
@@ -313,6 +339,12 @@ class RaytracingMaster:
         b = ctypes.byref(band if isinstance(band, _lib.SvoBand) else make_band(band))
         check(_lib.lib().svo_pack_hits(self._ctx, width, height, b, rgb8, part, stream), "svo_pack_hits")
 
+    def beam_starts_device(self, width, height, starts_ptr, band=None, stream=None):
+        """svo_beam_starts: every primary ray's beam start (SVO-space t, -inf: the cube entry) into a
+        device float buffer of the band's pixels (diagnostics)."""
+        b = None if band is None else ctypes.byref(make_band(band))
+        check(_lib.lib().svo_beam_starts(self._ctx, width, height, b, starts_ptr, stream), "svo_beam_starts")
+
     def count_fetches_device(self, width, height, fetch_ptr, stack_mode=STACK_HLSL, band=None, stream=None):
         b = None if band is None else ctypes.byref(make_band(band))
         check(_lib.lib().svo_count_fetches(self._ctx, width, height, stack_mode, b, fetch_ptr, stream),
@@ -368,6 +400,7 @@ class _MemberView(RaytracingMaster):
         self._owner = owner
         self._ctx = ctx
         self._options = owner._options
+        self._config = dict(owner._config)
         self.currentSample = 0
         self._c2w = None
         self.devices = None

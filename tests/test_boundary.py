@@ -41,7 +41,7 @@ def test_exports_every_declared_symbol(native):
 
 def test_abi_version_and_error_text(native):
     from raytracingtest_amd import _lib
-    assert native.svo_abi_version() == _lib.ABI_VERSION == 9
+    assert native.svo_abi_version() == _lib.ABI_VERSION == 10
     assert isinstance(native.svo_last_error(), bytes)
 
 
@@ -154,3 +154,71 @@ def test_profile_key_does_not_depend_on_the_tree_location(tmp_path):
     here = subprocess.run([sys.executable, "-c", code, ROOT], capture_output=True, text=True, check=True).stdout
     there = subprocess.run([sys.executable, "-c", code, str(dst)], capture_output=True, text=True, check=True).stdout
     assert here.strip() and here == there
+
+
+CONFIG_DEFAULTS = {
+    "tile_order": 1, "xcd_strips": 1, "issue_priority": 1, "order_every": 32, "move_every": 4, "move_spread": 1,
+    "relayout": 1, "fetch_all": -1, "loop_form": -1, "lat_ratio": 0.3, "segments": 1, "seg_table_latency": 0x444,
+    "seg_table_issue": 0x4, "seg_table_thin": 0x888, "seg_ratio": 0.28, "seg_thin_ratio": 0.083, "seg_cap": 96,
+    "seg_min_chain": 160, "seg_move": 2, "seg_jitter": 2, "seg_all": 0, "seg_scramble": 0, "beam": 1, "beam_back": 2,
+    "shadow_form": 0, "shadow_order": 1, "readback": 0, "host_copy_threads": 0, "sparse_payload": 0, "peer_copy": 0}
+
+
+def test_config_struct_size_version_and_layout(tmp_path):
+    """svo_config (ABI 10): the ctypes mirror has the header's size, version and every field at the
+    header's offset (the C# shim's StructLayout(Sequential) follows the same order)."""
+    from raytracingtest_amd import _lib
+    fields = [n for n, _ in _lib.CONFIG_FIELDS]
+    src = tmp_path / "cfg.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "svo_rt.h"\nint main(void) {\n'
+                   '  printf("%zu %d\\n", sizeof(svo_config), SVO_CONFIG_VERSION);\n' +
+                   "".join(f'  printf("%zu\\n", offsetof(svo_config, {f}));\n' for f in fields) +
+                   '  return 0;\n}\n')
+    exe = tmp_path / "cfg"
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                    str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert int(out[0]) == ctypes.sizeof(_lib.SvoConfig) == 128
+    assert int(out[1]) == _lib.CONFIG_VERSION == 1
+    for f, off in zip(fields, out[2:]):
+        assert int(off) == getattr(_lib.SvoConfig, f).offset, f
+    # every field is documented in INTEGRATION.md's config table and declared in the header
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    header = open(HEADER).read()
+    for f in fields:
+        assert f"`{f}`" in doc, f"INTEGRATION.md does not document {f}"
+        assert re.search(rf"\b{f};", header), f
+
+
+def test_config_defaults_and_size_versioning_without_gpu(native):
+    """svo_get_config(NULL) gives the documented defaults (no device touched); a config smaller than
+    size + version, or larger than this library's, is rejected; a shorter (older) struct is filled
+    only up to its size."""
+    from raytracingtest_amd import _lib
+    got = _lib.default_config()
+    for k, v in CONFIG_DEFAULTS.items():
+        assert got[k] == pytest.approx(v), k
+    assert set(got) == set(CONFIG_DEFAULTS)
+    c = _lib.SvoConfig()
+    c.size = 4
+    assert native.svo_get_config(None, ctypes.byref(c)) == -1
+    assert native.svo_set_config(None, ctypes.byref(c)) == -1
+    # an older caller's struct: only the first 16 bytes (size, version, tile_order, xcd_strips)
+    buf = (ctypes.c_uint8 * 128)(*([0xEE] * 128))
+    hdr = ctypes.cast(buf, ctypes.POINTER(_lib.SvoConfig))
+    hdr.contents.size = 16
+    assert native.svo_get_config(None, hdr) == 0
+    assert hdr.contents.size == 16 and hdr.contents.version == 1
+    assert hdr.contents.tile_order == 1 and hdr.contents.xcd_strips == 1
+    assert all(b == 0xEE for b in bytes(buf)[16:]), "wrote past the caller's size"
+
+
+def test_library_reads_no_policy_from_the_environment():
+    """policy travels in svo_config; the library's getenv calls are the four
+    diagnostic switches (traces, the wave log, the splat's and the occupancy sweep's timing aids)."""
+    names = []
+    for f in ("svo_rt.hip", "svo_kernel.hip", "svo_build.hip"):
+        text = open(os.path.join(ROOT, "raytracingtest_amd", "csrc", f)).read()
+        names += re.findall(r"getenv\(\s*\"(\w+)\"", text)
+        assert text.count("getenv(") == len(re.findall(r"getenv\(\s*\"\w+\"", text)), f
+    assert sorted(names) == ["SVO_BEAM_DIAG", "SVO_DEBUG", "SVO_LDS_PAD", "SVO_WAVE_LOG"]

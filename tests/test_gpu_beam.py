@@ -13,7 +13,7 @@ import pytest
 
 from raytracingtest_amd import RaytracingMaster
 from raytracingtest_amd.builder import build_menger
-from raytracingtest_amd.camera import CAMERAS, Camera, main_light, overview_camera
+from raytracingtest_amd.camera import CAMERAS, Camera, look_rotation, main_light, overview_camera
 
 from test_gpu_frame import _bufs, _check, _oracle
 
@@ -80,14 +80,16 @@ def test_beam_starts_match_oracle_c3_poses(torch, oracle_mod, c3_svo, mode):
         m.close()
 
 
-@pytest.mark.parametrize("back", ["0", "1", "4", "9"])
-def test_every_splat_depth_matches_oracle(torch, oracle_mod, monkeypatch, c3_svo, back):
-    """Boxes from the leaves themselves (0) up to depth 1 (9): the bound only gets looser."""
-    monkeypatch.setenv("SVO_BEAM_BACK", back)
+@pytest.mark.parametrize("back", [0, 1, 4, 9])
+def test_every_splat_depth_matches_oracle(torch, oracle_mod, c3_svo, back):
+    """Boxes from the leaves themselves (0) up to depth 1 (9): the bound only gets looser.  The
+    splat depth is set after the upload, so the context rebuilds the pool's splat list from its
+    device copy (svo_set_config)."""
     w, h = 480, 270
     m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
     try:
         m.SetSVOBuffer(c3_svo)
+        m.set_config(beam_back=back)
         for name in ("flyover", "main", "buried"):
             cam = _cams()[name]
             m.UpdateShaderParameters(cam, w, h)
@@ -115,14 +117,13 @@ def test_pixel_offsets_at_the_ends_of_the_range(torch, oracle_mod, c3_svo, off):
         m.close()
 
 
-def test_beam_on_and_off_give_identical_frames(torch, monkeypatch, c3_svo):
+def test_beam_on_and_off_give_identical_frames(torch, c3_svo):
     """The full C3 bench frame (1920x1080, flyover and Main.unity poses): the beam-started launch and
     the continuous one write the same bytes in every output."""
     w, h = 1920, 1080
     out = {}
-    for beam in ("1", "0"):
-        monkeypatch.setenv("SVO_BEAM", beam)
-        m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+    for beam in (1, 0):
+        m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo), config={"beam": beam})
         try:
             m.SetSVOBuffer(c3_svo)
             for name in ("flyover", "main"):
@@ -133,7 +134,7 @@ def test_beam_on_and_off_give_identical_frames(torch, monkeypatch, c3_svo):
         finally:
             m.close()
     for name in ("flyover", "main"):
-        for on, off in zip(out[("1", name)], out[("0", name)]):
+        for on, off in zip(out[(1, name)], out[(0, name)]):
             for k in on:
                 assert on[k] == off[k], f"{name}: output {k} differs with beam starts"
 
@@ -213,3 +214,111 @@ def test_views_and_held_bursts_without_host_sync(torch, oracle_mod, c3_svo):
                 raise AssertionError(f"frame {k} (view {v}): {e}") from None
     finally:
         m.close()
+
+
+def _sweep_cameras(n=64, seed=0xBEA4):
+    """n seeded random cameras around the C3 cube ([-16, 16]^3 world): eyes above the terrain inside
+    the cube, below it (inside solid ground), just outside a face (boxes crossing the camera plane)
+    and far outside; look-at points in the cube or near-axis directions (within 1e-2..1e-5 rad of
+    an axis, some exactly on it); vertical FOV 10..170 degrees; a pixel offset anywhere in [0, 1]^2
+    (the ends of the range included)."""
+    rng = np.random.default_rng(seed)
+    cams = []
+    for i in range(n):
+        kind = i % 4
+        if kind == 0:     # inside the cube, above the terrain
+            eye = rng.uniform([-15, 2, -15], [15, 15.5, 15])
+        elif kind == 1:   # inside the cube, under the terrain surface
+            eye = rng.uniform([-15, -15.5, -15], [15, -6, 15])
+        elif kind == 2:   # just outside a face: the nearest boxes straddle the camera plane
+            eye = rng.uniform(-15, 15, 3)
+            ax = rng.integers(3)
+            eye[ax] = rng.choice([-1, 1]) * rng.uniform(16.0, 16.5)
+        else:             # far outside
+            d = rng.normal(size=3)
+            eye = d / np.linalg.norm(d) * rng.uniform(40, 600)
+        if rng.random() < 0.3:   # near an axis direction
+            fwd = np.zeros(3)
+            fwd[rng.integers(3)] = rng.choice([-1.0, 1.0])
+            eps = 0.0 if rng.random() < 0.3 else 10.0 ** rng.uniform(-5, -2)
+            fwd = fwd + eps * rng.normal(size=3)
+            if abs(fwd[1]) > 0.99:   # LookRotation's up vector must not be parallel
+                fwd[0] += 1e-3
+        else:
+            fwd = rng.uniform(-12, 12, 3) - eye
+        fov = float(rng.uniform(10, 170))
+        off = rng.random(2)
+        if i % 8 == 3:
+            off = np.array([float(rng.integers(2)), float(rng.integers(2))])
+        cams.append((Camera(position=tuple(eye), rotation=look_rotation(fwd), fov=fov), tuple(float(v) for v in off)))
+    return cams
+
+
+def test_beam_bound_random_camera_sweep(torch, oracle_mod, c3_svo):
+    """the beam bound's conservativeness swept once over 64 seeded random cameras
+    on the C3 pool at 256x144 (eyes inside / under / just outside / far outside the cube, FOV
+    10..170 degrees, boxes across the camera plane, near-axis views, offsets in [0, 1]^2), both
+    stack modes: every record equals the oracle's IntersectSVO (NVIDIASVO.compute:40-54,66-69 is
+    where the walk starts), and on every hit ray the start the kernel used (svo_beam_starts) is at
+    or below the oracle's f32 hit t.  The minimum slack, in units of the start's rounding margin
+    (2 sum|coef| + sum|bias|) 2^-20, is reported (SVO_BEAM_SWEEP_OUT=<file> writes
+    the summary)."""
+    import json
+    import os
+    w, h = 256, 144
+    m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+    starts = torch.empty(w * h, dtype=torch.float32, device="cuda")
+    summary = {"cameras": 0, "rays": 0, "hit_rays": 0, "beam_rays": 0, "min_slack_margins": None,
+               "min_slack_rel": None, "per_camera": []}
+    try:
+        m.SetSVOBuffer(c3_svo)
+        for i, (cam, off) in enumerate(_sweep_cameras()):
+            m.UpdateShaderParameters(cam, w, h, pixel_offset=off)
+            m.beam_starts_device(w, h, starts.data_ptr())
+            m.synchronize()
+            st = starts.cpu().numpy().astype(np.float64)
+            for mode in (0, 1):
+                ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, c3_svo, cam, w, h, mode, off=off)
+                b = _render(torch, m, w, h, mode, keys=("hits", "rgba"))
+                try:
+                    _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+                except AssertionError as e:
+                    raise AssertionError(f"camera {i} mode {mode} ({cam.position}, fov {cam.fov:.1f}, off {off}): {e}") from None
+                hit = (ref_hits["flags"] & 1) != 0
+                t_svo = ref_hits["t"].astype(np.float64) / 2048.0   # bestHit.distance = 2048 t_min, exact
+                sel = hit & np.isfinite(st)
+                bad = np.flatnonzero(sel & (st > t_svo))
+                assert len(bad) == 0, f"camera {i} mode {mode}: {len(bad)} hit rays start past their hit"
+                if mode == 0 and sel.any():
+                    # the start's rounding margin per ray, from the ray setup in float64
+                    c2w, ip = (np.asarray(a, np.float64) for a in cam.uniforms(w, h))
+                    px = (np.arange(w * h) % w + off[0]) / w * 2 - 1
+                    py = (np.arange(w * h) // w + off[1]) / h * 2 - 1
+                    v = ip @ np.stack([px, py, np.zeros_like(px), np.ones_like(px)])
+                    d = (c2w[:3, :3] @ v[:3]).T
+                    d /= np.linalg.norm(d, axis=1, keepdims=True)
+                    o = c2w[:3, 3] / 32 + 1.5
+                    with np.errstate(divide="ignore"):
+                        coef = 1.0 / np.abs(d)
+                    margin = (2 * coef.sum(1) + (coef * o[None, :]).sum(1)) * 2.0 ** -20
+                    slack = (t_svo - st)[sel] / margin[sel]
+                    rel = ((t_svo - st) / t_svo)[sel]
+                    mn, mr = float(np.min(slack)), float(np.min(rel))
+                    summary["per_camera"].append({"eye": [round(float(x), 3) for x in cam.position],
+                                                  "fov": round(cam.fov, 2), "off": off, "hit_rays": int(hit.sum()),
+                                                  "beam_rays": int(sel.sum()), "min_slack_margins": round(mn, 3)})
+                    summary["min_slack_margins"] = mn if summary["min_slack_margins"] is None else min(mn, summary["min_slack_margins"])
+                    summary["min_slack_rel"] = mr if summary["min_slack_rel"] is None else min(mr, summary["min_slack_rel"])
+                    summary["beam_rays"] += int(sel.sum())
+                if mode == 0:
+                    summary["hit_rays"] += int(hit.sum())
+            summary["cameras"] += 1
+            summary["rays"] += w * h
+    finally:
+        m.close()
+    assert summary["cameras"] == 64 and summary["beam_rays"] > 0
+    if os.environ.get("SVO_BEAM_SWEEP_OUT"):
+        with open(os.environ["SVO_BEAM_SWEEP_OUT"], "w") as fh:
+            json.dump(summary, fh, indent=1)
+    print(f"beam sweep: {summary['beam_rays']} beam-started hit rays over {summary['cameras']} cameras, "
+          f"min slack {summary['min_slack_margins']:.3f} margins ({summary['min_slack_rel']:.3e} relative)")

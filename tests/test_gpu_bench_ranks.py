@@ -80,12 +80,11 @@ def test_two_ranks_assemble_the_whole_frame(gpu, payload):
 def test_multidevice_bench_like_for_like(gpu, copy):
     """bench.py --gpus 2 without torchrun (the multi-device context, both members on
     cuda:0): the step leaves hit records + RGBA32F + RGBA8 of the whole frame on the
-    display device, every output equal to a one-launch render; SVO_PEER_COPY=1 takes
+    display device, every output equal to a one-launch render; svo_config.peer_copy 1 takes
     the copy fallback a member without peer access gets (svo_create_multi)."""
-    env = dict(os.environ, SVO_PEER_COPY="1" if copy else "0")
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--devices", "0,0", "--steps", "6", "--warmup", "2",
-           "--cpu-seconds", "0", "--no-extras"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+           "--cpu-seconds", "0", "--no-extras", "--set", f"peer_copy={1 if copy else 0}"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["scaling"] == "strong" and d["roofline"]["achieved"] > 0

@@ -17,7 +17,7 @@ import pytest
 from raytracingtest_amd import HIT_DTYPE, RaytracingMaster, SvoError, band_rows
 from raytracingtest_amd import _lib
 from raytracingtest_amd.builder import build_menger
-from raytracingtest_amd.camera import Camera, look_rotation, main_camera, main_light, overview_camera
+from raytracingtest_amd.camera import CAMERAS, Camera, look_rotation, main_camera, main_light, overview_camera
 from raytracingtest_amd.svo_data import SVOData
 
 pytestmark = pytest.mark.gpu
@@ -250,19 +250,18 @@ def test_multi_device_payload_regrowth_across_streams(torch, oracle_mod):
 
 
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0, 0]])
-def test_multi_device_sparse_payload(torch, oracle_mod, monkeypatch, devices):
-    """SVO_SPARSE_PAYLOAD=1: the multi-device context's display-only frames travel as
+def test_multi_device_sparse_payload(torch, oracle_mod, devices):
+    """svo_config.sparse_payload 1: the multi-device context's display-only frames travel as
     sparse parts (masks + offsets + hit RGB, packed on each member) that the display
     member's assemble pulls with no host round trip -- round-robin and weighted
     deals, frames alternating cameras (a stale part would show), bit-identical to
     the oracle."""
     from raytracingtest_amd.distributed import weighted_owner
-    monkeypatch.setenv("SVO_SPARSE_PAYLOAD", "1")
     svo = build_menger(8)
     w, h = 333, 250
     cams = [overview_camera(), Camera(position=(30.0, 12.0, -25.0), rotation=look_rotation((-30.0, -12.0, 25.0)))]
     refs = [_oracle(oracle_mod, svo, c, w, h) for c in cams]
-    m = RaytracingMaster(devices=devices, capacity_nodes=len(svo))
+    m = RaytracingMaster(devices=devices, capacity_nodes=len(svo), config={"sparse_payload": 1})
     try:
         m.SetSVOBuffer(svo)
         for owner in (None, weighted_owner(len(devices), 3 / 8)):
@@ -316,17 +315,16 @@ def test_multi_device_weighted_deal(torch, oracle_mod):
 
 
 @pytest.mark.parametrize("compact", [False, True])
-def test_multi_device_shadow_rays(torch, oracle_mod, monkeypatch, compact):
+def test_multi_device_shadow_rays(torch, oracle_mod, compact):
     """The C3 '+1 shadow ray' frame through the multi-device context: the
     occlusion flag travels in the compact record and the display member
     rebuilds the black Result."""
     svo = build_menger(8)
     w, h = 400, 240
     cam = overview_camera()
-    if compact:   # every member's shadow pass over its bands' compacted hit list
-        monkeypatch.setenv("SVO_SHADOW_COMPACT", "1")
     ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h, shadows=True)
-    m = RaytracingMaster(devices=[0, 0, 0], capacity_nodes=len(svo))
+    # compact: every member's shadow pass over its bands' compacted hit list
+    m = RaytracingMaster(devices=[0, 0, 0], capacity_nodes=len(svo), config={"shadow_form": 2 if compact else 0})
     try:
         m.SetSVOBuffer(svo)
         m.UpdateShaderParameters(cam, w, h)
@@ -616,15 +614,10 @@ def test_two_streams_every_pixel_written(torch, oracle_mod, n_streams):
     """Launches of one context cycling over several streams (advisor r1): each
     stream has its own dispatch-order state (up to 4; a fifth stream takes over
     the least recently used set after that stream's renders), the orders are
-    rebuilt every launch (SVO_ORDER_EVERY=1), the renders run concurrently, and
+    rebuilt every launch (order_every 1), the renders run concurrently, and
     every frame is still complete and equal to the oracle's."""
-    import os
-    os.environ["SVO_ORDER_EVERY"] = "1"
-    try:
-        svo = build_menger(8)
-        m = RaytracingMaster(device=0, capacity_nodes=len(svo))
-    finally:
-        del os.environ["SVO_ORDER_EVERY"]
+    svo = build_menger(8)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo), config={"order_every": 1})
     w, h = 640, 360
     cam = overview_camera()
     ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
@@ -668,6 +661,141 @@ def test_forgotten_streams_destroyed_then_new_ones(torch, oracle_mod):
                 _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
             del streams
         m.forget_stream(torch.cuda.Stream().cuda_stream)
+    finally:
+        m.close()
+
+
+def _hip_runtime():
+    """The HIP runtime this process already loaded (torch's or /opt/rocm's: one soname), for raw
+    stream handles that a test can really destroy (torch pools its streams and never does)."""
+    import ctypes
+    path = None
+    with open("/proc/self/maps") as fh:
+        for line in fh:
+            if "libamdhip64" in line:
+                path = line.split()[-1]
+                break
+    assert path, "no HIP runtime loaded"
+    hip = ctypes.CDLL(path)
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    return hip
+
+
+@pytest.mark.parametrize("release", ["synchronize", "forget"])
+def test_raw_streams_destroyed_after_forget_or_synchronize(torch, oracle_mod, release):
+    """a host that follows the stream-lifetime rule (svo_rt.h) -- svo_synchronize, or
+    svo_forget_stream per stream, then hipStreamDestroy -- and renders on fresh streams until the
+    dispatch-order sets are evicted (six streams after four) and the host-path scratch moves (the
+    two-pass shadow form without caller hit records uses it, then svo_render on the context's own
+    stream): no event may land on a destroyed handle (HIP may hand the same value to a new stream),
+    and every frame equals the oracle's.  Raw hipStreamCreate handles, really destroyed."""
+    import ctypes
+    hip = _hip_runtime()
+    svo = build_menger(8)
+    w, h = 320, 184
+    cam = overview_camera()
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+    sh_hits, sh_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h, shadows=True)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo), config={"shadow_form": 1})
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        for generation in range(3):
+            streams = []
+            for _ in range(4 if generation == 0 else 6):
+                hs = ctypes.c_void_p()
+                assert hip.hipStreamCreate(ctypes.byref(hs)) == 0
+                streams.append(hs.value)
+            outs = [_bufs(torch, w * h) for _ in range(2 * len(streams))]
+            for i, b in enumerate(outs):
+                m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr(),
+                               stream=streams[i % len(streams)])
+            # the scratch: shadow rays as a second pass need records the caller did not ask for
+            m.SetShadowRays(True)
+            sh = _bufs(torch, w * h)
+            m.render_frame(w, h, rgba=sh["rgba"].data_ptr(), stream=streams[0])
+            m.SetShadowRays(False)
+            if release == "synchronize":
+                m.synchronize()
+            else:
+                for st in streams:
+                    m.forget_stream(st)
+            for st in streams:
+                assert hip.hipStreamDestroy(st) == 0
+            for b in outs:
+                _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+            assert sh["rgba"].cpu().numpy().tobytes() == sh_rgba.astype(np.float32).tobytes()
+            rgba, hits = m.Render(w, h)   # the context's own stream takes the scratch over
+            assert hits.tobytes() == ref_hits.tobytes()
+    finally:
+        m.close()
+
+
+def test_config_change_takes_effect(torch, oracle_mod, monkeypatch, capfd):
+    """policy set through the ABI (svo_set_config) on a live context, with no
+    policy environment variable, changes what the next launches do -- beam starts off / on (the
+    starts svo_beam_starts reports and the fetches the beam-started walk makes), the segment class
+    table each launch dispatches in (the SVO_DEBUG order trace, a diagnostic), the readback form --
+    while every frame stays the oracle's; out-of-range fields are refused and change nothing."""
+    import re
+    from raytracingtest_amd import _lib
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    monkeypatch.setenv("SVO_DEBUG", "2")   # diagnostics only: the order trace
+    svo = build_sampler_svo(4, 11)   # C3's pool and frame: heavy chains, so every class table applies
+    w, h = 1920, 1080
+    cam = CAMERAS["flyover"]()
+    ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, svo, cam, w, h)
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    try:
+        m.SetSVOBuffer(svo)
+        m.UpdateShaderParameters(cam, w, h)
+        assert m.get_config() == _lib.default_config()
+        starts = torch.empty(w * h, dtype=torch.float32, device="cuda")
+        fetch = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+
+        def probe():
+            m.beam_starts_device(w, h, starts.data_ptr())
+            m.set_count_beam(True)
+            m.count_fetches_device(w, h, fetch.data_ptr())
+            m.set_count_beam(False)
+            m.synchronize()
+            return int(np.isfinite(starts.cpu().numpy()).sum()), int(fetch.to(torch.int64).sum().item())
+
+        def frames(n=4):
+            capfd.readouterr()
+            for _ in range(n):
+                b = _bufs(torch, w * h)
+                m.render_frame(w, h, hits=b["hits"].data_ptr(), rgba=b["rgba"].data_ptr())
+                m.synchronize()
+                _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+            return [int(k, 16) for k in re.findall(r"svo order: .* kpack ([0-9a-f]+) ", capfd.readouterr().err)]
+
+        beam_rays, beam_fetches = probe()
+        assert beam_rays > 0
+        frames()
+        m.set_config(beam=0)
+        off_rays, off_fetches = probe()
+        assert off_rays == 0 and off_fetches > beam_fetches   # every ray from the cube entry
+        frames()
+        m.set_config(beam=1, beam_back=1)                     # rebuilt from the device copy
+        back_rays, back_fetches = probe()
+        assert 0 < back_rays <= beam_rays and back_fetches < off_fetches
+        m.set_config(seg_table_issue=0x888, seg_table_latency=0x888, seg_table_thin=0x888)
+        assert frames(6)[-1] == 0x888
+        m.set_config(segments=0)
+        assert frames(3)[-1] == 0
+        before = m.get_config()
+        for bad in ({"seg_table_issue": 0x5}, {"order_every": 0}, {"shadow_form": 3}, {"lat_ratio": float("nan")}):
+            with pytest.raises(SvoError):
+                m.set_config(**bad)
+            assert m.get_config() == before
+        m.set_config(readback=2)
+        m.RenderProgressiveAsync(w, h)
+        m.RenderProgressiveAsync(w, h)
+        got = m.ProgressiveLast(w, h)
+        assert got is not None and got.shape == (h, w)
     finally:
         m.close()
 
@@ -1111,17 +1239,16 @@ def test_render_samples_multi_device(torch, oracle_mod, devices):
 
 
 @pytest.mark.parametrize("move_every", [1, 4])
-def test_moving_camera_frames_match_oracle(torch, oracle_mod, monkeypatch, move_every):
+def test_moving_camera_frames_match_oracle(torch, oracle_mod, move_every):
     """A camera that moves every frame (the interactive case, RaytracingMaster.cs:55-74): the
     dispatch order is rebuilt every move_every-th frame from older views' costs (svo_rt.hip
-    launch, SVO_MOVE_EVERY), then the pan stops and the held view gets its own order.  Placement
+    launch, svo_config.move_every), then the pan stops and the held view gets its own order.  Placement
     only: every frame equals the oracle's frame for its own view, and so does the held one."""
-    monkeypatch.setenv("SVO_MOVE_EVERY", str(move_every))
     svo = build_menger(8)
     w, h = 320, 184
     eyes = [(4.0 * np.sin(0.05 * i), 20.0, -40.0 + 3.0 * i) for i in range(7)]
     cams = [overview_camera(e, (0.0, 0.0, 0.0)) for e in eyes]
-    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo), config={"move_every": move_every})
     try:
         m.SetSVOBuffer(svo)
         bufs = [_bufs(torch, w * h) for _ in cams]

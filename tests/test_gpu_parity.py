@@ -4,6 +4,8 @@ Bar (BASELINE.json north_star): hit voxel (parent, hit_idx, hit_scale, flags)
 bit-exact; t and normal within 1e-5 relative -- asserted bit-exact here since
 kernel and oracle share the strict-IEEE op order; RGBA of hit pixels within
 rtol 1e-5 (miss colour is the procedural sky stand-in, also compared)."""
+import re
+
 import numpy as np
 import pytest
 
@@ -194,24 +196,22 @@ def test_errors_are_loud(rm):
         m.close()
 
 
-@pytest.mark.parametrize("env", [
-    {"SVO_XCD_REMAP": "0"}, {"SVO_TILE_ORDER": "0"}, {"SVO_PRIO": "0"}, {"SVO_FETCH_ALL": "0"},
-    {"SVO_FETCH_ALL": "1"}, {"SVO_ORDER_EVERY": "1"}, {"SVO_SHADOW_ORDER": "0", "SVO_FUSED_SHADOWS": "0"},
-    {"SVO_SHADOW_COMPACT": "1"}, {"SVO_LAT": "1"}, {"SVO_LAT": "0"}, {"SVO_LAT_RATIO": "1000"}])
-def test_runtime_switches_identical(oracle_mod, monkeypatch, env):
-    """Every surviving placement / loop-form switch (svo_rt.hip svo_create; the
+@pytest.mark.parametrize("cfg", [
+    {"xcd_strips": 0}, {"tile_order": 0}, {"issue_priority": 0}, {"fetch_all": 0},
+    {"fetch_all": 1}, {"order_every": 1}, {"shadow_order": 0, "shadow_form": 1},
+    {"shadow_form": 2}, {"loop_form": 1}, {"loop_form": 0}, {"lat_ratio": 1000.0}])
+def test_runtime_switches_identical(oracle_mod, cfg):
+    """Every surviving placement / loop-form switch of svo_config (svo_set_config; the
     loop forms and block shapes measured slower in round 1 were removed) gives
     the oracle's frame, over repeated (cost-ordered) launches, with and without
     shadow rays."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     svo = build_menger(7)
     cam = overview_camera()
     w, h = 520, 264
-    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo), config=cfg)
     try:
         m.SetSVOBuffer(svo)
         m.UpdateShaderParameters(cam, w, h)
@@ -225,8 +225,8 @@ def test_runtime_switches_identical(oracle_mod, monkeypatch, env):
         m.close()
 
 
-@pytest.mark.parametrize("lat", ["0", "1"])
-def test_degenerate_frame_sizes(oracle_mod, monkeypatch, lat):
+@pytest.mark.parametrize("lat", [0, 1])
+def test_degenerate_frame_sizes(oracle_mod, lat):
     """Frames far from the 8x8 tile grid (one pixel, one row, one column, partial
     tiles on both edges) in both loop forms, with and without the fused shadow
     rays, over repeated (cost-ordered) launches: every record equals the oracle's.
@@ -234,9 +234,8 @@ def test_degenerate_frame_sizes(oracle_mod, monkeypatch, lat):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    monkeypatch.setenv("SVO_LAT", lat)
     svo = build_menger(7)
-    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo), config={"loop_form": lat})
     try:
         m.SetSVOBuffer(svo)
         for cam in (main_camera(), overview_camera()):
@@ -282,20 +281,18 @@ def test_shadow_rays_parity(rm, oracle_mod, mode):
 
 
 @pytest.mark.parametrize("form", ["two_pass", "fused", "compact"])
-def test_shadow_pass_forms_identical(oracle_mod, monkeypatch, form):
+def test_shadow_pass_forms_identical(oracle_mod, form):
     """The shadow rays as a second cost-ordered launch over the tiles
-    (SVO_FUSED_SHADOWS=0), fused into the primary launch (default), and as a second
-    launch over the compacted hit list (SVO_SHADOW_COMPACT=1: ballot masks, prefix
+    (shadow_form 1), fused into the primary launch (0, the default), and as a second
+    launch over the compacted hit list (2: ballot masks, prefix
     sum, dense waves of 64 hits) give the oracle's frame, over repeated launches
     (the dispatch order is rebuilt from recorded costs) and with RGBA only."""
-    monkeypatch.setenv("SVO_FUSED_SHADOWS", "0" if form == "two_pass" else "1")
-    if form == "compact":
-        monkeypatch.setenv("SVO_SHADOW_COMPACT", "1")
     svo = build_menger(8)
     cam = overview_camera()
     w, h = 480, 272
     ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, svo, cam, w, h, 0, shadows=True)
-    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    form_id = {"fused": 0, "two_pass": 1, "compact": 2}[form]
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo), config={"shadow_form": form_id})
     try:
         m.SetSVOBuffer(svo)
         m.UpdateShaderParameters(cam, w, h)
@@ -444,7 +441,7 @@ def test_c1_golden_frames(rm, text_svo, mode, camera_name):
 
 
 @pytest.mark.parametrize("stack_mode", [0, 1])
-def test_loop_forms_identical_on_a_split_band(oracle_mod, monkeypatch, stack_mode):
+def test_loop_forms_identical_on_a_split_band(oracle_mod, stack_mode):
     """The two loop forms (lean; latency: the node kept in the stack entry, the next node
     loaded mid-trip) and the automatic choice between them (the order kernel's cost stats,
     svo_rt.hip launch) give the oracle's records on a strong-split band of a depth-9 terrain
@@ -461,12 +458,8 @@ def test_loop_forms_identical_on_a_split_band(oracle_mod, monkeypatch, stack_mod
     ys = band_rows(h, band)
     ref_hits, ref_rgba, _ = _oracle_render(oracle_mod, svo, cam, w, h, stack_mode)
     ref = ref_hits.reshape(h, w)[ys]
-    for lat in ("0", "1", None):
-        if lat is None:
-            monkeypatch.delenv("SVO_LAT", raising=False)
-        else:
-            monkeypatch.setenv("SVO_LAT", lat)
-        m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    for lat in (0, 1, -1):   # svo_config.loop_form: lean, latency, automatic
+        m = RaytracingMaster(device=0, capacity_nodes=len(svo), config={"loop_form": lat})
         try:
             m.SetSVOBuffer(svo)
             m.UpdateShaderParameters(cam, w, h)
@@ -475,9 +468,49 @@ def test_loop_forms_identical_on_a_split_band(oracle_mod, monkeypatch, stack_mod
                 m.render_device(w, h, hits_ptr=buf.data_ptr(), band=band, stack_mode=stack_mode)
                 m.synchronize()
                 got = buf.cpu().numpy().view(ref.dtype).reshape(len(ys), w)
-                assert got.tobytes() == ref.tobytes(), f"SVO_LAT={lat}"
+                assert got.tobytes() == ref.tobytes(), f"loop_form={lat}"
         finally:
             m.close()
+
+
+_DECISION = re.compile(r"svo lat: view (\d+) T \d+ M \d+ slots \d+ ratio ([0-9.]+) bound ([0-9.]+) "
+                       r"thin ([0-9.]+) beam (\d) -> (\w+)( thin)?")
+
+
+def _pose_decisions(monkeypatch, capfd, config, plan):
+    """Render the C3 frame at each pose of `plan` as a burst of 12 launches with no host sync (the
+    host runs ahead of the GPU) and return, per pose, the decisions the library's SVO_DEBUG trace
+    printed for that pose's view: (ratio, bound, thin_bound, beam, form, thin)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from raytracingtest_amd.camera import CAMERAS
+    from raytracingtest_amd.native_builder import build_sampler_svo
+    monkeypatch.setenv("SVO_DEBUG", "1")   # diagnostics only: the decision trace (read at svo_create)
+    svo = build_sampler_svo(4, 11)   # config C3's pool
+    w, h = 1920, 1080
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo), config=config)
+    out = []
+    try:
+        m.SetSVOBuffer(svo)
+        buf = torch.empty(w * h * 24, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        for view, pose in enumerate(plan, start=1):
+            capfd.readouterr()
+            m.UpdateShaderParameters(CAMERAS[pose](), w, h)
+            for _ in range(12):
+                m.render_device(w, h, hits_ptr=buf.data_ptr(), stack_mode=0)
+            m.synchronize()
+            err = capfd.readouterr().err
+            found = _DECISION.findall(err)
+            mine = [(float(r), float(b), float(tb), int(be), f, bool(th)) for v, r, b, tb, be, f, th in found
+                    if int(v) == view]
+            assert mine, f"no decision from view {view} ({pose}): {err[-2000:]}"
+            assert all(int(v) >= view - 1 for v, *_ in found), f"{pose}: stale decisions {found}"
+            out.append((pose, mine))
+    finally:
+        m.close()
+    return out
 
 
 def test_loop_form_choice_follows_the_pose(monkeypatch, capfd):
@@ -486,37 +519,31 @@ def test_loop_form_choice_follows_the_pose(monkeypatch, capfd):
     submitted as a burst of launches with no host sync (the host runs ahead of the GPU),
     every decision taken at a pose uses that pose's own costs -- the sky-heavy overview the
     latency form, the flyover and Main poses the lean loop (costs of the walk from
-    the cube entry, SVO_BEAM=0 -- beam starts shorten every wave but the heaviest and make the
-    flyover pose latency-bound too).  Reads the library's SVO_LAT_DEBUG trace."""
-    import re
-    torch = pytest.importorskip("torch")
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    from raytracingtest_amd.camera import CAMERAS
-    from raytracingtest_amd.native_builder import build_sampler_svo
-    monkeypatch.setenv("SVO_LAT_DEBUG", "1")
-    monkeypatch.setenv("SVO_BEAM", "0")
-    monkeypatch.delenv("SVO_LAT", raising=False)
-    monkeypatch.delenv("SVO_LAT_RATIO", raising=False)
-    svo = build_sampler_svo(4, 11)   # config C3's pool
-    w, h = 1920, 1080
-    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
-    try:
-        m.SetSVOBuffer(svo)
-        buf = torch.empty(w * h * 24, dtype=torch.uint8, device="cuda")
-        torch.cuda.synchronize()
-        plan = [("flyover", "lean"), ("overview", "latency"), ("main", "lean"), ("overview", "latency")]
-        for view, (pose, form) in enumerate(plan, start=1):
-            capfd.readouterr()
-            m.UpdateShaderParameters(CAMERAS[pose](), w, h)
-            for _ in range(12):
-                m.render_device(w, h, hits_ptr=buf.data_ptr(), stack_mode=0)
-            m.synchronize()
-            err = capfd.readouterr().err
-            decisions = re.findall(r"svo lat: view (\d+) .*-> (\w+)", err)
-            mine = [f for v, f in decisions if int(v) == view]
-            assert mine, f"no decision from view {view} ({pose}): {decisions}"
-            assert all(f == form for f in mine), f"{pose}: {decisions}"
-            assert all(int(v) >= view - 1 for v, _ in decisions), f"{pose}: stale decisions {decisions}"
-    finally:
-        m.close()
+    the cube entry, beam 0 -- beam starts shorten every wave but the heaviest and make the
+    flyover pose latency-bound too).  Reads the library's SVO_DEBUG decision trace."""
+    plan = ["flyover", "overview", "main", "overview"]
+    want = {"flyover": "lean", "overview": "latency", "main": "lean"}
+    for pose, mine in _pose_decisions(monkeypatch, capfd, {"beam": 0}, plan):
+        assert all(d[3] == 0 for d in mine)
+        assert all(d[4] == want[pose] for d in mine), f"{pose}: {mine}"
+
+
+def test_class_table_choice_follows_the_pose_with_beam_starts(monkeypatch, capfd):
+    """The default launch (beam starts on): the same jumps between the C3 poses, and each view's
+    class-table decision (issue-bound table, latency-bound table, or the thin table) is the current
+    rule applied to that view's own statistics (svo_rt.hip launch: latency-bound iff the summed
+    trips T < bound x slots x heaviest M -- bound = seg_ratio 0.28, x/÷ 1.15 once the geometry has a
+    decision -- and thin iff also below seg_thin_ratio 0.083): the trace's ratio, bound and form
+    agree.  Beside the rule, the poses far from a boundary take their table: the sky-heavy overview
+    (ratio ~0.06) the thin table, the Main.unity pose (~0.49) the issue-bound one."""
+    plan = ["flyover", "overview", "main", "overview", "flyover"]
+    for pose, mine in _pose_decisions(monkeypatch, capfd, None, plan):
+        for ratio, bound, thin_bound, beam, form, thin in mine:
+            assert beam == 1
+            assert (form == "latency") == (ratio < bound), f"{pose}: {mine}"
+            assert thin == (form == "latency" and ratio < thin_bound), f"{pose}: {mine}"
+        table = {"latency": "thin" if mine[-1][5] else "latency", "lean": "issue"}[mine[-1][4]]
+        if pose == "overview":
+            assert table == "thin", f"{pose}: {mine}"
+        if pose == "main":
+            assert table == "issue", f"{pose}: {mine}"

@@ -3,8 +3,8 @@
 A heavy tile's rays are traced as SEG_K t-segments side by side.  The
 form must give every output bit-identical to the continuous loop -- i.e. to the oracle's
 IntersectSVO (NVIDIASVO.compute:57-198) -- whatever the segment starts are.  Checked here
-with every tile segmented (SVO_SEG_ALL), with only the heavy classes (SVO_SEG, the form a
-launch uses), with arbitrary starts (SVO_SEG_SCRAMBLE: unordered, NaN, +-inf, outside the
+with every tile segmented (svo_config.seg_all), with only the heavy classes (the class tables, the
+form a launch uses), with arbitrary starts (seg_scramble: unordered, NaN, +-inf, outside the
 cube), over consecutive frames (the starts are rebalanced from frame to frame), a moving
 camera, a band of a split frame and the sparse payload's hit masks, in both stack modes.
 """
@@ -36,8 +36,8 @@ def c3_svo():
     return build_sampler_svo(cfg["sampler"], cfg["max_level"], device=0)
 
 
-def _frames(torch, oracle_mod, svo, cams, w, h, mode, n_frames=3, keys=None):
-    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+def _frames(torch, oracle_mod, svo, cams, w, h, mode, n_frames=3, keys=None, config=None):
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo), config=config)
     try:
         m.SetSVOBuffer(svo)
         for cam in cams:
@@ -54,41 +54,35 @@ def _frames(torch, oracle_mod, svo, cams, w, h, mode, n_frames=3, keys=None):
 
 
 @pytest.mark.parametrize("mode,k", [(0, 4), (1, 4), (0, 8), (1, 8)])
-def test_every_tile_segmented_matches_oracle(torch, oracle_mod, monkeypatch, text_svo, mode, k):
+def test_every_tile_segmented_matches_oracle(torch, oracle_mod, text_svo, mode, k):
     """Every tile traced as K = 4 or 8 segments per ray: every output of every frame equals the oracle."""
-    monkeypatch.setenv("SVO_SEG_ALL", str(k))
-    _frames(torch, oracle_mod, text_svo, [main_camera(), overview_camera()], 256, 256, mode)
-    _frames(torch, oracle_mod, build_menger(8), [overview_camera()], 480, 272, mode)
+    cfg = {"seg_all": k}
+    _frames(torch, oracle_mod, text_svo, [main_camera(), overview_camera()], 256, 256, mode, config=cfg)
+    _frames(torch, oracle_mod, build_menger(8), [overview_camera()], 480, 272, mode, config=cfg)
 
 
 @pytest.mark.parametrize("mode,k", [(0, 4), (1, 4), (0, 8), (1, 8)])
-def test_arbitrary_segment_starts_match_oracle(torch, oracle_mod, monkeypatch, mode, k):
+def test_arbitrary_segment_starts_match_oracle(torch, oracle_mod, mode, k):
     """Starts that are unordered, NaN, +-inf or outside the cube (a new hash every launch):
     the records do not depend on them."""
-    monkeypatch.setenv("SVO_SEG_ALL", str(k))
-    monkeypatch.setenv("SVO_SEG_SCRAMBLE", "12345")
     _frames(torch, oracle_mod, build_menger(8), [overview_camera()], 480, 272, mode, n_frames=4,
-            keys=("hits", "rgba", "position", "voxel"))
+            keys=("hits", "rgba", "position", "voxel"), config={"seg_all": k, "seg_scramble": 12345})
 
 
-@pytest.mark.parametrize("mode,table", [(0, "448"), (1, "448"), (0, "888")])
-def test_c3_heavy_tiles_segmented_full_frame(torch, oracle_mod, monkeypatch, c3_svo, mode, table):
+@pytest.mark.parametrize("mode,table", [(0, 0x448), (1, 0x448), (0, 0x888)])
+def test_c3_heavy_tiles_segmented_full_frame(torch, oracle_mod, c3_svo, mode, table):
     """The bench workload (C3, 1920x1080, flyover), each XCD's heaviest classes segmented as the
     launch's own rule does (the class table forced for every launch, K = 4 and 8 mixed): six
     consecutive frames, every ray equal to the oracle's."""
-    monkeypatch.setenv("SVO_SEG_LAT", table)
-    monkeypatch.setenv("SVO_SEG_ISSUE", table)
     w, h = 1920, 1080
-    _frames(torch, oracle_mod, c3_svo, [CAMERAS["flyover"]()], w, h, mode, n_frames=6, keys=("hits", "rgba"))
+    _frames(torch, oracle_mod, c3_svo, [CAMERAS["flyover"]()], w, h, mode, n_frames=6, keys=("hits", "rgba"),
+            config={"seg_table_latency": table, "seg_table_issue": table, "seg_table_thin": table})
 
 
-@pytest.mark.parametrize("seg_move", ["1", "2"])
-def test_c3_segmented_moving_camera(torch, oracle_mod, monkeypatch, c3_svo, seg_move):
-    """A pan (a new view per frame: even splits by default, under SVO_SEG_MOVE=1 the starts carried
+@pytest.mark.parametrize("seg_move", [1, 2])
+def test_c3_segmented_moving_camera(torch, oracle_mod, c3_svo, seg_move):
+    """A pan (a new view per frame: even splits by default, under seg_move 1 the starts carried
     over from the previous view), then held."""
-    monkeypatch.setenv("SVO_SEG_ISSUE", "488")
-    monkeypatch.setenv("SVO_MOVE_EVERY", "1")
-    monkeypatch.setenv("SVO_SEG_MOVE", seg_move)
     from raytracingtest_amd.camera import FLYOVER_EYE, FLYOVER_TARGET
     w, h = 1920, 1080
     cams = []
@@ -96,24 +90,24 @@ def test_c3_segmented_moving_camera(torch, oracle_mod, monkeypatch, c3_svo, seg_
         a = 0.01 * i
         eye = (FLYOVER_EYE[0] + 2.0 * np.sin(a), FLYOVER_EYE[1], FLYOVER_EYE[2] + 2.0 * (1.0 - np.cos(a)))
         cams.append(overview_camera(eye, FLYOVER_TARGET))
-    _frames(torch, oracle_mod, c3_svo, cams, w, h, 0, n_frames=2, keys=("hits", "rgba"))
+    _frames(torch, oracle_mod, c3_svo, cams, w, h, 0, n_frames=2, keys=("hits", "rgba"),
+            config={"seg_table_issue": 0x488, "move_every": 1, "seg_move": seg_move})
 
 
-@pytest.mark.parametrize("jit", ["1", "2"])
-def test_c3_segmented_jittered_one_sample_launches(torch, oracle_mod, monkeypatch, c3_svo, jit):
+@pytest.mark.parametrize("jit", [1, 2])
+def test_c3_segmented_jittered_one_sample_launches(torch, oracle_mod, c3_svo, jit):
     """svo_render_samples one sample per launch (the one-sample route: the render launch with the
     blend in its store epilogue), a new jittered offset every launch, on the C3 frame whose heavy
     tiles are segmented once the order exists -- from even splits (the default), or under
-    SVO_SEG_JITTER=1 from the starts another sub-pixel ray stored, with the segments past an earlier segment's record
+    seg_jitter 1 from the starts another sub-pixel ray stored, with the segments past an earlier segment's record
     ended early: the accumulation equals the oracle's renders + orc_accumulate, bit for bit."""
     from raytracingtest_amd.camera import jitter_offsets
     from test_gpu_frame import _oracle_accumulated
-    monkeypatch.setenv("SVO_SEG_JITTER", jit)
     w, h = 1920, 1080
     cam = CAMERAS["flyover"]()
     offs = jitter_offsets(6)
     want = _oracle_accumulated(oracle_mod, c3_svo, cam, w, h, offs)
-    m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo))
+    m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo), config={"seg_jitter": jit})
     try:
         m.SetSVOBuffer(c3_svo)
         m.UpdateShaderParameters(cam, w, h)
@@ -128,10 +122,9 @@ def test_c3_segmented_jittered_one_sample_launches(torch, oracle_mod, monkeypatc
 
 
 @pytest.mark.parametrize("mode,k", [(0, 4), (1, 4), (0, 8)])
-def test_segmented_band_and_hit_masks(torch, oracle_mod, monkeypatch, mode, k):
+def test_segmented_band_and_hit_masks(torch, oracle_mod, mode, k):
     """Rank 1's band of an 8-way 8-row split (the strong split's per-GPU launch), with the sparse
     payload's per-tile hit masks: records, RGB payload and masks equal the oracle's."""
-    monkeypatch.setenv("SVO_SEG_ALL", str(k))
     svo = build_menger(8)
     w, h = 512, 384
     cam = overview_camera()
@@ -151,7 +144,7 @@ def test_segmented_band_and_hit_masks(torch, oracle_mod, monkeypatch, mode, k):
             for r, c in zip(*np.nonzero(blk)):   # lane (bit) = row * 8 + column of the tile
                 mask |= 1 << (int(r) * 8 + int(c))
             want_masks[ty * (w // 8) + tx] = np.uint64(mask)
-    m = RaytracingMaster(device=0, capacity_nodes=len(svo))
+    m = RaytracingMaster(device=0, capacity_nodes=len(svo), config={"seg_all": k})
     try:
         m.SetSVOBuffer(svo)
         m.UpdateShaderParameters(cam, w, h)
