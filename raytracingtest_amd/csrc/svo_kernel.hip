@@ -1144,6 +1144,14 @@ __device__ __forceinline__ float seg_start(const LaunchParams &p, const float *h
 // whole tiles take the latency form (trace_lat, twice the LDS).
 // Part `part` of a tile traced as K segments per ray (render_seg_kernel; K a template constant so
 // the part's wave-uniform values need no SGPRs across the traversal loop).
+// Diagnostics (SVO_WAVE_LOG, p.wave_log != null): per workgroup of render_seg_kernel, at blockIdx.x:
+// [0] trace start, [1] trace end, [8] entry (s_memrealtime, 100 MHz), [2] the order entry,
+// [3] XCC_ID | the wave's trips << 8 (the band-floor decomposition, tools/band_floor.py).
+__device__ __forceinline__ void seg_log(const LaunchParams &p, int slot, uint32_t v) {
+    if (p.wave_log && threadIdx.x == 0) p.wave_log[WAVE_LOG_WORDS * (size_t)blockIdx.x + slot] = v;
+}
+__device__ __forceinline__ uint32_t now_100mhz() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+
 template <int MODE, bool FA, int K>
 __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restrict__ stk_base, int t, int part, int bx,
                                          int by) {
@@ -1180,8 +1188,13 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
     const float t_stop = seg_start(p, hint8, have, hi, e1, t_entry, t_exit);
     uint32_t n_lane, armed_at;
     bool stopped;
+    if (p.wave_log) seg_log(p, 0, now_100mhz());
     trace_seg<MODE, FA, true, false, K>(p, f, stk, k == 0 ? bs : t_start, t_stop, k == 0 && r.t_min >= bs, n_lane, armed_at,
                         stopped);
+    if (p.wave_log) {
+        seg_log(p, 1, now_100mhz());
+        seg_log(p, 3, ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFFu) | ((uint32_t)f.trips << 8));
+    }
     from_fray(f, r);
     // the record holder: the first segment that did not stop (the last one never stops)
     const int fsel = group_min(stopped ? K : k, K);
@@ -1224,10 +1237,22 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
 }
 
 template <int MODE, bool FA, bool LAT>
-__global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))) void render_seg_kernel(LaunchParams p, int tiles_x) {
+// VGPR budget: unbounded, the compiler gave this kernel 68-70 VGPRs -- 7 waves per SIMD (a wave needs
+// <= 64 for 8, MI355X_MICROARCH.md occupancy table).  Asking for 8 waves per EU fits it in 64 VGPRs at
+// the cost of one spilled dword, stored and reloaded outside the traversal loop (tools/kernel_resources.py).
+#ifndef SVO_SEG_WAVES_PER_EU
+#define SVO_SEG_WAVES_PER_EU 8
+#endif
+__global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR), amdgpu_waves_per_eu(SVO_SEG_WAVES_PER_EU, 8)))
+void render_seg_kernel(LaunchParams p, int tiles_x) {
     extern __shared__ uint2 stk_base[];
     const int lane = threadIdx.x;
+    const uint32_t t_in = p.wave_log ? now_100mhz() : 0u;
     const uint32_t entry = p.tile_order[blockIdx.x];
+    if (p.wave_log) {
+        seg_log(p, 8, t_in);
+        seg_log(p, 2, entry);
+    }
     if (entry == SEG_EMPTY) return;
     const int t = (int)(entry & 0x0FFFFFFFu);
     const int code = (int)(entry >> 28);   // 0: a whole tile; 1..4: part of a K = 4 tile; 5..12: K = 8
@@ -1253,9 +1278,14 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
         }
         FRay f;
         to_fray(r, f);
+        if (p.wave_log) seg_log(p, 0, now_100mhz());
         if (LAT) trace_lat<MODE>(p, f, stk);
         else if (p.tile_start) trace_beam<MODE, FA>(p, f, stk, beam_start(p, f, x, gy));
         else trace_lean<MODE, false, false, FA>(p, f, stk);
+        if (p.wave_log) {
+            seg_log(p, 1, now_100mhz());
+            seg_log(p, 3, ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFFu) | ((uint32_t)f.trips << 8));
+        }
         from_fray(f, r);
         const float4 acc = accum_load(p, out_index(p, lr, gy, x));
         Record o;

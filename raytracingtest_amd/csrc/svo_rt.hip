@@ -131,7 +131,8 @@ struct Sched {
     Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
     unsigned long long built_view = 0;   // the context's view generation the order was built under
-    unsigned long long view_prev = ~0ull;   // the view generation of this stream's last launch
+    unsigned long long view_prev = ~0ull;   // the view generation of this stream's last launch ...
+    float off_prev[2] = {-1.0f, -1.0f};     // ... and its pixel offset
     unsigned long long built_cost = ~0ull;  // the context's cost generation the order was built under
     unsigned long long last_build = 0;      // the launch count at the last order build
     int built_mode = -1;                 // shadows | stack_mode << 2 of the costs it was built from
@@ -1049,6 +1050,11 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     if (ordered) {
         rc = sched_for(ctx, s, &q);
         if (rc) return rc;
+        // a new _PixelOffset at the same view (the reference's frame loop draws one every frame,
+        // RaytracingMaster.cs:35): the stored segment starts belong to another sub-pixel ray
+        if (!p.samples && q->view_prev == ctx->view_gen &&
+            (p.cam.px_off[0] != q->off_prev[0] || p.cam.px_off[1] != q->off_prev[1]))
+            jittered = true;
         // field by field (a hash of overlapping shifted fields could match another geometry
         // and reuse a permutation of a different tile count)
         key.width = width;
@@ -1253,7 +1259,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // 0.0804 ms with it against 0.0629 without, N = 4 0.0500 / 0.0457, N = 8 0.0388 / 0.0395)
     p.lat = latency_bound && ctx->lat_mode != 0 && (!p.seg || ctx->lat_mode == 1) ? 1 : 0;
     const char *log_path = ctx->wave_log_path.empty() ? nullptr : ctx->wave_log_path.c_str();
-    const size_t n_wave = (size_t)n_tiles;
+    // one record per workgroup: the tile kernel's grid, or the segmented kernel's (its part entries)
+    const size_t n_wave = p.seg ? (size_t)svo::order_strips_grid(n_tiles, p.seg, p.seg_kmax) : (size_t)n_tiles;
     if (log_path && !instr) {
         if (ctx->wave_log_cap < n_wave) {
             HIP_TRY(hipDeviceSynchronize());
@@ -1373,6 +1380,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         const unsigned long long n = q->launches++;   // (p.tile_cost is cost_buf[n % 2])
         const bool moving = q->view_prev != ctx->view_gen;   // a new view since this stream's last launch
         q->view_prev = ctx->view_gen;
+        q->off_prev[0] = p.cam.px_off[0];
+        q->off_prev[1] = p.cam.px_off[1];
         // the periodic rebuild only when costs can have changed without a new view (a jittered
         // pixel offset, a new light or pool, per-launch sample offsets): a held view with nothing
         // else changed records the same costs every launch, so its order stays exact

@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round 6 evidence steps, one GPU session; each step under its own time limit, chained so that a
+# failure ends the session.  Usage: bash tools/gpu_round6.sh <step> [tag]
+set -o pipefail
+step=$1; tag=${2:-r06}
+out=gpurun_out/$tag
+mkdir -p "$out"
+dropin() {   # the drop-in loop (held / jittered / pan) under one svo_config
+    local name=$1; shift
+    timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main "$@" > "$out/dropin_$name.txt" 2>&1
+}
+bench_lib() {   # the default bench line (no extras) with a given library build
+    local name=$1 lib=$2
+    SVO_RT_LIB=$lib timeout -k 10 150 python -u bench.py --no-extras --cpu-seconds 0 --steps 1000 --warmup 50 \
+        > "$out/bench_$name.json" 2> "$out/bench_$name.err"
+}
+case $step in
+policy)
+    dropin default && dropin jit1 --set seg_jitter=1 && dropin jit0 --set seg_jitter=0 &&
+    dropin ord1 --set order_every=1 && dropin iss44 --set seg_table_issue=0x44 && dropin noseg --set segments=0 ;;
+occupancy)
+    lib8=$PWD/raytracingtest_amd/libsvo_rt.so; lib7=$PWD/build/ab/seg7/libsvo_rt.so
+    bench_lib w8a "$lib8" && bench_lib w7a "$lib7" && bench_lib w8b "$lib8" && bench_lib w7b "$lib7" ;;
+band)
+    timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
+    timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
+    rank=$(python -c "import json; print(json.load(open('$out/band_floor_8.json'))['slowest_rank'])") &&
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null &&
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/band_trace" -o band -- \
+        python3 tools/band_floor.py --gpus 8 --trace-only --rank "$rank" > "$out/band_trace.txt" 2>&1 ;;
+esac
