@@ -1796,7 +1796,9 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
                                                                      uint32_t *__restrict__ order, int n, int tiles_x,
                                                                      uint32_t *stats, int seg_cap,
                                                                      const uint16_t *__restrict__ part_cost,
-                                                                     int seg_kpack, int spread) {
+                                                                     int seg_kpack, int spread,
+                                                                     const uint16_t *__restrict__ hist_in,
+                                                                     uint16_t *__restrict__ hist_out) {
     __shared__ uint32_t red[ORDER_THREADS / 64], red_sum[ORDER_THREADS / 64];
     constexpr int NC = 6;
     __shared__ uint32_t cnt[NC], base[NC + 1], rank[NC], segs[NC];
@@ -1824,50 +1826,71 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         if (w.r >= tiles_y) { w.r -= tiles_y; w.c += 1; }
     };
     auto tile_of = [&](const Walk &w) { return w.r * tiles_x + strip_col(x, w.c); };
+    // history (hist_in != null: the same view as the previous build, costs drifting with the pixel
+    // offset -- the drop-in's jittered frame loop): a tile is classed by the max of its cost now and its
+    // decayed cost of earlier builds, so a tile whose cost depends on the sub-pixel offset keeps the
+    // class of its heavier offsets; hist_out = that decayed max (a separate buffer: no build reads
+    // what another XCD's workgroup of the same build writes)
+    auto eff_cost = [&](int t) -> uint32_t {
+        const uint32_t k = cost_at(t);
+        return hist_in ? max(k, (uint32_t)hist_in[t]) : k;
+    };
     // spread (a moving camera: the costs are a few frames old and the heavy tiles have drifted by up to
     // a tile on screen): a tile's class is that of the heaviest of it and its 8 neighbours
     auto class_cost = [&](const Walk &w) -> uint32_t {
         const int col = strip_col(x, w.c);
-        if (!spread) return cost_at(w.r * tiles_x + col);
+        if (!spread) return eff_cost(w.r * tiles_x + col);
         uint32_t m = 0;
         for (int dy = -1; dy <= 1; ++dy) {
             const int r = w.r + dy;
             if (r < 0 || r >= tiles_y) continue;
             for (int dx = -1; dx <= 1; ++dx) {
                 const int c = col + dx;
-                if (c >= 0 && c < tiles_x) m = max(m, cost_at(r * tiles_x + c));
+                if (c >= 0 && c < tiles_x) m = max(m, eff_cost(r * tiles_x + c));
             }
         }
         return m;
     };
-    uint32_t mx = 0, sum = 0;
+    __shared__ uint32_t red_eff[ORDER_THREADS / 64];
+    uint32_t mx = 0, sum = 0, mxe = 0;
     for (Walk w = start(); w.e < len; next(w)) {
-        const uint32_t k = cost_at(tile_of(w));
+        const int t = tile_of(w);
+        const uint32_t k = cost_at(t);
         mx = max(mx, k);
         sum += k;
+        if (hist_out) {
+            const uint32_t h = hist_in ? hist_in[t] : 0u;
+            mxe = max(mxe, max(k, h));
+            hist_out[t] = (uint16_t)max(k, h - (h >> 3));
+        }
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+        mxe = max(mxe, (uint32_t)__shfl_xor((int)mxe, d));
         sum += (uint32_t)__shfl_xor((int)sum, d);
     }
     if (lane == 0) {
         red[wave] = mx;
         red_sum[wave] = sum;
+        red_eff[wave] = mxe;
     }
     if (tid < NC) cnt[tid] = 0;
     __syncthreads();
     mx = 0;
     sum = 0;
+    mxe = 0;
 #pragma unroll
     for (int w = 0; w < ORDER_THREADS / 64; ++w) {
         mx = max(mx, red[w]);
         sum += red_sum[w];
+        mxe = max(mxe, red_eff[w]);
     }
-    if (stats && tid == 0) {
+    if (stats && tid == 0) {   // the loop-form rule reads the launch's own costs
         stats[2 * x] = mx;
         stats[2 * x + 1] = sum;
     }
+    if (hist_in) mx = max(mx, mxe);   // the classes scale with the costs they are taken from
     // six classes, the top half split three ways so the very heaviest tiles are the
     // XCD's first dispatches (they bound the launch); the render kernel's s_setprio
     // classes are >= 1/2, >= 1/4, >= 1/8 of the XCD's max and the rest
@@ -1912,7 +1935,8 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
 }
 
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
-                               uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_kpack, int spread) {
+                               uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_kpack, int spread,
+                               const uint16_t *hist_in, uint16_t *hist_out) {
     if (n_tiles <= 0) return hipSuccess;
     if (seg_cap > 0 && (n_tiles / tiles_x) * tiles_x != n_tiles) return hipErrorInvalidValue;
     for (int c = 0; c < 6; ++c) {
@@ -1922,7 +1946,7 @@ hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tile
     if (seg_cap > 0 && ((size_t)order_strips_grid(n_tiles, seg_cap, seg_kmax_of(seg_kpack)) >> 28) != 0)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
-                       stats, seg_cap, part_cost, seg_kpack, spread);
+                       stats, seg_cap, part_cost, seg_kpack, spread, hist_in, hist_out);
     return hipGetLastError();
 }
 

@@ -115,6 +115,9 @@ struct Sched {
     bool build_seen[2] = {};             // the render stream already waits for it (or it completed)
     Geo build_key[2];
     int next_buf = 0;
+    uint16_t *hist[2] = {};            // cost history of the order builds at a held view (svo_config.cost_history)
+    int hist_cur = 0;                  // hist[hist_cur] holds the last build's
+    bool hist_valid = false;           // ... made at the current geometry and view
     uint16_t *shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
     uint32_t *shadow_order = nullptr;
     size_t cap = 0;
@@ -340,7 +343,8 @@ struct svo_ctx {
     int seg_move = 2;                // env SVO_SEG_MOVE: a launch at a new view
     int seg_jitter = 2;              // env SVO_SEG_JITTER: a jittered launch (the one-sample samples route)
     int spread = 1;                  // env SVO_SPREAD=0: a moving camera's order classes tiles by their own costs only
-    int relayout = 1;                // env SVO_RELAYOUT=0: keep an order built from costs of another class layout
+    int relayout = 1;                // svo_config.relayout 0: keep an order built from costs of another class layout
+    int cost_history = 1;            // svo_config.cost_history: held-view builds class by the decayed max cost
     int seg_min_chain = 160;         // env SVO_SEG_MIN_CHAIN: a latency-bound launch whose heaviest tile costs fewer
                                      // trips takes the latency form, unsegmented, without beam starts
     float seg_ratio = 0.28f;         // svo_config.seg_ratio: ... and the same with beam starts (class table only)
@@ -414,6 +418,7 @@ void reset_builds(Sched &q) {
         q.build_key[i] = Geo();
     }
     q.order_key = q.shadow_key = Geo();
+    q.hist_valid = false;
 }
 
 void free_sched(Sched &q) {
@@ -421,6 +426,8 @@ void free_sched(Sched &q) {
         if (q.cost_buf[i]) hipFree(q.cost_buf[i]);
         if (q.part_buf[i]) hipFree(q.part_buf[i]);
         if (q.order_buf[i]) hipFree(q.order_buf[i]);
+        if (q.hist[i]) hipFree(q.hist[i]);
+        q.hist[i] = nullptr;
         q.cost_buf[i] = q.part_buf[i] = nullptr;
         q.order_buf[i] = nullptr;
     }
@@ -1085,7 +1092,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 HIP_TRY(hipMalloc(&q->part_buf[i], svo::SEG_KMAX * cap * sizeof(uint16_t)));
                 HIP_TRY(hipMemset(q->part_buf[i], 0, svo::SEG_KMAX * cap * sizeof(uint16_t)));
                 HIP_TRY(hipMalloc(&q->order_buf[i], order_need * sizeof(uint32_t)));
+                HIP_TRY(hipMalloc(&q->hist[i], cap * sizeof(uint16_t)));
             }
+            q->hist_valid = false;
             HIP_TRY(hipMalloc(&q->shadow_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(q->shadow_cost, 0, cap * sizeof(uint16_t)));
             HIP_TRY(hipMalloc(&q->shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
@@ -1407,12 +1416,21 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         // on the side stream, behind this launch (its costs; and every launch that read buffer bi)
         HIP_TRY(hipEventRecord(q->render_done, s));
         HIP_TRY(hipStreamWaitEvent(q->side, q->render_done, 0));
+        // cost history: a build at the view (and geometry) of the previous one folds that build's
+        // decayed costs in (a held view, costs drifting with the pixel offset); any other starts afresh
+        const bool same = q->hist_valid && q->built_view == ctx->view_gen && [&] {
+            Geo g = q->order_key; g.seg = g.kpack = 0; return g == key; }();
+        const bool hist = ctx->cost_history && p.xcd_remap == 2 && !moving_build;
+        const uint16_t *h_in = hist && same ? q->hist[q->hist_cur] : nullptr;
+        uint16_t *h_out = hist ? q->hist[q->hist_cur ^ 1] : nullptr;
         e = p.xcd_remap == 2 ? svo::launch_order_strips(p.tile_cost, q->order_buf[bi], n_tiles, (width + 7) / 8, q->side,
                                                         st16, okey.seg, p.part_cost, okey.kpack,
-                                                        moving_build && ctx->spread ? 1 : 0)
+                                                        moving_build && ctx->spread ? 1 : 0, h_in, h_out)
                              : svo::launch_order_tiles(p.tile_cost, q->order_buf[bi], n_tiles, q->side, st16);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         HIP_TRY(hipEventRecord(q->build_ev[bi], q->side));
+        if (h_out) q->hist_cur ^= 1;
+        q->hist_valid = h_out != nullptr;
         q->build_at[bi] = (long long)q->launches - 1;   // launches was incremented above
         q->build_seen[bi] = false;
         q->build_key[bi] = okey;
@@ -1755,6 +1773,7 @@ void config_of(const svo_ctx *c, svo_config *o) {
     k.move_every = c->move_every;
     k.move_spread = c->spread;
     k.relayout = c->relayout;
+    k.cost_history = c->cost_history;
     k.fetch_all = c->fetch_all;
     k.loop_form = c->lat_mode;
     k.lat_ratio = c->lat_ratio;
@@ -1795,7 +1814,7 @@ int check_config(const svo_config &k) {
     const char *bad = !bit(k.tile_order) ? "tile_order" : !bit(k.xcd_strips) ? "xcd_strips"
                     : !bit(k.issue_priority) ? "issue_priority" : k.order_every < 1 ? "order_every"
                     : k.move_every < 1 ? "move_every" : !bit(k.move_spread) ? "move_spread"
-                    : !bit(k.relayout) ? "relayout" : k.fetch_all < -1 || k.fetch_all > 1 ? "fetch_all"
+                    : !bit(k.relayout) ? "relayout" : !bit(k.cost_history) ? "cost_history" : k.fetch_all < -1 || k.fetch_all > 1 ? "fetch_all"
                     : k.loop_form < -1 || k.loop_form > 1 ? "loop_form" : !ratio(k.lat_ratio) ? "lat_ratio"
                     : !bit(k.segments) ? "segments" : !table(k.seg_table_latency) ? "seg_table_latency"
                     : !table(k.seg_table_issue) ? "seg_table_issue" : !table(k.seg_table_thin) ? "seg_table_thin"
@@ -1823,6 +1842,7 @@ int apply_config(svo_ctx *c, const svo_config &k) {
     c->move_every = k.move_every;
     c->spread = k.move_spread;
     c->relayout = k.relayout;
+    c->cost_history = k.cost_history;
     c->fetch_all = k.fetch_all;
     c->lat_mode = k.loop_form;
     c->lat_ratio = k.lat_ratio;

@@ -28,4 +28,14 @@ band)
     cd /tmp && export TMPDIR=/tmp && cd - > /dev/null &&
     timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/band_trace" -o band -- \
         python3 tools/band_floor.py --gpus 8 --trace-only --rank "$rank" > "$out/band_trace.txt" 2>&1 ;;
+bandab)
+    bf() { local name=$1 n=$2; shift 2
+           timeout -k 10 150 python -u tools/band_floor.py --gpus $n --out "$out/bf_${name}_$n.json" "$@" \
+               > "$out/bf_${name}_$n.txt" 2>&1; }
+    bf default 1 && bf default 8 && bf t4 8 --set seg_table_thin=0x8888 && bf t5 8 --set seg_table_thin=0x88888 &&
+    bf t5c 8 --set seg_table_thin=0x88888 --set seg_cap=256 && bf t6c 8 --set seg_table_thin=0x888888 --set seg_cap=512 &&
+    bf default 4 && bf l4 4 --set seg_table_latency=0x4444 && bf l5 4 --set seg_table_latency=0x44444 --set seg_cap=256 &&
+    bf l8 4 --set seg_table_latency=0x8888 --set seg_cap=256 && bf default 2 && bf l4 2 --set seg_table_latency=0x4444 ;;
+jitter)
+    timeout -k 10 200 python -u tools/jitter_probe.py > "$out/jitter_probe.txt" 2>&1 ;;
 esac
