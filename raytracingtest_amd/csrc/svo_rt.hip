@@ -540,17 +540,22 @@ std::shared_ptr<const std::vector<uint2>> build_beam_boxes(const uint32_t *lo, c
     auto out = std::make_shared<std::vector<uint2>>();
     struct Item { uint32_t node, x, y, z; };
     std::vector<Item> cur{{0u, 0u, 0u, 0u}}, nxt;
+    // a pool whose subtrees are shared (linked sub-SVOs) expands them once per position; past this many
+    // boxes the walk stops descending and lists the nodes it reached as boxes of their own (coarser,
+    // still a lower bound: every voxel of the pool lies in one of the listed boxes)
+    constexpr size_t BUDGET = (size_t)1 << 23;
     for (int d = 0; d < ds && !cur.empty(); ++d) {
         nxt.clear();
         for (const Item &it : cur) {
             const uint32_t m = lo[it.node] & 0xFFu, v = (lo[it.node] >> 8) & 0xFFu;
             uint32_t rank = 0;
+            const bool descend = nxt.size() + out->size() < BUDGET;
             for (uint32_t c = 0; c < 8; ++c) {
                 const bool inner = (m >> c) & 1u;
                 const uint32_t child = inner ? first[it.node] + rank++ : 0u;
                 if (!((v >> c) & 1u)) continue;
                 const uint32_t x = 2 * it.x + (c & 1u), y = 2 * it.y + ((c >> 1) & 1u), z = 2 * it.z + ((c >> 2) & 1u);
-                if (inner && d + 1 < ds) {
+                if (inner && d + 1 < ds && descend) {
                     if (child < n) nxt.push_back({child, x, y, z});
                 } else {
                     out->push_back(make_uint2(x | (y << 16), z | ((uint32_t)(d + 1) << 16)));
@@ -639,37 +644,41 @@ int recompute_pool(svo_ctx *ctx) {
             lo[i] = pool[i].x;
             first[i] = pool[i].y;
         }
-        if (!simple) {   // breadth-first from the root, every node at most once
-            std::vector<uint8_t> seen(n, 0);
-            std::vector<uint32_t> cur{0}, nxt;
-            seen[0] = 1;
-            int depth = 0, deep = 0;   // levels of uploaded descriptors; the deepest empty child's level
-            bool tree = true;
-            while (!cur.empty() && tree && depth <= 22) {
-                ++depth;
-                nxt.clear();
-                for (uint32_t li : cur) {
-                    const uint32_t m = lo[li] & 0xFFu;
-                    uint32_t rank = 0;
-                    for (int c = 0; c < 8; ++c) {
-                        if (!((m >> c) & 1u)) continue;
-                        const uint64_t child = (uint64_t)first[li] + rank++;
-                        if (child >= n) {   // not uploaded: an empty descriptor one level down
-                            deep = std::max(deep, depth + 1);
-                            continue;
-                        }
-                        if (seen[child]) { tree = false; break; }
-                        seen[child] = 1;
-                        nxt.push_back((uint32_t)child);
-                    }
-                    if (!tree) break;
+        if (!simple) {
+            // the longest descriptor path from the root, depth(v) = 1 + the max depth of v's non-leaf
+            // children (a child past the uploads reads as an empty descriptor: depth 1): an iterative
+            // depth-first walk, each node finished once, so shared subtrees (every trunk leaf linking
+            // the same sub-SVO, Clipmap.cs:158-159) cost nothing extra; a cycle has no depth
+            std::vector<uint8_t> state(n, 0), dep(n, 0), acc(n, 0);   // state: 0 new, 1 open, 2 done
+            struct Frame { uint32_t v; uint32_t slot; };
+            std::vector<Frame> st{{0u, 0u}};
+            state[0] = 1;
+            bool ok = true;
+            while (!st.empty() && ok) {
+                Frame &f = st.back();
+                const uint32_t v = f.v, m = lo[v] & 0xFFu;
+                bool pushed = false;
+                while (f.slot < 8) {
+                    const uint32_t c = f.slot++;
+                    if (!((m >> c) & 1u)) continue;
+                    const uint64_t child = (uint64_t)first[v] + (uint32_t)__builtin_popcount(m & ((1u << c) - 1u));
+                    if (child >= n) { acc[v] = std::max<uint8_t>(acc[v], 1); continue; }
+                    if (state[child] == 1) { ok = false; break; }   // a cycle
+                    if (state[child] == 2) { acc[v] = std::max(acc[v], dep[child]); continue; }
+                    state[child] = 1;
+                    st.push_back({(uint32_t)child, 0u});
+                    pushed = true;
+                    break;
                 }
-                cur.swap(nxt);
+                if (!ok || pushed) continue;
+                dep[v] = (uint8_t)std::min(1 + (int)acc[v], 23);   // 23: deeper than the stack allows
+                state[v] = 2;
+                st.pop_back();
+                if (!st.empty()) acc[st.back().v] = std::max(acc[st.back().v], dep[v]);
             }
-            depth = std::max(depth, deep);
-            if (tree && cur.empty() && depth <= 22) {
+            if (ok && dep[0] <= 22) {
                 ctx->depth_exact = true;
-                ctx->depth = depth;
+                ctx->depth = dep[0];
             }
         }
         if (ctx->depth_exact && ctx->beam) boxes = build_beam_boxes(lo.data(), first.data(), n, ctx->depth, ctx->beam_back);

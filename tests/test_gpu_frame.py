@@ -921,9 +921,11 @@ def test_clipmap_linked_sub_svo_trunk_first(torch, oracle_mod, devices):
     NaiveCreator.cs:156-159; builder.link_leaves) is uploaded FIRST, then the
     sub-SVO at offset 10000 (SetSVOBuffer(data, 10000)).  Between the two uploads
     the links read the zero-filled pool (empty descriptors); after the second,
-    the frame equals the oracle's over the combined pool, both stack modes.  With
-    a multi-device context each upload is validated once and replicated to the
-    other members device to device."""
+    the frame equals the oracle's over the combined pool, both stack modes, with beam
+    starts (the pool's longest path gives its depth; its splat list expands the shared
+    sub-SVO per position), and the beam-started walk fetches fewer nodes than the
+    reference's.  With a multi-device context each upload is validated once and
+    replicated to the other members device to device."""
     from raytracingtest_amd.builder import link_leaves
     from raytracingtest_amd.native_builder import build_sampler_svo
     base = 10000
@@ -962,6 +964,27 @@ def test_clipmap_linked_sub_svo_trunk_first(torch, oracle_mod, devices):
             assert rgba.reshape(-1, 4).tobytes() == ref_rgba.tobytes()
         linked = np.count_nonzero((ref["flags"] & 1) != 0)
         assert linked > 500 and np.all(ref["parent"][(ref["flags"] & 1) != 0] >= base)
+        # the linked pool (every trunk leaf sharing one sub-SVO: a DAG) has an exact
+        # depth (its longest path) and a splat list expanded per position, so its primary rays get beam
+        # starts (the frames above ran with them) and the walk they run fetches fewer nodes
+        one = m if devices is None else m.member(0)
+        assert one.info()["depth"] < 22
+        starts = torch.empty(w * h, dtype=torch.float32, device="cuda")
+        fetch_ref = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+        fetch_beam = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        one.beam_starts_device(w, h, starts.data_ptr())
+        one.count_fetches_device(w, h, fetch_ref.data_ptr())
+        one.set_count_beam(True)
+        one.count_fetches_device(w, h, fetch_beam.data_ptr())
+        one.set_count_beam(False)
+        one.synchronize()
+        st = starts.cpu().numpy()
+        hit = (ref["flags"] & 1) != 0
+        assert np.isfinite(st).sum() > linked // 2
+        assert np.all(st[hit] <= ref["t"][hit] / 2048.0)   # every start at or before its hit
+        f_ref, f_beam = int(fetch_ref.to(torch.int64).sum()), int(fetch_beam.to(torch.int64).sum())
+        assert f_beam < 0.9 * f_ref, (f_beam, f_ref)
     finally:
         m.close()
 

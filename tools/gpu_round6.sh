@@ -37,5 +37,6 @@ bandab)
     bf default 4 && bf l4 4 --set seg_table_latency=0x4444 && bf l5 4 --set seg_table_latency=0x44444 --set seg_cap=256 &&
     bf l8 4 --set seg_table_latency=0x8888 --set seg_cap=256 && bf default 2 && bf l4 2 --set seg_table_latency=0x4444 ;;
 jitter)
-    timeout -k 10 200 python -u tools/jitter_probe.py > "$out/jitter_probe.txt" 2>&1 ;;
+    timeout -k 10 200 python -u tools/jitter_probe.py > "$out/jitter_probe.txt" 2>&1 &&
+    timeout -k 10 200 python -u tools/jitter_probe.py --set cost_history=0 > "$out/jitter_probe_h0.txt" 2>&1 ;;
 esac
