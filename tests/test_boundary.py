@@ -222,3 +222,16 @@ def test_library_reads_no_policy_from_the_environment():
         names += re.findall(r"getenv\(\s*\"(\w+)\"", text)
         assert text.count("getenv(") == len(re.findall(r"getenv\(\s*\"\w+\"", text)), f
     assert sorted(names) == ["SVO_BEAM_DIAG", "SVO_DEBUG", "SVO_LDS_PAD", "SVO_WAVE_LOG"]
+
+
+def test_csharp_shim_config_struct_follows_the_header():
+    """unity/RaytracingMasterNative.cs's SvoConfig (StructLayout Sequential, no C# toolchain here to
+    compile it) declares the header's fields in the header's order with 4-byte types."""
+    from raytracingtest_amd import _lib
+    text = open(os.path.join(ROOT, "unity", "RaytracingMasterNative.cs")).read()
+    body = re.search(r"public struct SvoConfig \{(.*?)\n    \}", text, re.S).group(1)
+    names = []
+    for decl in re.findall(r"public (uint|int|float) ([^;]+);", body):
+        names += [n.strip() for n in decl[1].split(",")]
+    snake = [re.sub(r"([A-Z])", lambda m: "_" + m.group(1).lower(), n) for n in names]
+    assert snake == ["size", "version"] + [n for n, _ in _lib.CONFIG_FIELDS]

@@ -42,6 +42,24 @@ public static class SvoNative {
     [DllImport(Lib)] public static extern int svo_destroy(IntPtr ctx);
     [DllImport(Lib)] public static extern IntPtr svo_last_error();
 
+    // svo_config (include/svo_rt.h, ABI 10): the render policy, versioned by size -- field order and
+    // types exactly the header's (132 bytes; tests/test_boundary.py checks the C layout)
+    [StructLayout(LayoutKind.Sequential)]
+    public struct SvoConfig {
+        public uint size, version;
+        public int tileOrder, xcdStrips, issuePriority, orderEvery, moveEvery, moveSpread, relayout, costHistory,
+                   fetchAll, loopForm;
+        public float latRatio;
+        public int segments;
+        public uint segTableLatency, segTableIssue, segTableThin;
+        public float segRatio, segThinRatio;
+        public int segCap, segMinChain, segMove, segJitter, segAll;
+        public uint segScramble;
+        public int beam, beamBack, shadowForm, shadowOrder, readback, hostCopyThreads, sparsePayload, peerCopy;
+    }
+    [DllImport(Lib)] public static extern int svo_get_config(IntPtr ctx, ref SvoConfig cfg);
+    [DllImport(Lib)] public static extern int svo_set_config(IntPtr ctx, ref SvoConfig cfg);
+
     [StructLayout(LayoutKind.Sequential)]
     public struct SvobResult {   // == svob_result
         public UIntPtr nNodes; public int depth; public int v1Ok;
@@ -82,6 +100,18 @@ public class RaytracingMasterNative : MonoBehaviour {
     public SampleFunctions.Type sampleType = SampleFunctions.Type.Custom1;
     [Range(1, 8)] public int gpus = 1;   // > 1: the frame is split in 8-row bands over GPUs 0..gpus-1
 
+    // Render policy (svo_config): the Inspector fields a developer tunes; the defaults are the
+    // library's (svo_get_config(NULL)).  None changes the image -- only where the time goes.
+    [Header("Render policy (svo_config)")]
+    public bool beamStarts = true;               // beam: rays start at their tile's lower bound of the hit t
+    [Range(0, 8)] public int beamBack = 2;       // splat boxes this many levels above the leaves
+    public bool segmentedRays = true;            // segments: heavy tiles traced as exact t-segments
+    public bool costOrderedDispatch = true;      // tile_order: heaviest tiles dispatched first
+    [Range(1, 32)] public int moveEvery = 4;     // while the camera moves, rebuild the order every k-th frame
+    public bool costHistory = true;              // a held view's order keeps tiles' heaviest recent costs
+    public enum ShadowForm { Fused = 0, TilePass = 1, CompactedList = 2 }
+    public ShadowForm shadowForm = ShadowForm.Fused;
+
     IntPtr _ctx;
     Camera _camera;
     Texture2D _frame;
@@ -118,7 +148,25 @@ public class RaytracingMasterNative : MonoBehaviour {
             SvoNative.Check(SvoNative.svo_create_multi(devices, gpus, capacity, 8, out ctx), "svo_create_multi");
         }
         _ctx = ctx;
+        ApplyConfig();
     }
+
+    // the Inspector fields into the context's svo_config; the other fields keep the library's values
+    void ApplyConfig() {
+        if (_ctx == IntPtr.Zero) return;
+        var cfg = new SvoNative.SvoConfig { size = (uint)Marshal.SizeOf<SvoNative.SvoConfig>() };
+        SvoNative.Check(SvoNative.svo_get_config(_ctx, ref cfg), "svo_get_config");
+        cfg.beam = beamStarts ? 1 : 0;
+        cfg.beamBack = beamBack;
+        cfg.segments = segmentedRays ? 1 : 0;
+        cfg.tileOrder = costOrderedDispatch ? 1 : 0;
+        cfg.moveEvery = moveEvery;
+        cfg.costHistory = costHistory ? 1 : 0;
+        cfg.shadowForm = (int)shadowForm;
+        SvoNative.Check(SvoNative.svo_set_config(_ctx, ref cfg), "svo_set_config");
+    }
+
+    void OnValidate() { ApplyConfig(); }   // an Inspector edit at run time takes effect at the next frame
 
     // RaytracingMaster.cs:90-109 (key R): NaiveCreator.Create(SampleFunctions.functions[sampleType], maxLevel)
     // by the native builder on GPU 0, uploaded in the wide node format -- every BASELINE pool from
