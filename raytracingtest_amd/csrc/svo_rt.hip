@@ -43,12 +43,6 @@
 #include "svo_rt.h"
 #include "svo_traverse.h"
 
-// A camera that moves every frame splats its beam starts on a stream of its own, ahead of the render
-// (Sched::splat_stream); 0 puts the splat in front of the render on the render stream (A/B builds).
-#ifndef SVO_SPLAT_AHEAD
-#define SVO_SPLAT_AHEAD 1
-#endif
-
 namespace {
 
 thread_local std::string g_last_error;
@@ -131,17 +125,6 @@ struct Sched {
     float4 *seg_hint = nullptr;        // segmented tiles: per pixel the segment starts (svo_traverse.h)
     size_t hint_cap = 0;
     unsigned long long *tile_start = nullptr;   // beam starts of this stream's launches (svo_traverse.h)
-    // Splat ahead (a camera that moves every frame): the splat of a new view runs on its own stream
-    // into the buffer the previous view did NOT use, concurrently with the previous render's tail
-    // (its last waves leave CUs idle), instead of in front of the render on the render stream.
-    // ts_buf[ts_cur] holds the current view's keys (ts_buf[0] is tile_start); ts_free[i] is recorded
-    // on the render stream right behind the last render that read buffer i, ts_done[i] behind the
-    // splat into it.  Device-scope events: nothing the host reads.
-    unsigned long long *ts_buf2 = nullptr;
-    int ts_cur = 0;
-    hipStream_t splat_stream = nullptr;
-    hipEvent_t ts_free[2] = {}, ts_done[2] = {};
-    bool ts_free_set[2] = {};
     size_t ts_cap = 0;
     uint32_t ts_gen = 0;               // the generation of the last launch's keys ...
     unsigned long long ts_view = ~0ull; // ... splatted for this view, splat list and frame size
@@ -1342,7 +1325,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             }
             const int tx = (width + 7) / 8, ty = (height + 7) / 8, sx = (width + 63) / 64, sy = (height + 63) / 64;
             const size_t need = (size_t)tx * ty + (size_t)sx * sy + 1;
-            // the stream's own buffers; an instrumented launch (no scheduling state) the shared scratch
+            // the stream's own buffer; an instrumented launch (no scheduling state) the shared scratch
             unsigned long long *&buf = q ? q->tile_start : ctx->count_ts;
             size_t &cap = q ? q->ts_cap : ctx->count_ts_cap;
             uint32_t &gen = q ? q->ts_gen : ctx->count_ts_gen;
@@ -1352,47 +1335,22 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             }
             const bool reuse = q && q->ts_view == ctx->view_gen && q->ts_boxes == ctx->pool_boxes_id && q->ts_w == width &&
                                q->ts_h == height && cap >= need && gen != 0;
-            const bool ahead = SVO_SPLAT_AHEAD && q;
             if (!reuse && (cap < need || gen == 0xFFFFFFFEu)) {   // (re)filled with all-ones keys: generation 0, stale
-                HIP_TRY(hipDeviceSynchronize());   // a pending launch may still read the old buffers
+                HIP_TRY(hipDeviceSynchronize());   // a pending launch may still read the old buffer
                 if (cap < need) {
                     if (buf) hipFree(buf);
                     buf = nullptr;
-                    if (q && q->ts_buf2) hipFree(q->ts_buf2);
-                    if (q) q->ts_buf2 = nullptr;
                     cap = 0;
                     HIP_TRY(hipMalloc(&buf, need * sizeof(unsigned long long)));
-                    if (ahead) HIP_TRY(hipMalloc(&q->ts_buf2, need * sizeof(unsigned long long)));
                     cap = need;
                 }
                 HIP_TRY(hipMemset(buf, 0xFF, cap * sizeof(unsigned long long)));
-                if (ahead) HIP_TRY(hipMemset(q->ts_buf2, 0xFF, cap * sizeof(unsigned long long)));
-                if (q) q->ts_free_set[0] = q->ts_free_set[1] = false;   // nothing pending after the synchronize
                 gen = 0;
             }
             if (!reuse) ++gen;
-            unsigned long long *target = buf;
-            if (ahead && !reuse) {
-                if (!q->splat_stream) {
-                    HIP_TRY(hipStreamCreateWithFlags(&q->splat_stream, hipStreamNonBlocking));
-                    for (int i = 0; i < 2; ++i) {
-                        HIP_TRY(hipEventCreateWithFlags(&q->ts_free[i], hipEventDisableTiming | hipEventReleaseToDevice));
-                        HIP_TRY(hipEventCreateWithFlags(&q->ts_done[i], hipEventDisableTiming | hipEventReleaseToDevice));
-                    }
-                }
-                if (!q->ts_buf2) {
-                    HIP_TRY(hipDeviceSynchronize());
-                    HIP_TRY(hipMalloc(&q->ts_buf2, cap * sizeof(unsigned long long)));
-                    HIP_TRY(hipMemset(q->ts_buf2, 0xFF, cap * sizeof(unsigned long long)));
-                }
-                q->ts_cur ^= 1;   // the buffer the previous view's renders did not read ...
-                target = q->ts_cur ? q->ts_buf2 : buf;
-            } else if (ahead) {
-                target = q->ts_cur ? q->ts_buf2 : buf;
-            }
             bp.boxes = ctx->d_boxes;
             bp.n_boxes = ctx->n_boxes;
-            bp.tile_start = target;
+            bp.tile_start = buf;
             bp.gen = gen;
             bp.diag = ctx->beam_diag;   // timing diagnostics only
             bp.tiles_x = tx;
@@ -1404,21 +1362,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
             bp.width = width;
             bp.height = height;
             if (!reuse) {
-                if (ahead) {
-                    const int nb = q->ts_cur, ob = nb ^ 1;
-                    // ... once every render that read it has finished (recorded at the last switch)
-                    if (q->ts_free_set[nb]) HIP_TRY(hipStreamWaitEvent(q->splat_stream, q->ts_free[nb], 0));
-                    hipError_t eb = svo::launch_beam_splat(bp, q->splat_stream);
-                    if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
-                    HIP_TRY(hipEventRecord(q->ts_done[nb], q->splat_stream));
-                    // the renders of the old buffer end here; this render waits for its own splat
-                    HIP_TRY(hipEventRecord(q->ts_free[ob], s));
-                    q->ts_free_set[ob] = true;
-                    HIP_TRY(hipStreamWaitEvent(s, q->ts_done[nb], 0));
-                } else {
-                    hipError_t eb = svo::launch_beam_splat(bp, s);
-                    if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
-                }
+                hipError_t eb = svo::launch_beam_splat(bp, s);
+                if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
                 if (q) {
                     q->ts_view = ctx->view_gen;
                     q->ts_boxes = ctx->pool_boxes_id;
@@ -1426,7 +1371,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                     q->ts_h = height;
                 }
             }
-            p.tile_start = target;
+            p.tile_start = buf;
             p.ts_gen = gen;
             p.ts_tiles_x = tx;
             p.ts_super_x = sx;
@@ -1800,15 +1745,6 @@ int destroy_single(svo_ctx *ctx) {
         free_sched(q);
         if (q.seg_hint) hipFree(q.seg_hint);
         if (q.tile_start) hipFree(q.tile_start);
-        if (q.ts_buf2) hipFree(q.ts_buf2);
-        if (q.splat_stream) {
-            hipStreamSynchronize(q.splat_stream);
-            hipStreamDestroy(q.splat_stream);
-        }
-        for (int i = 0; i < 2; ++i) {
-            if (q.ts_free[i]) hipEventDestroy(q.ts_free[i]);
-            if (q.ts_done[i]) hipEventDestroy(q.ts_done[i]);
-        }
         if (q.done) hipEventDestroy(q.done);
         for (int r = 0; r < Sched::STATS_RING; ++r)
             if (q.stats_ev[r]) hipEventDestroy(q.stats_ev[r]);

@@ -39,9 +39,4 @@ bandab)
 jitter)
     timeout -k 10 200 python -u tools/jitter_probe.py > "$out/jitter_probe.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/jitter_probe.py --set cost_history=0 > "$out/jitter_probe_h0.txt" 2>&1 ;;
-splat)
-    lib1=$PWD/raytracingtest_amd/libsvo_rt.so; lib0=$PWD/build/ab/splat0/libsvo_rt.so
-    d() { local name=$1 lib=$2; shift 2
-          SVO_RT_LIB=$lib timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main "$@" > "$out/dropin_$name.txt" 2>&1; }
-    d ahead1a "$lib1" && d ahead0a "$lib0" && d ahead1b "$lib1" && d ahead0b "$lib0" ;;
 esac
