@@ -39,4 +39,15 @@ bandab)
 jitter)
     timeout -k 10 200 python -u tools/jitter_probe.py > "$out/jitter_probe.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/jitter_probe.py --set cost_history=0 > "$out/jitter_probe_h0.txt" 2>&1 ;;
+jitter2)
+    j() { local name=$1; shift; timeout -k 10 200 python -u tools/jitter_probe.py "$@" > "$out/jp_$name.txt" 2>&1; }
+    j default && j iss8 --set seg_table_issue=0x8 && j jit0 --set seg_jitter=0 && j jit1 --set seg_jitter=1 &&
+    j iss48 --set seg_table_issue=0x48 ;;
+pantrace)
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+    for dg in 0 1 2; do
+        SVO_BEAM_DIAG=$dg timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d "$out/pan_diag$dg" -o pan -- \
+            python3 tools/moving_camera.py --frames 200 > "$out/pan_diag$dg.txt" 2>&1 || exit 1
+    done ;;
+*) echo "unknown step $step"; exit 2 ;;
 esac

@@ -2,6 +2,7 @@
 the C3 render kernel (render_device, value's outputs, span per launch over back-to-back launches)
 under pixel-offset sequences that separate the ray set from the staleness of per-stream state:
   fixed(a, b)   the same offset every frame, for several offsets (is the (0.5, 0.5) ray set special?),
+  nudge         (0.5, 0.5) and its next float alternating: the jittered-launch policy on an unchanged ray set,
   alt           two offsets alternating (every frame's stored starts and costs are the other ray set's),
   random        a new seeded offset every frame (the drop-in's loop),
 and for `random` the per-launch kernel times (library events) against the offsets.
@@ -74,6 +75,9 @@ def main():
         out = {"pose": pose, "set": conf or "defaults"}
         for name, offs in (("fixed_0.5_0.5", [(0.5, 0.5)]), ("fixed_0.1_0.1", [(0.1, 0.1)]),
                            ("fixed_0.9_0.3", [(0.9, 0.3)]), ("fixed_0.25_0.75", [(0.25, 0.75)]),
+                           # the same rays every frame, but a "new" offset (one ulp apart) each frame: the
+                           # launch is a jittered one (even segment splits), the order's costs are its own
+                           ("nudge_0.5", [(0.5, 0.5), (float(np.nextafter(np.float32(0.5), np.float32(1))), 0.5)]),
                            ("alt_0.5_0.1", [(0.5, 0.5), (0.1, 0.1)]), ("random", [tuple(x) for x in rnd]),
                            ("fixed_0.5_0.5_again", [(0.5, 0.5)])):
             out[name] = round(run(offs), 4)
