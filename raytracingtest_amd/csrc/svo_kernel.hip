@@ -1146,7 +1146,8 @@ __device__ __forceinline__ float seg_start(const LaunchParams &p, const float *h
 // the part's wave-uniform values need no SGPRs across the traversal loop).
 // Diagnostics (SVO_WAVE_LOG, p.wave_log != null): per workgroup of render_seg_kernel, at blockIdx.x:
 // [0] trace start, [1] trace end, [8] entry (s_memrealtime, 100 MHz), [2] the order entry,
-// [3] XCC_ID | the wave's trips << 8 (the band-floor decomposition, tools/band_floor.py).
+// [3] XCC_ID | the wave's trips << 8, [9] lane 0's end (after the rebalance, before a part's record
+// stores; after its stores for a whole tile) (the band-floor decomposition, tools/band_floor.py).
 __device__ __forceinline__ void seg_log(const LaunchParams &p, int slot, uint32_t v) {
     if (p.wave_log && threadIdx.x == 0) p.wave_log[WAVE_LOG_WORDS * (size_t)blockIdx.x + slot] = v;
 }
@@ -1229,6 +1230,7 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
             else reinterpret_cast<uint8_t *>(p.out.hitmask)[8 * (size_t)t + part] = (uint8_t)bits;
         }
     }
+    if (p.wave_log) seg_log(p, 9, now_100mhz());
     if (!writer || !inside) return;
     const float4 acc = accum_load(p, out_index(p, lr, gy, x));
     Record o;
@@ -1296,6 +1298,7 @@ void render_seg_kernel(LaunchParams p, int tiles_x) {
         }
         if (p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, (int)(SEG_COST_FLAG - 1));
         store_outputs(p.out, out_index(p, lr, gy, x), o, acc);
+        if (p.wave_log) seg_log(p, 9, now_100mhz());
         return;
     }
     if (code <= 4) seg_part<MODE, FA, 4>(p, stk_base, t, code - 1, bx, by);

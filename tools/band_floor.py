@@ -97,7 +97,7 @@ def main():
     logged_ms = band_ms(ml, band, 1)
     ml.close()
     rec = np.fromfile(log, np.uint32).reshape(-1, WORDS).astype(np.int64)
-    entry, t0, t1, code, trips = rec[:, 8], rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3] >> 8
+    entry, t0, t1, code, trips, ex = rec[:, 8], rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3] >> 8, rec[:, 9]
     traced = (t1 > 0) & (t0 > 0)
     base = entry[entry > 0].min()
     ent, st, en = entry - base, t0 - base, t1 - base
@@ -114,6 +114,10 @@ def main():
             "empty_slots": int(((code & 0xFFFFFFFF) == 0xFFFFFFFF).sum()),
             "part_workgroups": int(((code >> 28) > 0).sum() - ((code & 0xFFFFFFFF) == 0xFFFFFFFF).sum()),
             "first_to_last_trace_end_us": round(en[traced].max() * tick, 2),
+            "first_to_last_exit_us": round((ex[traced & (ex > 0)] - base).max() * tick, 2) if (traced & (ex > 0)).any() else None,
+            "latest_exit": {"order_entry": hex(int(code[int(np.argmax(np.where(traced & (ex > 0), ex, 0)))])),
+                            "trips": int(trips[int(np.argmax(np.where(traced & (ex > 0), ex, 0)))]),
+                            "entry_us": round(float(ent[int(np.argmax(np.where(traced & (ex > 0), ex, 0)))]) * tick, 2)},
             "heaviest": {"order_entry": hex(int(code[k])), "trips": int(trips[k]),
                          "ramp_us": round(ent[k] * tick, 2), "setup_us": round((st[k] - ent[k]) * tick, 2),
                          "chain_us": round(dur[k] * tick, 2),

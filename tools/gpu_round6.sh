@@ -49,5 +49,11 @@ pantrace)
         SVO_BEAM_DIAG=$dg timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d "$out/pan_diag$dg" -o pan -- \
             python3 tools/moving_camera.py --frames 200 > "$out/pan_diag$dg.txt" 2>&1 || exit 1
     done ;;
+bandab2)
+    bf() { local name=$1 n=$2; shift 2
+           timeout -k 10 150 python -u tools/band_floor.py --gpus $n --out "$out/bf_${name}_$n.json" "$@" \
+               > "$out/bf_${name}_$n.txt" 2>&1; }
+    bf default 8 && bf t4 8 --set seg_table_thin=0x8888 && bf t48 8 --set seg_table_thin=0x4888 &&
+    bf t448 8 --set seg_table_thin=0x44888 --set seg_cap=192 && bf default 4 && bf l48 4 --set seg_table_latency=0x4444 ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac
