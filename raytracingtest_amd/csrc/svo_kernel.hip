@@ -1045,6 +1045,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
         if (lane == 0) p.out.hitmask[t] = hm;
     }
     if (p.tile_cost && (!SH || lane == 0)) p.tile_cost[t] = (uint16_t)min(trips, 65535);
+    if (p.cost_max && lane == 0) atomicMax(p.cost_max + t, (uint32_t)trips);
     if (p.wave_log && lane == 0) {   // 100 MHz constant clock, tile, XCC_ID
         uint32_t *w = p.wave_log + WAVE_LOG_WORDS * (size_t)blockIdx.x;
         w[8] = t_entry;
@@ -1213,6 +1214,7 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
         if (lane == 0) {
             p.part_cost[SEG_KMAX * (size_t)t + part] = (uint16_t)min(m, (uint32_t)(SEG_COST_FLAG - 1));
             if (part == 0) p.tile_cost[t] = (uint16_t)(SEG_COST_FLAG | K);
+            if (p.cost_max) atomicMax(p.cost_max + t, m);
         }
     }
     if (p.out.hitmask) {   // this part's R pixels: bits part * R .. part * R + R - 1 of the tile's mask
@@ -1297,6 +1299,7 @@ void render_seg_kernel(LaunchParams p, int tiles_x) {
             if (lane == 0) p.out.hitmask[t] = hm;
         }
         if (p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, (int)(SEG_COST_FLAG - 1));
+        if (p.cost_max && lane == 0) atomicMax(p.cost_max + t, (uint32_t)f.trips);
         store_outputs(p.out, out_index(p, lr, gy, x), o, acc);
         if (p.wave_log) seg_log(p, 9, now_100mhz());
         return;
@@ -1366,6 +1369,7 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
     Record o;
     record(p, r, x, gy, o);   // p.out.rgba is set (the accumulation), so the hit is shaded
     if (k == 0 && lane == 0 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);
+    if (k == 0 && lane == 0 && p.cost_max) atomicMax(p.cost_max + t, (uint32_t)f.trips);
     // the colour into this wave's own stack region (dead now; 16 B per lane <= the stack's share)
     float4 *col = reinterpret_cast<float4 *>(stk_base + (size_t)k * region);
     col[lane] = make_float4(o.rgb[0], o.rgb[1], o.rgb[2], 1.0f);
@@ -1800,8 +1804,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
                                                                      uint32_t *stats, int seg_cap,
                                                                      const uint16_t *__restrict__ part_cost,
                                                                      int seg_kpack, int spread,
-                                                                     const uint16_t *__restrict__ hist_in,
-                                                                     uint16_t *__restrict__ hist_out) {
+                                                                     uint32_t *cost_max, int decay) {
     __shared__ uint32_t red[ORDER_THREADS / 64], red_sum[ORDER_THREADS / 64];
     constexpr int NC = 6;
     __shared__ uint32_t cnt[NC], base[NC + 1], rank[NC], segs[NC];
@@ -1829,14 +1832,16 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         if (w.r >= tiles_y) { w.r -= tiles_y; w.c += 1; }
     };
     auto tile_of = [&](const Walk &w) { return w.r * tiles_x + strip_col(x, w.c); };
-    // history (hist_in != null: the same view as the previous build, costs drifting with the pixel
-    // offset -- the drop-in's jittered frame loop): a tile is classed by the max of its cost now and its
-    // decayed cost of earlier builds, so a tile whose cost depends on the sub-pixel offset keeps the
-    // class of its heavier offsets; hist_out = that decayed max (a separate buffer: no build reads
-    // what another XCD's workgroup of the same build writes)
+    // recent maximum (cost_max != null: the renders since the previous build atomicMax'ed each tile's
+    // cost in): a tile is classed by the max of its cost now and that recent max, so a tile that is
+    // heavy only at some sub-pixel offsets (the drop-in's jittered loop) or some of the last few views
+    // keeps the class of its heavier rays; the build then decays the max (>> decay) for the next one
+    // decay < 0 (the first build at a view the camera now holds): the launch's own costs, and the max
+    // restarts from them
+    const bool use_max = cost_max && decay >= 0;
     auto eff_cost = [&](int t) -> uint32_t {
         const uint32_t k = cost_at(t);
-        return hist_in ? max(k, (uint32_t)hist_in[t]) : k;
+        return use_max ? max(k, cost_max[t]) : k;
     };
     // spread (a moving camera: the costs are a few frames old and the heavy tiles have drifted by up to
     // a tile on screen): a tile's class is that of the heaviest of it and its 8 neighbours
@@ -1861,11 +1866,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         const uint32_t k = cost_at(t);
         mx = max(mx, k);
         sum += k;
-        if (hist_out) {
-            const uint32_t h = hist_in ? hist_in[t] : 0u;
-            mxe = max(mxe, max(k, h));
-            hist_out[t] = (uint16_t)max(k, h - (h >> 3));
-        }
+        if (use_max) mxe = max(mxe, max(k, cost_max[t]));
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -1893,7 +1894,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         stats[2 * x] = mx;
         stats[2 * x + 1] = sum;
     }
-    if (hist_in) mx = max(mx, mxe);   // the classes scale with the costs they are taken from
+    if (use_max) mx = max(mx, mxe);   // the classes scale with the costs they are taken from
     // six classes, the top half split three ways so the very heaviest tiles are the
     // XCD's first dispatches (they bound the launch); the render kernel's s_setprio
     // classes are >= 1/2, >= 1/4, >= 1/8 of the XCD's max and the rest
@@ -1935,11 +1936,19 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         }
     }
     for (int j = (int)base[NC] + tid; j < L; j += ORDER_THREADS) order[(size_t)j * 8 + x] = SEG_EMPTY;
+    if (cost_max) {   // (another XCD's workgroup may still read a neighbour's value: placement only)
+        __syncthreads();
+        for (Walk w = start(); w.e < len; next(w)) {
+            const int t = tile_of(w);
+            const uint32_t e = use_max ? max(cost_at(t), cost_max[t]) : cost_at(t);
+            cost_max[t] = use_max ? e - (e >> decay) : e;
+        }
+    }
 }
 
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
                                uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_kpack, int spread,
-                               const uint16_t *hist_in, uint16_t *hist_out) {
+                               uint32_t *cost_max, int decay) {
     if (n_tiles <= 0) return hipSuccess;
     if (seg_cap > 0 && (n_tiles / tiles_x) * tiles_x != n_tiles) return hipErrorInvalidValue;
     for (int c = 0; c < 6; ++c) {
@@ -1949,7 +1958,7 @@ hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tile
     if (seg_cap > 0 && ((size_t)order_strips_grid(n_tiles, seg_cap, seg_kmax_of(seg_kpack)) >> 28) != 0)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
-                       stats, seg_cap, part_cost, seg_kpack, spread, hist_in, hist_out);
+                       stats, seg_cap, part_cost, seg_kpack, spread, cost_max, decay);
     return hipGetLastError();
 }
 

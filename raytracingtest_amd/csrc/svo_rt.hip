@@ -115,9 +115,8 @@ struct Sched {
     bool build_seen[2] = {};             // the render stream already waits for it (or it completed)
     Geo build_key[2];
     int next_buf = 0;
-    uint16_t *hist[2] = {};            // cost history of the order builds at a held view (svo_config.cost_history)
-    int hist_cur = 0;                  // hist[hist_cur] holds the last build's
-    bool hist_valid = false;           // ... made at the current geometry and view
+    uint32_t *cost_max = nullptr;      // each tile's recent maximum cost (svo_config.cost_history) ...
+    Geo cost_max_key;                  // ... at this geometry (another one: zeroed first)
     uint16_t *shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
     uint32_t *shadow_order = nullptr;
     size_t cap = 0;
@@ -418,7 +417,7 @@ void reset_builds(Sched &q) {
         q.build_key[i] = Geo();
     }
     q.order_key = q.shadow_key = Geo();
-    q.hist_valid = false;
+    q.cost_max_key = Geo();
 }
 
 void free_sched(Sched &q) {
@@ -426,13 +425,13 @@ void free_sched(Sched &q) {
         if (q.cost_buf[i]) hipFree(q.cost_buf[i]);
         if (q.part_buf[i]) hipFree(q.part_buf[i]);
         if (q.order_buf[i]) hipFree(q.order_buf[i]);
-        if (q.hist[i]) hipFree(q.hist[i]);
-        q.hist[i] = nullptr;
         q.cost_buf[i] = q.part_buf[i] = nullptr;
         q.order_buf[i] = nullptr;
     }
     if (q.shadow_cost) hipFree(q.shadow_cost);
     if (q.shadow_order) hipFree(q.shadow_order);
+    if (q.cost_max) hipFree(q.cost_max);
+    q.cost_max = nullptr;
     q.shadow_cost = nullptr;
     q.shadow_order = nullptr;
     q.cap = 0;
@@ -1101,9 +1100,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 HIP_TRY(hipMalloc(&q->part_buf[i], svo::SEG_KMAX * cap * sizeof(uint16_t)));
                 HIP_TRY(hipMemset(q->part_buf[i], 0, svo::SEG_KMAX * cap * sizeof(uint16_t)));
                 HIP_TRY(hipMalloc(&q->order_buf[i], order_need * sizeof(uint32_t)));
-                HIP_TRY(hipMalloc(&q->hist[i], cap * sizeof(uint16_t)));
             }
-            q->hist_valid = false;
+            HIP_TRY(hipMalloc(&q->cost_max, cap * sizeof(uint32_t)));
+            q->cost_max_key = Geo();
             HIP_TRY(hipMalloc(&q->shadow_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(q->shadow_cost, 0, cap * sizeof(uint16_t)));
             HIP_TRY(hipMalloc(&q->shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
@@ -1131,6 +1130,13 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         }
         p.tile_cost = q->cost_buf[q->launches & 1];   // this launch's costs (see Sched)
         p.part_cost = q->part_buf[q->launches & 1];
+        if (ctx->cost_history && p.xcd_remap == 2) {   // the recent maximum, restarted at another geometry
+            if (q->cost_max_key != key) {
+                HIP_TRY(hipMemsetAsync(q->cost_max, 0, (size_t)n_tiles * sizeof(uint32_t), s));
+                q->cost_max_key = key;
+            }
+            p.cost_max = q->cost_max;
+        }
         if (p.shadows == 1 && ctx->shadow_order_enabled) {
             p.shadow_cost = q->shadow_cost;
             p.shadow_order = q->shadow_key == key ? q->shadow_order : nullptr;
@@ -1425,21 +1431,18 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         // on the side stream, behind this launch (its costs; and every launch that read buffer bi)
         HIP_TRY(hipEventRecord(q->render_done, s));
         HIP_TRY(hipStreamWaitEvent(q->side, q->render_done, 0));
-        // cost history: a build at the view (and geometry) of the previous one folds that build's
-        // decayed costs in (a held view, costs drifting with the pixel offset); any other starts afresh
-        const bool same = q->hist_valid && q->built_view == ctx->view_gen && [&] {
-            Geo g = q->order_key; g.seg = g.kpack = 0; return g == key; }();
-        const bool hist = ctx->cost_history && p.xcd_remap == 2 && !moving_build;
-        const uint16_t *h_in = hist && same ? q->hist[q->hist_cur] : nullptr;
-        uint16_t *h_out = hist ? q->hist[q->hist_cur ^ 1] : nullptr;
+        // the recent maximum: decayed by 1/8 per build at a held view (a build every order_every-th
+        // launch), by 1/2 while the camera moves (a build every move_every-th launch, views apart);
+        // the first build at a view the camera then holds restarts it from that launch's costs (after
+        // a jump to another pose no build may inherit the old pose's heavy tiles)
+        uint32_t *cmax = p.cost_max;
+        const int decay = moving_build ? 1 : q->built_view != ctx->view_gen ? -1 : 3;
         e = p.xcd_remap == 2 ? svo::launch_order_strips(p.tile_cost, q->order_buf[bi], n_tiles, (width + 7) / 8, q->side,
                                                         st16, okey.seg, p.part_cost, okey.kpack,
-                                                        moving_build && ctx->spread ? 1 : 0, h_in, h_out)
+                                                        moving_build && ctx->spread ? 1 : 0, cmax, decay)
                              : svo::launch_order_tiles(p.tile_cost, q->order_buf[bi], n_tiles, q->side, st16);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         HIP_TRY(hipEventRecord(q->build_ev[bi], q->side));
-        if (h_out) q->hist_cur ^= 1;
-        q->hist_valid = h_out != nullptr;
         q->build_at[bi] = (long long)q->launches - 1;   // launches was incremented above
         q->build_seen[bi] = false;
         q->build_key[bi] = okey;

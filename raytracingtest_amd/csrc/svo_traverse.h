@@ -92,6 +92,7 @@ struct LaunchParams {
     // and records its wave trip count in tile_cost.
     const uint32_t *tile_order;   // n_tiles entries + 36 class boundaries
     uint16_t *tile_cost;
+    uint32_t *cost_max;           // nullable: every launch atomicMax'es each tile's cost in (order builds decay it)
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
     int fetch_all;                // lean loop (!guard): every lane loads its node every trip
@@ -183,13 +184,12 @@ size_t order_cost_capacity(int n_tiles);
 // 4 c .. 4 c + 3: 0 = not segmented, 4 or 8.
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
                                uint32_t *stats = nullptr, int seg_cap = 0, const uint16_t *part_cost = nullptr,
-                               int seg_kpack = 0, int spread = 0, const uint16_t *hist_in = nullptr,
-                               uint16_t *hist_out = nullptr);
+                               int seg_kpack = 0, int spread = 0, uint32_t *cost_max = nullptr, int decay = 3);
 // spread != 0: each tile is classed by the heaviest cost of its 3x3 neighbourhood (costs recorded a few
 // frames before, while the camera moves); the stats stay those of the tiles themselves.
-// hist_out (nullable, n_tiles entries): written with each tile's decayed cost history max(cost,
-// h - h / 8), h = hist_in[t] (0 without hist_in); hist_in (nullable): the previous build's, and then
-// every tile is classed by max(cost, h) -- a held view whose costs drift with the pixel offset.
+// cost_max (nullable, n_tiles entries): each tile's recent maximum cost (the renders atomicMax their
+// costs in, LaunchParams::cost_max); every tile is classed by max(cost, cost_max), and the build then
+// decays the maximum, cost_max = m - (m >> decay) -- costs that drift with the pixel offset or view.
 __host__ __device__ inline int seg_kmax_of(int kpack) {
     int m = 1;
     for (int c = 0; c < 6; ++c) {
