@@ -1799,12 +1799,56 @@ size_t order_cost_capacity(int n_tiles) {
 // stats (nullable, host-visible): [2 x] = the max and [2 x + 1] = the sum of XCD x's tile
 // costs -- the launch's heaviest wave and its total wave trips, which the host uses to pick
 // the loop form of the next launches (svo_rt.hip launch).
+// A tile's cost as the last launch recorded it: its wave's trips, or for a segmented tile the max of
+// its parts' continuous-equivalent trips (render_seg_kernel)
+__device__ __forceinline__ uint32_t recorded_cost(const uint16_t *cost_in, const uint16_t *part_cost, int t) {
+    const uint32_t k = cost_in[t];
+    if (!(k & SEG_COST_FLAG) || !part_cost) return k & 0x7FFFu;
+    const uint4 q = *reinterpret_cast<const uint4 *>(part_cost + SEG_KMAX * (size_t)t);
+    uint32_t m = max(max(q.x & 0xFFFFu, q.x >> 16), max(q.y & 0xFFFFu, q.y >> 16));
+    if ((k & 15u) == 8u) m = max(m, max(max(q.z & 0xFFFFu, q.z >> 16), max(q.w & 0xFFFFu, q.w >> 16)));
+    return m;
+}
+
+// The class cost of every tile for an order build that needs more than the tile's own cost -- the
+// recent maximum (cost_max, use_max) and, while the camera moves, the max over the 3x3 neighbourhood
+// (spread): one thread per tile, so the neighbourhood's loads overlap across the chip instead of
+// queueing in the order kernel's eight workgroups (a moving build took 61 us there, on 8 CUs beside
+// the render: profiles/r06_pan_splat_diag.txt).
+__global__ __launch_bounds__(256) void class_cost_kernel(const uint16_t *__restrict__ cost_in,
+                                                         const uint16_t *__restrict__ part_cost,
+                                                         const uint32_t *__restrict__ cost_max, int use_max, int spread,
+                                                         int n, int tiles_x, uint16_t *__restrict__ eff_out) {
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= n) return;
+    auto eff = [&](int u) {
+        const uint32_t k = recorded_cost(cost_in, part_cost, u);
+        return use_max ? max(k, cost_max[u]) : k;
+    };
+    uint32_t m = 0;
+    if (!spread) {
+        m = eff(t);
+    } else {
+        const int tiles_y = n / tiles_x, r0 = t / tiles_x, c0 = t - r0 * tiles_x;
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int r = r0 + dy;
+            if (r < 0 || r >= tiles_y) continue;
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int c = c0 + dx;
+                if (c >= 0 && c < tiles_x) m = max(m, eff(r * tiles_x + c));
+            }
+        }
+    }
+    eff_out[t] = (uint16_t)min(m, 0xFFFFu);
+}
+
 __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint16_t *__restrict__ cost_in,
                                                                      uint32_t *__restrict__ order, int n, int tiles_x,
                                                                      uint32_t *stats, int seg_cap,
                                                                      const uint16_t *__restrict__ part_cost,
                                                                      int seg_kpack, int spread,
-                                                                     uint32_t *cost_max, int decay) {
+                                                                     uint32_t *cost_max, int decay,
+                                                                     const uint16_t *__restrict__ eff_in) {
     __shared__ uint32_t red[ORDER_THREADS / 64], red_sum[ORDER_THREADS / 64];
     constexpr int NC = 6;
     __shared__ uint32_t cnt[NC], base[NC + 1], rank[NC], segs[NC];
@@ -1812,14 +1856,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     const int len = n / 8, tiles_y = n / tiles_x;
     const int L = len + (seg_kmax_of(seg_kpack) - 1) * seg_cap;   // every XCD's list length (grid = 8 L)
     // a segmented tile's parts recorded their own continuous-equivalent trips (render_seg_kernel)
-    auto cost_at = [&](int t) -> uint32_t {
-        const uint32_t k = cost_in[t];
-        if (!(k & SEG_COST_FLAG) || !part_cost) return k & 0x7FFFu;
-        const uint4 q = *reinterpret_cast<const uint4 *>(part_cost + SEG_KMAX * (size_t)t);
-        uint32_t m = max(max(q.x & 0xFFFFu, q.x >> 16), max(q.y & 0xFFFFu, q.y >> 16));
-        if ((k & 15u) == 8u) m = max(m, max(max(q.z & 0xFFFFu, q.z >> 16), max(q.w & 0xFFFFu, q.w >> 16)));
-        return m;
-    };
+    auto cost_at = [&](int t) -> uint32_t { return recorded_cost(cost_in, part_cost, t); };
     // position e of this XCD's list is (column c = e / tiles_y, row e % tiles_y) of its
     // strips (strip_tile); the threads walk it in steps of ORDER_THREADS with one
     // division at the start instead of integer divisions per element (11.6 -> 9.7 us
@@ -1845,8 +1882,10 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     };
     // spread (a moving camera: the costs are a few frames old and the heavy tiles have drifted by up to
     // a tile on screen): a tile's class is that of the heaviest of it and its 8 neighbours
+    // eff_in (class_cost_kernel's output): the class costs precomputed one thread per tile
     auto class_cost = [&](const Walk &w) -> uint32_t {
         const int col = strip_col(x, w.c);
+        if (eff_in) return eff_in[w.r * tiles_x + col];
         if (!spread) return eff_cost(w.r * tiles_x + col);
         uint32_t m = 0;
         for (int dy = -1; dy <= 1; ++dy) {
@@ -1866,7 +1905,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         const uint32_t k = cost_at(t);
         mx = max(mx, k);
         sum += k;
-        if (use_max) mxe = max(mxe, max(k, cost_max[t]));
+        if (use_max) mxe = max(mxe, eff_in ? (uint32_t)eff_in[t] : max(k, cost_max[t]));
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -1948,7 +1987,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
 
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
                                uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_kpack, int spread,
-                               uint32_t *cost_max, int decay) {
+                               uint32_t *cost_max, int decay, uint16_t *eff_scratch) {
     if (n_tiles <= 0) return hipSuccess;
     if (seg_cap > 0 && (n_tiles / tiles_x) * tiles_x != n_tiles) return hipErrorInvalidValue;
     for (int c = 0; c < 6; ++c) {
@@ -1957,8 +1996,15 @@ hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tile
     }
     if (seg_cap > 0 && ((size_t)order_strips_grid(n_tiles, seg_cap, seg_kmax_of(seg_kpack)) >> 28) != 0)
         return hipErrorInvalidValue;
+    const bool use_max = cost_max && decay >= 0;
+    const uint16_t *eff = nullptr;
+    if (eff_scratch && (use_max || spread)) {   // the class costs one thread per tile first
+        hipLaunchKernelGGL(class_cost_kernel, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, stream, cost,
+                           part_cost, cost_max, use_max ? 1 : 0, spread, n_tiles, tiles_x, eff_scratch);
+        eff = eff_scratch;
+    }
     hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
-                       stats, seg_cap, part_cost, seg_kpack, spread, cost_max, decay);
+                       stats, seg_cap, part_cost, seg_kpack, spread, cost_max, decay, eff);
     return hipGetLastError();
 }
 

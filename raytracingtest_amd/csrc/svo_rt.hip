@@ -115,6 +115,7 @@ struct Sched {
     bool build_seen[2] = {};             // the render stream already waits for it (or it completed)
     Geo build_key[2];
     int next_buf = 0;
+    uint16_t *eff_buf = nullptr;       // the class costs of a build with a maximum or spread (class_cost_kernel)
     uint32_t *cost_max = nullptr;      // each tile's recent maximum cost (svo_config.cost_history) ...
     Geo cost_max_key;                  // ... at this geometry (another one: zeroed first)
     uint16_t *shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
@@ -432,6 +433,8 @@ void free_sched(Sched &q) {
     if (q.shadow_order) hipFree(q.shadow_order);
     if (q.cost_max) hipFree(q.cost_max);
     q.cost_max = nullptr;
+    if (q.eff_buf) hipFree(q.eff_buf);
+    q.eff_buf = nullptr;
     q.shadow_cost = nullptr;
     q.shadow_order = nullptr;
     q.cap = 0;
@@ -1102,6 +1105,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 HIP_TRY(hipMalloc(&q->order_buf[i], order_need * sizeof(uint32_t)));
             }
             HIP_TRY(hipMalloc(&q->cost_max, cap * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&q->eff_buf, cap * sizeof(uint16_t)));
             q->cost_max_key = Geo();
             HIP_TRY(hipMalloc(&q->shadow_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(q->shadow_cost, 0, cap * sizeof(uint16_t)));
@@ -1439,7 +1443,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         const int decay = moving_build ? 1 : q->built_view != ctx->view_gen ? -1 : 3;
         e = p.xcd_remap == 2 ? svo::launch_order_strips(p.tile_cost, q->order_buf[bi], n_tiles, (width + 7) / 8, q->side,
                                                         st16, okey.seg, p.part_cost, okey.kpack,
-                                                        moving_build && ctx->spread ? 1 : 0, cmax, decay)
+                                                        moving_build && ctx->spread ? 1 : 0, cmax, decay, q->eff_buf)
                              : svo::launch_order_tiles(p.tile_cost, q->order_buf[bi], n_tiles, q->side, st16);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         HIP_TRY(hipEventRecord(q->build_ev[bi], q->side));
