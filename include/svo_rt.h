@@ -129,7 +129,6 @@ typedef struct svo_config {
     int32_t  move_every;         /* >= 1: while the camera moves, rebuild every k-th launch (4) */
     int32_t  move_spread;        /* 1: a moving camera's order classes a tile by its 3x3 neighbourhood (1) */
     int32_t  relayout;           /* 1: rebuild once in a new class table's own layout (1) */
-    int32_t  cost_history;       /* 1: at a held view, class tiles by their decayed max cost over the builds (1) */
     int32_t  fetch_all;          /* -1: by pool size (< 2^24 nodes: 1); 0: fetch on a changed node; 1: every trip */
     /* loop form */
     int32_t  loop_form;          /* -1: by the last order build's statistics; 0: lean; 1: latency form */

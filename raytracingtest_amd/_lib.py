@@ -92,7 +92,7 @@ CONFIG_VERSION = 1
 _i32, _u32, _f32 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_float
 CONFIG_FIELDS = [
     ("tile_order", _i32), ("xcd_strips", _i32), ("issue_priority", _i32), ("order_every", _i32),
-    ("move_every", _i32), ("move_spread", _i32), ("relayout", _i32), ("cost_history", _i32), ("fetch_all", _i32),
+    ("move_every", _i32), ("move_spread", _i32), ("relayout", _i32), ("fetch_all", _i32),
     ("loop_form", _i32), ("lat_ratio", _f32),
     ("segments", _i32), ("seg_table_latency", _u32), ("seg_table_issue", _u32), ("seg_table_thin", _u32),
     ("seg_ratio", _f32), ("seg_thin_ratio", _f32), ("seg_cap", _i32), ("seg_min_chain", _i32),

@@ -1045,7 +1045,6 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR))
         if (lane == 0) p.out.hitmask[t] = hm;
     }
     if (p.tile_cost && (!SH || lane == 0)) p.tile_cost[t] = (uint16_t)min(trips, 65535);
-    if (p.cost_max && lane == 0) atomicMax(p.cost_max + t, (uint32_t)trips);
     if (p.wave_log && lane == 0) {   // 100 MHz constant clock, tile, XCC_ID
         uint32_t *w = p.wave_log + WAVE_LOG_WORDS * (size_t)blockIdx.x;
         w[8] = t_entry;
@@ -1214,7 +1213,6 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
         if (lane == 0) {
             p.part_cost[SEG_KMAX * (size_t)t + part] = (uint16_t)min(m, (uint32_t)(SEG_COST_FLAG - 1));
             if (part == 0) p.tile_cost[t] = (uint16_t)(SEG_COST_FLAG | K);
-            if (p.cost_max) atomicMax(p.cost_max + t, m);
         }
     }
     if (p.out.hitmask) {   // this part's R pixels: bits part * R .. part * R + R - 1 of the tile's mask
@@ -1299,7 +1297,6 @@ void render_seg_kernel(LaunchParams p, int tiles_x) {
             if (lane == 0) p.out.hitmask[t] = hm;
         }
         if (p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, (int)(SEG_COST_FLAG - 1));
-        if (p.cost_max && lane == 0) atomicMax(p.cost_max + t, (uint32_t)f.trips);
         store_outputs(p.out, out_index(p, lr, gy, x), o, acc);
         if (p.wave_log) seg_log(p, 9, now_100mhz());
         return;
@@ -1369,7 +1366,6 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
     Record o;
     record(p, r, x, gy, o);   // p.out.rgba is set (the accumulation), so the hit is shaded
     if (k == 0 && lane == 0 && p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, 65535);
-    if (k == 0 && lane == 0 && p.cost_max) atomicMax(p.cost_max + t, (uint32_t)f.trips);
     // the colour into this wave's own stack region (dead now; 16 B per lane <= the stack's share)
     float4 *col = reinterpret_cast<float4 *>(stk_base + (size_t)k * region);
     col[lane] = make_float4(o.rgb[0], o.rgb[1], o.rgb[2], 1.0f);
@@ -1799,56 +1795,11 @@ size_t order_cost_capacity(int n_tiles) {
 // stats (nullable, host-visible): [2 x] = the max and [2 x + 1] = the sum of XCD x's tile
 // costs -- the launch's heaviest wave and its total wave trips, which the host uses to pick
 // the loop form of the next launches (svo_rt.hip launch).
-// A tile's cost as the last launch recorded it: its wave's trips, or for a segmented tile the max of
-// its parts' continuous-equivalent trips (render_seg_kernel)
-__device__ __forceinline__ uint32_t recorded_cost(const uint16_t *cost_in, const uint16_t *part_cost, int t) {
-    const uint32_t k = cost_in[t];
-    if (!(k & SEG_COST_FLAG) || !part_cost) return k & 0x7FFFu;
-    const uint4 q = *reinterpret_cast<const uint4 *>(part_cost + SEG_KMAX * (size_t)t);
-    uint32_t m = max(max(q.x & 0xFFFFu, q.x >> 16), max(q.y & 0xFFFFu, q.y >> 16));
-    if ((k & 15u) == 8u) m = max(m, max(max(q.z & 0xFFFFu, q.z >> 16), max(q.w & 0xFFFFu, q.w >> 16)));
-    return m;
-}
-
-// The class cost of every tile for an order build that needs more than the tile's own cost -- the
-// recent maximum (cost_max, use_max) and, while the camera moves, the max over the 3x3 neighbourhood
-// (spread): one thread per tile, so the neighbourhood's loads overlap across the chip instead of
-// queueing in the order kernel's eight workgroups (a moving build took 61 us there, on 8 CUs beside
-// the render: profiles/r06_pan_splat_diag.txt).
-__global__ __launch_bounds__(256) void class_cost_kernel(const uint16_t *__restrict__ cost_in,
-                                                         const uint16_t *__restrict__ part_cost,
-                                                         const uint32_t *__restrict__ cost_max, int use_max, int spread,
-                                                         int n, int tiles_x, uint16_t *__restrict__ eff_out) {
-    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (t >= n) return;
-    auto eff = [&](int u) {
-        const uint32_t k = recorded_cost(cost_in, part_cost, u);
-        return use_max ? max(k, cost_max[u]) : k;
-    };
-    uint32_t m = 0;
-    if (!spread) {
-        m = eff(t);
-    } else {
-        const int tiles_y = n / tiles_x, r0 = t / tiles_x, c0 = t - r0 * tiles_x;
-        for (int dy = -1; dy <= 1; ++dy) {
-            const int r = r0 + dy;
-            if (r < 0 || r >= tiles_y) continue;
-            for (int dx = -1; dx <= 1; ++dx) {
-                const int c = c0 + dx;
-                if (c >= 0 && c < tiles_x) m = max(m, eff(r * tiles_x + c));
-            }
-        }
-    }
-    eff_out[t] = (uint16_t)min(m, 0xFFFFu);
-}
-
 __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint16_t *__restrict__ cost_in,
                                                                      uint32_t *__restrict__ order, int n, int tiles_x,
                                                                      uint32_t *stats, int seg_cap,
                                                                      const uint16_t *__restrict__ part_cost,
-                                                                     int seg_kpack, int spread,
-                                                                     uint32_t *cost_max, int decay,
-                                                                     const uint16_t *__restrict__ eff_in) {
+                                                                     int seg_kpack, int spread) {
     __shared__ uint32_t red[ORDER_THREADS / 64], red_sum[ORDER_THREADS / 64];
     constexpr int NC = 6;
     __shared__ uint32_t cnt[NC], base[NC + 1], rank[NC], segs[NC];
@@ -1856,7 +1807,14 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
     const int len = n / 8, tiles_y = n / tiles_x;
     const int L = len + (seg_kmax_of(seg_kpack) - 1) * seg_cap;   // every XCD's list length (grid = 8 L)
     // a segmented tile's parts recorded their own continuous-equivalent trips (render_seg_kernel)
-    auto cost_at = [&](int t) -> uint32_t { return recorded_cost(cost_in, part_cost, t); };
+    auto cost_at = [&](int t) -> uint32_t {
+        const uint32_t k = cost_in[t];
+        if (!(k & SEG_COST_FLAG) || !part_cost) return k & 0x7FFFu;
+        const uint4 q = *reinterpret_cast<const uint4 *>(part_cost + SEG_KMAX * (size_t)t);
+        uint32_t m = max(max(q.x & 0xFFFFu, q.x >> 16), max(q.y & 0xFFFFu, q.y >> 16));
+        if ((k & 15u) == 8u) m = max(m, max(max(q.z & 0xFFFFu, q.z >> 16), max(q.w & 0xFFFFu, q.w >> 16)));
+        return m;
+    };
     // position e of this XCD's list is (column c = e / tiles_y, row e % tiles_y) of its
     // strips (strip_tile); the threads walk it in steps of ORDER_THREADS with one
     // division at the start instead of integer divisions per element (11.6 -> 9.7 us
@@ -1869,71 +1827,50 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         if (w.r >= tiles_y) { w.r -= tiles_y; w.c += 1; }
     };
     auto tile_of = [&](const Walk &w) { return w.r * tiles_x + strip_col(x, w.c); };
-    // recent maximum (cost_max != null: the renders since the previous build atomicMax'ed each tile's
-    // cost in): a tile is classed by the max of its cost now and that recent max, so a tile that is
-    // heavy only at some sub-pixel offsets (the drop-in's jittered loop) or some of the last few views
-    // keeps the class of its heavier rays; the build then decays the max (>> decay) for the next one
-    // decay < 0 (the first build at a view the camera now holds): the launch's own costs, and the max
-    // restarts from them
-    const bool use_max = cost_max && decay >= 0;
-    auto eff_cost = [&](int t) -> uint32_t {
-        const uint32_t k = cost_at(t);
-        return use_max ? max(k, cost_max[t]) : k;
-    };
     // spread (a moving camera: the costs are a few frames old and the heavy tiles have drifted by up to
     // a tile on screen): a tile's class is that of the heaviest of it and its 8 neighbours
-    // eff_in (class_cost_kernel's output): the class costs precomputed one thread per tile
     auto class_cost = [&](const Walk &w) -> uint32_t {
         const int col = strip_col(x, w.c);
-        if (eff_in) return eff_in[w.r * tiles_x + col];
-        if (!spread) return eff_cost(w.r * tiles_x + col);
+        if (!spread) return cost_at(w.r * tiles_x + col);
         uint32_t m = 0;
         for (int dy = -1; dy <= 1; ++dy) {
             const int r = w.r + dy;
             if (r < 0 || r >= tiles_y) continue;
             for (int dx = -1; dx <= 1; ++dx) {
                 const int c = col + dx;
-                if (c >= 0 && c < tiles_x) m = max(m, eff_cost(r * tiles_x + c));
+                if (c >= 0 && c < tiles_x) m = max(m, cost_at(r * tiles_x + c));
             }
         }
         return m;
     };
-    __shared__ uint32_t red_eff[ORDER_THREADS / 64];
-    uint32_t mx = 0, sum = 0, mxe = 0;
+    uint32_t mx = 0, sum = 0;
     for (Walk w = start(); w.e < len; next(w)) {
-        const int t = tile_of(w);
-        const uint32_t k = cost_at(t);
+        const uint32_t k = cost_at(tile_of(w));
         mx = max(mx, k);
         sum += k;
-        if (use_max) mxe = max(mxe, eff_in ? (uint32_t)eff_in[t] : max(k, cost_max[t]));
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
-        mxe = max(mxe, (uint32_t)__shfl_xor((int)mxe, d));
         sum += (uint32_t)__shfl_xor((int)sum, d);
     }
     if (lane == 0) {
         red[wave] = mx;
         red_sum[wave] = sum;
-        red_eff[wave] = mxe;
     }
     if (tid < NC) cnt[tid] = 0;
     __syncthreads();
     mx = 0;
     sum = 0;
-    mxe = 0;
 #pragma unroll
     for (int w = 0; w < ORDER_THREADS / 64; ++w) {
         mx = max(mx, red[w]);
         sum += red_sum[w];
-        mxe = max(mxe, red_eff[w]);
     }
-    if (stats && tid == 0) {   // the loop-form rule reads the launch's own costs
+    if (stats && tid == 0) {
         stats[2 * x] = mx;
         stats[2 * x + 1] = sum;
     }
-    if (use_max) mx = max(mx, mxe);   // the classes scale with the costs they are taken from
     // six classes, the top half split three ways so the very heaviest tiles are the
     // XCD's first dispatches (they bound the launch); the render kernel's s_setprio
     // classes are >= 1/2, >= 1/4, >= 1/8 of the XCD's max and the rest
@@ -1975,19 +1912,10 @@ __global__ __launch_bounds__(ORDER_THREADS) void order_strips_kernel(const uint1
         }
     }
     for (int j = (int)base[NC] + tid; j < L; j += ORDER_THREADS) order[(size_t)j * 8 + x] = SEG_EMPTY;
-    if (cost_max) {   // (another XCD's workgroup may still read a neighbour's value: placement only)
-        __syncthreads();
-        for (Walk w = start(); w.e < len; next(w)) {
-            const int t = tile_of(w);
-            const uint32_t e = use_max ? max(cost_at(t), cost_max[t]) : cost_at(t);
-            cost_max[t] = use_max ? e - (e >> decay) : e;
-        }
-    }
 }
 
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
-                               uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_kpack, int spread,
-                               uint32_t *cost_max, int decay, uint16_t *eff_scratch) {
+                               uint32_t *stats, int seg_cap, const uint16_t *part_cost, int seg_kpack, int spread) {
     if (n_tiles <= 0) return hipSuccess;
     if (seg_cap > 0 && (n_tiles / tiles_x) * tiles_x != n_tiles) return hipErrorInvalidValue;
     for (int c = 0; c < 6; ++c) {
@@ -1996,15 +1924,8 @@ hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tile
     }
     if (seg_cap > 0 && ((size_t)order_strips_grid(n_tiles, seg_cap, seg_kmax_of(seg_kpack)) >> 28) != 0)
         return hipErrorInvalidValue;
-    const bool use_max = cost_max && decay >= 0;
-    const uint16_t *eff = nullptr;
-    if (eff_scratch && (use_max || spread)) {   // the class costs one thread per tile first
-        hipLaunchKernelGGL(class_cost_kernel, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, stream, cost,
-                           part_cost, cost_max, use_max ? 1 : 0, spread, n_tiles, tiles_x, eff_scratch);
-        eff = eff_scratch;
-    }
     hipLaunchKernelGGL(order_strips_kernel, dim3(8), dim3(ORDER_THREADS), 0, stream, cost, order, n_tiles, tiles_x,
-                       stats, seg_cap, part_cost, seg_kpack, spread, cost_max, decay, eff);
+                       stats, seg_cap, part_cost, seg_kpack, spread);
     return hipGetLastError();
 }
 

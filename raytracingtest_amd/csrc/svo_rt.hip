@@ -115,9 +115,6 @@ struct Sched {
     bool build_seen[2] = {};             // the render stream already waits for it (or it completed)
     Geo build_key[2];
     int next_buf = 0;
-    uint16_t *eff_buf = nullptr;       // the class costs of a build with a maximum or spread (class_cost_kernel)
-    uint32_t *cost_max = nullptr;      // each tile's recent maximum cost (svo_config.cost_history) ...
-    Geo cost_max_key;                  // ... at this geometry (another one: zeroed first)
     uint16_t *shadow_cost = nullptr;   // the two-pass shadow form's own costs and order
     uint32_t *shadow_order = nullptr;
     size_t cap = 0;
@@ -344,7 +341,6 @@ struct svo_ctx {
     int seg_jitter = 2;              // env SVO_SEG_JITTER: a jittered launch (the one-sample samples route)
     int spread = 1;                  // env SVO_SPREAD=0: a moving camera's order classes tiles by their own costs only
     int relayout = 1;                // svo_config.relayout 0: keep an order built from costs of another class layout
-    int cost_history = 1;            // svo_config.cost_history: held-view builds class by the decayed max cost
     int seg_min_chain = 160;         // env SVO_SEG_MIN_CHAIN: a latency-bound launch whose heaviest tile costs fewer
                                      // trips takes the latency form, unsegmented, without beam starts
     float seg_ratio = 0.28f;         // svo_config.seg_ratio: ... and the same with beam starts (class table only)
@@ -418,7 +414,6 @@ void reset_builds(Sched &q) {
         q.build_key[i] = Geo();
     }
     q.order_key = q.shadow_key = Geo();
-    q.cost_max_key = Geo();
 }
 
 void free_sched(Sched &q) {
@@ -431,10 +426,6 @@ void free_sched(Sched &q) {
     }
     if (q.shadow_cost) hipFree(q.shadow_cost);
     if (q.shadow_order) hipFree(q.shadow_order);
-    if (q.cost_max) hipFree(q.cost_max);
-    q.cost_max = nullptr;
-    if (q.eff_buf) hipFree(q.eff_buf);
-    q.eff_buf = nullptr;
     q.shadow_cost = nullptr;
     q.shadow_order = nullptr;
     q.cap = 0;
@@ -1104,9 +1095,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 HIP_TRY(hipMemset(q->part_buf[i], 0, svo::SEG_KMAX * cap * sizeof(uint16_t)));
                 HIP_TRY(hipMalloc(&q->order_buf[i], order_need * sizeof(uint32_t)));
             }
-            HIP_TRY(hipMalloc(&q->cost_max, cap * sizeof(uint32_t)));
-            HIP_TRY(hipMalloc(&q->eff_buf, cap * sizeof(uint16_t)));
-            q->cost_max_key = Geo();
             HIP_TRY(hipMalloc(&q->shadow_cost, cap * sizeof(uint16_t)));
             HIP_TRY(hipMemset(q->shadow_cost, 0, cap * sizeof(uint16_t)));
             HIP_TRY(hipMalloc(&q->shadow_order, ((size_t)n_tiles + 36) * sizeof(uint32_t)));
@@ -1134,13 +1122,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         }
         p.tile_cost = q->cost_buf[q->launches & 1];   // this launch's costs (see Sched)
         p.part_cost = q->part_buf[q->launches & 1];
-        if (ctx->cost_history && p.xcd_remap == 2) {   // the recent maximum, restarted at another geometry
-            if (q->cost_max_key != key) {
-                HIP_TRY(hipMemsetAsync(q->cost_max, 0, (size_t)n_tiles * sizeof(uint32_t), s));
-                q->cost_max_key = key;
-            }
-            p.cost_max = q->cost_max;
-        }
         if (p.shadows == 1 && ctx->shadow_order_enabled) {
             p.shadow_cost = q->shadow_cost;
             p.shadow_order = q->shadow_key == key ? q->shadow_order : nullptr;
@@ -1435,15 +1416,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         // on the side stream, behind this launch (its costs; and every launch that read buffer bi)
         HIP_TRY(hipEventRecord(q->render_done, s));
         HIP_TRY(hipStreamWaitEvent(q->side, q->render_done, 0));
-        // the recent maximum: decayed by 1/8 per build at a held view (a build every order_every-th
-        // launch), by 1/2 while the camera moves (a build every move_every-th launch, views apart);
-        // the first build at a view the camera then holds restarts it from that launch's costs (after
-        // a jump to another pose no build may inherit the old pose's heavy tiles)
-        uint32_t *cmax = p.cost_max;
-        const int decay = moving_build ? 1 : q->built_view != ctx->view_gen ? -1 : 3;
         e = p.xcd_remap == 2 ? svo::launch_order_strips(p.tile_cost, q->order_buf[bi], n_tiles, (width + 7) / 8, q->side,
                                                         st16, okey.seg, p.part_cost, okey.kpack,
-                                                        moving_build && ctx->spread ? 1 : 0, cmax, decay, q->eff_buf)
+                                                        moving_build && ctx->spread ? 1 : 0)
                              : svo::launch_order_tiles(p.tile_cost, q->order_buf[bi], n_tiles, q->side, st16);
         if (e != hipSuccess) return fail(SVO_ERR_HIP, std::string("tile order launch: ") + hipGetErrorString(e));
         HIP_TRY(hipEventRecord(q->build_ev[bi], q->side));
@@ -1789,7 +1764,6 @@ void config_of(const svo_ctx *c, svo_config *o) {
     k.move_every = c->move_every;
     k.move_spread = c->spread;
     k.relayout = c->relayout;
-    k.cost_history = c->cost_history;
     k.fetch_all = c->fetch_all;
     k.loop_form = c->lat_mode;
     k.lat_ratio = c->lat_ratio;
@@ -1830,7 +1804,7 @@ int check_config(const svo_config &k) {
     const char *bad = !bit(k.tile_order) ? "tile_order" : !bit(k.xcd_strips) ? "xcd_strips"
                     : !bit(k.issue_priority) ? "issue_priority" : k.order_every < 1 ? "order_every"
                     : k.move_every < 1 ? "move_every" : !bit(k.move_spread) ? "move_spread"
-                    : !bit(k.relayout) ? "relayout" : !bit(k.cost_history) ? "cost_history" : k.fetch_all < -1 || k.fetch_all > 1 ? "fetch_all"
+                    : !bit(k.relayout) ? "relayout" : k.fetch_all < -1 || k.fetch_all > 1 ? "fetch_all"
                     : k.loop_form < -1 || k.loop_form > 1 ? "loop_form" : !ratio(k.lat_ratio) ? "lat_ratio"
                     : !bit(k.segments) ? "segments" : !table(k.seg_table_latency) ? "seg_table_latency"
                     : !table(k.seg_table_issue) ? "seg_table_issue" : !table(k.seg_table_thin) ? "seg_table_thin"
@@ -1858,7 +1832,6 @@ int apply_config(svo_ctx *c, const svo_config &k) {
     c->move_every = k.move_every;
     c->spread = k.move_spread;
     c->relayout = k.relayout;
-    c->cost_history = k.cost_history;
     c->fetch_all = k.fetch_all;
     c->lat_mode = k.loop_form;
     c->lat_ratio = k.lat_ratio;

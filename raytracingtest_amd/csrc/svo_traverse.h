@@ -92,7 +92,6 @@ struct LaunchParams {
     // and records its wave trip count in tile_cost.
     const uint32_t *tile_order;   // n_tiles entries + 36 class boundaries
     uint16_t *tile_cost;
-    uint32_t *cost_max;           // nullable: every launch atomicMax'es each tile's cost in (order builds decay it)
     int prio;                     // s_setprio by cost class (env SVO_PRIO)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
     int fetch_all;                // lean loop (!guard): every lane loads its node every trip
@@ -184,16 +183,9 @@ size_t order_cost_capacity(int n_tiles);
 // 4 c .. 4 c + 3: 0 = not segmented, 4 or 8.
 hipError_t launch_order_strips(const uint16_t *cost, uint32_t *order, int n_tiles, int tiles_x, hipStream_t stream,
                                uint32_t *stats = nullptr, int seg_cap = 0, const uint16_t *part_cost = nullptr,
-                               int seg_kpack = 0, int spread = 0, uint32_t *cost_max = nullptr, int decay = 3,
-                               uint16_t *eff_scratch = nullptr);
+                               int seg_kpack = 0, int spread = 0);
 // spread != 0: each tile is classed by the heaviest cost of its 3x3 neighbourhood (costs recorded a few
 // frames before, while the camera moves); the stats stay those of the tiles themselves.
-// cost_max (nullable, n_tiles entries): each tile's recent maximum cost (the renders atomicMax their
-// costs in, LaunchParams::cost_max); every tile is classed by max(cost, cost_max), and the build then
-// decays the maximum, cost_max = m - (m >> decay) -- costs that drift with the pixel offset or view;
-// decay < 0: classes from the launch's own costs, and the maximum restarts from them.
-// eff_scratch (nullable, n_tiles entries): with a maximum or spread, the class costs are first
-// computed one thread per tile into it (class_cost_kernel), the order kernel then reads one word per tile.
 __host__ __device__ inline int seg_kmax_of(int kpack) {
     int m = 1;
     for (int c = 0; c < 6; ++c) {

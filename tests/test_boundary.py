@@ -158,7 +158,7 @@ def test_profile_key_does_not_depend_on_the_tree_location(tmp_path):
 
 CONFIG_DEFAULTS = {
     "tile_order": 1, "xcd_strips": 1, "issue_priority": 1, "order_every": 32, "move_every": 4, "move_spread": 1,
-    "relayout": 1, "cost_history": 1, "fetch_all": -1, "loop_form": -1, "lat_ratio": 0.3, "segments": 1, "seg_table_latency": 0x444,
+    "relayout": 1, "fetch_all": -1, "loop_form": -1, "lat_ratio": 0.3, "segments": 1, "seg_table_latency": 0x444,
     "seg_table_issue": 0x4, "seg_table_thin": 0x888, "seg_ratio": 0.28, "seg_thin_ratio": 0.083, "seg_cap": 96,
     "seg_min_chain": 160, "seg_move": 2, "seg_jitter": 2, "seg_all": 0, "seg_scramble": 0, "beam": 1, "beam_back": 2,
     "shadow_form": 0, "shadow_order": 1, "readback": 0, "host_copy_threads": 0, "sparse_payload": 0, "peer_copy": 0}
@@ -178,7 +178,7 @@ def test_config_struct_size_version_and_layout(tmp_path):
     subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o",
                     str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
-    assert int(out[0]) == ctypes.sizeof(_lib.SvoConfig) == 132
+    assert int(out[0]) == ctypes.sizeof(_lib.SvoConfig) == 128
     assert int(out[1]) == _lib.CONFIG_VERSION == 1
     for f, off in zip(fields, out[2:]):
         assert int(off) == getattr(_lib.SvoConfig, f).offset, f

@@ -55,8 +55,5 @@ bandab2)
                > "$out/bf_${name}_$n.txt" 2>&1; }
     bf default 8 && bf t4 8 --set seg_table_thin=0x8888 && bf t48 8 --set seg_table_thin=0x4888 &&
     bf t448 8 --set seg_table_thin=0x44888 --set seg_cap=192 && bf default 4 && bf l48 4 --set seg_table_latency=0x4444 ;;
-jitter3)
-    j() { local name=$1; shift; timeout -k 10 200 python -u tools/jitter_probe.py "$@" > "$out/jp_$name.txt" 2>&1; }
-    j default && j h0 --set cost_history=0 && dropin default && dropin h0 --set cost_history=0 ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac

@@ -47,8 +47,8 @@ public static class SvoNative {
     [StructLayout(LayoutKind.Sequential)]
     public struct SvoConfig {
         public uint size, version;
-        public int tileOrder, xcdStrips, issuePriority, orderEvery, moveEvery, moveSpread, relayout, costHistory,
-                   fetchAll, loopForm;
+        public int tileOrder, xcdStrips, issuePriority, orderEvery, moveEvery, moveSpread, relayout, fetchAll,
+                   loopForm;
         public float latRatio;
         public int segments;
         public uint segTableLatency, segTableIssue, segTableThin;
@@ -108,7 +108,6 @@ public class RaytracingMasterNative : MonoBehaviour {
     public bool segmentedRays = true;            // segments: heavy tiles traced as exact t-segments
     public bool costOrderedDispatch = true;      // tile_order: heaviest tiles dispatched first
     [Range(1, 32)] public int moveEvery = 4;     // while the camera moves, rebuild the order every k-th frame
-    public bool costHistory = true;              // a held view's order keeps tiles' heaviest recent costs
     public enum ShadowForm { Fused = 0, TilePass = 1, CompactedList = 2 }
     public ShadowForm shadowForm = ShadowForm.Fused;
 
@@ -161,7 +160,6 @@ public class RaytracingMasterNative : MonoBehaviour {
         cfg.segments = segmentedRays ? 1 : 0;
         cfg.tileOrder = costOrderedDispatch ? 1 : 0;
         cfg.moveEvery = moveEvery;
-        cfg.costHistory = costHistory ? 1 : 0;
         cfg.shadowForm = (int)shadowForm;
         SvoNative.Check(SvoNative.svo_set_config(_ctx, ref cfg), "svo_set_config");
     }
