@@ -21,6 +21,31 @@ policy)
 occupancy)
     lib8=$PWD/raytracingtest_amd/libsvo_rt.so; lib7=$PWD/build/ab/seg7/libsvo_rt.so
     bench_lib w8a "$lib8" && bench_lib w7a "$lib7" && bench_lib w8b "$lib8" && bench_lib w7b "$lib7" ;;
+r05ab)
+    # the round-5 tree (build/ab/r05tree, its own bench.py and libraries) against this one, and the
+    # unbounded-occupancy segmented kernel (seg7), interleaved, on the configs the round-5 table lists
+    one() { local name=$1 dir=$2 lib=$3; shift 3
+            (cd "$dir" && SVO_RT_LIB=$lib timeout -k 10 150 python -u bench.py --no-extras --cpu-seconds 0 "$@") \
+                > "$out/ab_$name.json" 2> "$out/ab_$name.err"; }
+    r6=$PWD; r5=$PWD/build/ab/r05tree; l6=$r6/raytracingtest_amd/libsvo_rt.so; l5=$r5/raytracingtest_amd/libsvo_rt.so
+    l7=$r6/build/ab/seg7/libsvo_rt.so
+    for rep in a b; do
+        one c5_r6$rep $r6 $l6 --config C5 --steps 300 --warmup 20 && one c5_r5$rep $r5 $l5 --config C5 --steps 300 --warmup 20 &&
+        one c5_w7$rep $r6 $l7 --config C5 --steps 300 --warmup 20 &&
+        one c4_r6$rep $r6 $l6 --config C4 --steps 300 --warmup 20 && one c4_r5$rep $r5 $l5 --config C4 --steps 300 --warmup 20 &&
+        one ov_r6$rep $r6 $l6 --camera overview && one ov_r5$rep $r5 $l5 --camera overview && one ov_w7$rep $r6 $l7 --camera overview &&
+        one fly_r6$rep $r6 $l6 && one fly_r5$rep $r5 $l5 || exit $?
+    done ;;
+bisect)
+    # C4 (one GPU, overview) on the round-5 tree, the round-6 commits touching the kernels, and this
+    # tree, interleaved: where the round's C4/C5 slowdown came in (build/ab/t_<commit>)
+    one() { local name=$1 dir=$2; shift 2
+            (cd "$dir" && timeout -k 10 150 python -u bench.py --no-extras --cpu-seconds 0 --config C4 --steps 300 --warmup 20 "$@") \
+                > "$out/bis_$name.json" 2> "$out/bis_$name.err"; }
+    for rep in a b; do
+        one r05$rep build/ab/r05tree && one 8096f73$rep build/ab/t_8096f73 && one c48f03c$rep build/ab/t_c48f03c &&
+        one e8037cc$rep build/ab/t_e8037cc && one head$rep . || exit $?
+    done ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&

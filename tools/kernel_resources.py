@@ -1,7 +1,7 @@
 """Per-kernel register / scratch / occupancy of libsvo_rt's kernels as the compiler reports them
 (-Rpass-analysis=kernel-resource-usage, the build's own flags), one line per kernel.
 
-  python tools/kernel_resources.py [--filter render_]
+  python tools/kernel_resources.py [--filter render_] [-D SVO_SEG_WAVES_PER_EU=1]
 """
 import argparse
 import os
@@ -18,12 +18,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--filter", default="render_")
     ap.add_argument("--source", default=os.path.join(ROOT, "raytracingtest_amd", "csrc", "svo_kernel.hip"))
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra -D definitions (A/B builds)")
     a = ap.parse_args()
     from raytracingtest_amd import build
     flags = [f for f in build.COMMON if f not in ("-shared", "-fPIC")]
     with tempfile.TemporaryDirectory() as td:
         r = subprocess.run([build.HIPCC, "--offload-arch=" + build.ARCH] + flags +
-                           ["-c", a.source, "-o", os.path.join(td, "k.o"), "-Rpass-analysis=kernel-resource-usage"],
+                           ["-D" + d for d in a.defines] + ["-c", a.source, "-o", os.path.join(td, "k.o"), "-Rpass-analysis=kernel-resource-usage"],
                            capture_output=True, text=True)
     cur = None
     rows = {}

@@ -1,5 +1,5 @@
-"""A/B of the render loop's latency form (trace_lat, env SVO_LAT=1) against the lean loop
-(SVO_LAT=0) and the library's automatic choice (SVO_LAT unset) on launches of decreasing size: the whole C3 frame, one rank's band of the strong
+"""A/B of the render loop's latency form (trace_lat, svo_config.loop_form 1) against the lean loop
+(loop_form 0) and the library's automatic choice (loop_form -1) on launches of decreasing size: the whole C3 frame, one rank's band of the strong
 1920x1080 split at N = 2, 4, 8 (round-robin 8-row bands), and the tile row holding the
 frame's heaviest tile alone.  Kernel time = the library's HIP events around the render
 kernel (mean of K launches after warmup).  Both contexts render the same frame; their hit
@@ -34,12 +34,8 @@ def main():
     cam = CAMERAS[a.camera or cfg["camera"]]()
     svo = build_sampler_svo(cfg["sampler"], cfg["max_level"])
     ctx = {}
-    for name, lat in (("lean", "0"), ("lat", "1"), ("auto", None)):
-        if lat is None:
-            os.environ.pop("SVO_LAT", None)
-        else:
-            os.environ["SVO_LAT"] = lat
-        rm = RaytracingMaster(capacity_nodes=len(svo))
+    for name, lat in (("lean", 0), ("lat", 1), ("auto", -1)):
+        rm = RaytracingMaster(capacity_nodes=len(svo), config={"loop_form": lat})
         rm.SetSVOBuffer(svo)
         rm.UpdateShaderParameters(cam, W, H)
         ctx[name] = rm

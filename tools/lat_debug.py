@@ -1,6 +1,6 @@
 """The automatic loop-form choice across camera jumps, submitted the way bench.py's
 extra_poses does (10 + 20 launches per pose, no host sync between them): prints the
-library's decisions (SVO_LAT_DEBUG) and each pose's kernel time.  A pose must get the
+library's decisions (SVO_DEBUG=1: one 'svo lat:' line per order build) and each pose's kernel time.  A pose must get the
 form its own costs call for, not the previous pose's.
 
   python tools/lat_debug.py [--config C3]
@@ -13,7 +13,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["SVO_LAT_DEBUG"] = "1"
+os.environ["SVO_DEBUG"] = "1"   # read when a context is created
 
 
 def main():

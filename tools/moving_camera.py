@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--cycle", type=int, default=0,
                     help="diagnostics: cycle through the first k views of the pan (a new view per frame, "
                          "views repeating) instead of panning on")
+    ap.add_argument("--move-every", type=int, default=None, help="svo_config.move_every (default: the library's)")
     a = ap.parse_args()
     import torch
     from bench import CONFIGS
@@ -34,7 +35,7 @@ def main():
     W, H = cfg["width"], cfg["height"]
     from raytracingtest_amd.native_builder import build_sampler_svo
     svo = build_sampler_svo(cfg["sampler"], cfg["max_level"])
-    rm = RaytracingMaster(capacity_nodes=len(svo))
+    rm = RaytracingMaster(capacity_nodes=len(svo), config={} if a.move_every is None else {"move_every": a.move_every})
     rm.SetSVOBuffer(svo)
     light = np.ascontiguousarray(main_light(), np.float32)
     views = []
@@ -85,7 +86,7 @@ def main():
             rm.set_kernel_timing(False)
             torch.cuda.synchronize()
             out.setdefault(name, []).append((ms, kms))
-            print(f"SVO_MOVE_EVERY={os.environ.get('SVO_MOVE_EVERY', 'default')} round {rnd} {name:6s}: {ms * 1e3:6.1f} us per frame (host issue {t_host / a.frames * 1e6:5.1f} us), "
+            print(f"move_every={a.move_every or 'default'} round {rnd} {name:6s}: {ms * 1e3:6.1f} us per frame (host issue {t_host / a.frames * 1e6:5.1f} us), "
                   f"render kernel {kms * 1e3:6.1f} us", flush=True)
     rm.close()
 

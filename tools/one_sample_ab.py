@@ -1,9 +1,10 @@
 """One-sample route against the render launch on the C3 frame: GPU span per
 launch of render_frame (hits + RGBA32F, hits only) and of svo_render_samples with one sample per
 launch -- a new jittered offset each launch, without the display words, and one fixed offset --
-then render_frame again, per camera; SVO_SEG_JITTER / SVO_SEG_MOVE from the environment.
+then render_frame again, per camera; optional svo_config fields as field=value after the cameras
+(e.g. seg_jitter=1 seg_move=1).
 
-  SVO_SEG_JITTER=1 python tools/one_sample_ab.py flyover,overview > gpurun_out/one_sample.txt
+  python tools/one_sample_ab.py flyover,overview [seg_jitter=1] > gpurun_out/one_sample.txt
 """
 import os, sys, time, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -27,8 +28,9 @@ def span(fn, k=300):
     for _ in range(k): fn()
     e1.record(s); torch.cuda.synchronize()
     return e0.elapsed_time(e1) / k
+CONF = {kv.split("=")[0]: int(kv.split("=")[1], 0) for kv in sys.argv[2:]}
 for cam in sys.argv[1].split(","):
-    rm = RaytracingMaster(device=0, capacity_nodes=len(svo)); rm.SetSVOBuffer(svo)
+    rm = RaytracingMaster(device=0, capacity_nodes=len(svo), config=CONF); rm.SetSVOBuffer(svo)
     rm.UpdateShaderParameters(CAMERAS[cam](), W, H)
     n = [0]
     def r(): rm.render_frame(W, H, hits=hits.data_ptr(), rgba=rgba.data_ptr(), stream=s.cuda_stream)

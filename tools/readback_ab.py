@@ -1,6 +1,6 @@
 """A/B of svo_render_progressive_async's readback: per-frame host time of
 the C3 1080p progressive loop through the pipelined entry point, with the frame's RGBA8 words
-moved to the pinned slot by one DMA copy (SVO_PIN_PUSH=0), a kernel writing the mapped pinned
+moved to the pinned slot by one DMA copy (svo_config.readback 0), a kernel writing the mapped pinned
 buffer (1) or two DMA copies on two streams (2), and one DMA copy of 3-byte pixels (RGB24); the
 blocking svo_render_progressive beside.
 Every mode's displayed frames are compared with the blocking path's for the same samples.
@@ -60,9 +60,8 @@ def main():
             ref.append(f.copy())
         out["blocking_svo_render_progressive_ms"] = round((time.perf_counter() - t) / 20 * 1e3, 4)
     for mode, rgb in ((0, False), (1, False), (2, False), (0, True)):
-        os.environ["SVO_PIN_PUSH"] = str(mode)
         key = f"async_push{mode}" + ("_rgb24" if rgb else "")
-        with RaytracingMaster(device=0, capacity_nodes=len(svo)) as rm:
+        with RaytracingMaster(device=0, capacity_nodes=len(svo), config={"readback": mode}) as rm:
             rm.SetSVOBuffer(svo)
             rm.UpdateShaderParameters(cam, W, H)
             got = []
@@ -84,7 +83,6 @@ def main():
         out[key] = {"ms_per_frame": round(ms, 4), "frames_compared": len(got), "frames_differing_from_blocking": bad,
                     "bytes_per_frame": W * H * (3 if rgb else 4)}
         print(json.dumps({key: out[key]}), file=sys.stderr, flush=True)
-    os.environ.pop("SVO_PIN_PUSH", None)
     print(json.dumps(out))
 
 

@@ -1,7 +1,8 @@
 """A/B of the segmented heavy tiles on the C3 frame: render-kernel time of the
 whole 1920x1080 flyover frame (N = 1) and of rank 1's round-robin 8-row band at N = 2, 4, 8 (the
-strong split's per-GPU launch), with SVO_SEG off and on (and the latency form's automatic choice
-in both), interleaved in one process (the env is read when a context is created).  Library
+strong split's per-GPU launch), with segments off and on (and the latency form's automatic choice
+in both), interleaved in one process; each variant is an svo_config (include/svo_rt.h) given to
+the context it creates.  Library
 events, median of --timed launches after a warmup past the clock ramp.
 
   python tools/seg_ab.py [--camera flyover] [--rounds 2] > gpurun_out/seg_ab.json
@@ -23,10 +24,10 @@ def main():
     ap.add_argument("--timed", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--variants", default="off,auto",
-                    help="comma list of: off (SVO_SEG=0), auto (the library's defaults), or '+'-joined "
-                         "l<hex> (SVO_SEG_LAT: K per cost class, class 0 in the low nibble), i<hex> (SVO_SEG_ISSUE), t<hex> (SVO_SEG_THIN), "
-                         "nobeam (SVO_BEAM=0) and norelayout (SVO_RELAYOUT=0)")
-    ap.add_argument("--cap", default=None, help="SVO_SEG_CAP")
+                    help="comma list of: off (segments = 0), auto (the library's defaults), or '+'-joined "
+                         "l<hex> (seg_table_latency: K per cost class, class 0 in the low nibble), i<hex> "
+                         "(seg_table_issue), t<hex> (seg_table_thin), nobeam (beam = 0) and norelayout (relayout = 0)")
+    ap.add_argument("--cap", default=None, help="seg_cap")
     ap.add_argument("--cameras", default=None, help="comma list (default: --camera)")
     a = ap.parse_args()
     import torch
@@ -45,25 +46,24 @@ def main():
     cams = (a.cameras or a.camera).split(",")
     for rnd in range(a.rounds):
         for name in a.variants.split(","):
-            for k in ("SVO_SEG", "SVO_SEG_LAT", "SVO_SEG_ISSUE", "SVO_SEG_CAP", "SVO_BEAM", "SVO_RELAYOUT", "SVO_SEG_THIN"):
-                os.environ.pop(k, None)
+            conf = {}
             for part in name.split("+"):
                 if part == "off":
-                    os.environ["SVO_SEG"] = "0"
-                elif part.startswith("l"):     # l<hex>: SVO_SEG_LAT, the class table of latency-bound launches
-                    os.environ["SVO_SEG_LAT"] = part[1:]
-                elif part.startswith("i"):     # i<hex>: SVO_SEG_ISSUE, the same for issue-bound launches
-                    os.environ["SVO_SEG_ISSUE"] = part[1:]
-                elif part.startswith("t"):     # t<hex>: SVO_SEG_THIN, the table of thin latency-bound launches
-                    os.environ["SVO_SEG_THIN"] = part[1:]
-                elif part == "nobeam":         # SVO_BEAM=0: rays from the cube entry
-                    os.environ["SVO_BEAM"] = "0"
-                elif part == "norelayout":     # SVO_RELAYOUT=0: keep the first order built at a new class table
-                    os.environ["SVO_RELAYOUT"] = "0"
+                    conf["segments"] = 0
+                elif part.startswith("l"):     # l<hex>: the class table of latency-bound launches
+                    conf["seg_table_latency"] = int(part[1:], 16)
+                elif part.startswith("i"):     # i<hex>: the same for issue-bound launches
+                    conf["seg_table_issue"] = int(part[1:], 16)
+                elif part.startswith("t"):     # t<hex>: the table of thin latency-bound launches
+                    conf["seg_table_thin"] = int(part[1:], 16)
+                elif part == "nobeam":         # rays from the cube entry
+                    conf["beam"] = 0
+                elif part == "norelayout":     # keep the first order built at a new class table
+                    conf["relayout"] = 0
             if a.cap:
-                os.environ["SVO_SEG_CAP"] = a.cap
+                conf["seg_cap"] = int(a.cap, 0)
             for cam in cams:
-                rm = RaytracingMaster(device=0, capacity_nodes=len(svo))
+                rm = RaytracingMaster(device=0, capacity_nodes=len(svo), config=conf)
                 rm.SetSVOBuffer(svo)
                 rm.UpdateShaderParameters(CAMERAS[cam](), W, H)
                 for _ in range(400):   # past the DVFS ramp
