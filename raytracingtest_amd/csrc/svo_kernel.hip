@@ -1148,12 +1148,14 @@ __device__ __forceinline__ float seg_start(const LaunchParams &p, const float *h
 // [0] trace start, [1] trace end, [8] entry (s_memrealtime, 100 MHz), [2] the order entry,
 // [3] XCC_ID | the wave's trips << 8, [9] lane 0's end (after the rebalance, before a part's record
 // stores; after its stores for a whole tile) (the band-floor decomposition, tools/band_floor.py).
+// The stamps are a template flag (LOG, launched only when p.wave_log is set): compiled into the
+// product kernel behind a runtime test they cost C4's launch 4-5 % (profiles/r06_seg_log_ab.json).
 __device__ __forceinline__ void seg_log(const LaunchParams &p, int slot, uint32_t v) {
-    if (p.wave_log && threadIdx.x == 0) p.wave_log[WAVE_LOG_WORDS * (size_t)blockIdx.x + slot] = v;
+    if (threadIdx.x == 0) p.wave_log[WAVE_LOG_WORDS * (size_t)blockIdx.x + slot] = v;
 }
 __device__ __forceinline__ uint32_t now_100mhz() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
 
-template <int MODE, bool FA, int K>
+template <int MODE, bool FA, int K, bool LOG>
 __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restrict__ stk_base, int t, int part, int bx,
                                          int by) {
     const int lane = threadIdx.x;
@@ -1189,10 +1191,10 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
     const float t_stop = seg_start(p, hint8, have, hi, e1, t_entry, t_exit);
     uint32_t n_lane, armed_at;
     bool stopped;
-    if (p.wave_log) seg_log(p, 0, now_100mhz());
+    if (LOG) seg_log(p, 0, now_100mhz());
     trace_seg<MODE, FA, true, false, K>(p, f, stk, k == 0 ? bs : t_start, t_stop, k == 0 && r.t_min >= bs, n_lane, armed_at,
                         stopped);
-    if (p.wave_log) {
+    if (LOG) {
         seg_log(p, 1, now_100mhz());
         seg_log(p, 3, ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFFu) | ((uint32_t)f.trips << 8));
     }
@@ -1230,7 +1232,7 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
             else reinterpret_cast<uint8_t *>(p.out.hitmask)[8 * (size_t)t + part] = (uint8_t)bits;
         }
     }
-    if (p.wave_log) seg_log(p, 9, now_100mhz());
+    if (LOG) seg_log(p, 9, now_100mhz());
     if (!writer || !inside) return;
     const float4 acc = accum_load(p, out_index(p, lr, gy, x));
     Record o;
@@ -1238,7 +1240,7 @@ __device__ __forceinline__ void seg_part(const LaunchParams &p, uint2 *__restric
     store_outputs(p.out, out_index(p, lr, gy, x), o, acc);
 }
 
-template <int MODE, bool FA, bool LAT>
+template <int MODE, bool FA, bool LAT, bool LOG>
 // VGPR budget: unbounded, the compiler gave this kernel 68-70 VGPRs -- 7 waves per SIMD (a wave needs
 // <= 64 for 8, MI355X_MICROARCH.md occupancy table).  Asking for 8 waves per EU fits it in 64 VGPRs at
 // the cost of one spilled dword, stored and reloaded outside the traversal loop (tools/kernel_resources.py).
@@ -1249,9 +1251,9 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_num_sgpr(SVO_NUM_SGPR),
 void render_seg_kernel(LaunchParams p, int tiles_x) {
     extern __shared__ uint2 stk_base[];
     const int lane = threadIdx.x;
-    const uint32_t t_in = p.wave_log ? now_100mhz() : 0u;
+    const uint32_t t_in = LOG ? now_100mhz() : 0u;
     const uint32_t entry = p.tile_order[blockIdx.x];
-    if (p.wave_log) {
+    if (LOG) {
         seg_log(p, 8, t_in);
         seg_log(p, 2, entry);
     }
@@ -1280,11 +1282,11 @@ void render_seg_kernel(LaunchParams p, int tiles_x) {
         }
         FRay f;
         to_fray(r, f);
-        if (p.wave_log) seg_log(p, 0, now_100mhz());
+        if (LOG) seg_log(p, 0, now_100mhz());
         if (LAT) trace_lat<MODE>(p, f, stk);
         else if (p.tile_start) trace_beam<MODE, FA>(p, f, stk, beam_start(p, f, x, gy));
         else trace_lean<MODE, false, false, FA>(p, f, stk);
-        if (p.wave_log) {
+        if (LOG) {
             seg_log(p, 1, now_100mhz());
             seg_log(p, 3, ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xFFu) | ((uint32_t)f.trips << 8));
         }
@@ -1298,11 +1300,11 @@ void render_seg_kernel(LaunchParams p, int tiles_x) {
         }
         if (p.tile_cost) p.tile_cost[t] = (uint16_t)min(f.trips, (int)(SEG_COST_FLAG - 1));
         store_outputs(p.out, out_index(p, lr, gy, x), o, acc);
-        if (p.wave_log) seg_log(p, 9, now_100mhz());
+        if (LOG) seg_log(p, 9, now_100mhz());
         return;
     }
-    if (code <= 4) seg_part<MODE, FA, 4>(p, stk_base, t, code - 1, bx, by);
-    else seg_part<MODE, FA, 8>(p, stk_base, t, code - 5, bx, by);
+    if (code <= 4) seg_part<MODE, FA, 4, LOG>(p, stk_base, t, code - 1, bx, by);
+    else seg_part<MODE, FA, 8, LOG>(p, stk_base, t, code - 5, bx, by);
 }
 
 // ------------------------------------------------------------- samples in flight
@@ -1646,12 +1648,18 @@ static hipError_t launch_variant(const LaunchParams &p, hipStream_t stream) {
     }
     if (!COUNT && p.seg > 0) {   // segmented heavy tiles (the order was built with seg_cap = p.seg)
         const dim3 sgrid((unsigned)order_strips_grid(bx * by, p.seg, p.seg_kmax));
-        if (p.lat)
-            hipLaunchKernelGGL((render_seg_kernel<MODE, true, true>), sgrid, block, 2 * lds, stream, p, bx);
+        if (p.lat && p.wave_log)
+            hipLaunchKernelGGL((render_seg_kernel<MODE, true, true, true>), sgrid, block, 2 * lds, stream, p, bx);
+        else if (p.lat)
+            hipLaunchKernelGGL((render_seg_kernel<MODE, true, true, false>), sgrid, block, 2 * lds, stream, p, bx);
+        else if (p.fetch_all && p.wave_log)
+            hipLaunchKernelGGL((render_seg_kernel<MODE, true, false, true>), sgrid, block, lds, stream, p, bx);
         else if (p.fetch_all)
-            hipLaunchKernelGGL((render_seg_kernel<MODE, true, false>), sgrid, block, lds, stream, p, bx);
+            hipLaunchKernelGGL((render_seg_kernel<MODE, true, false, false>), sgrid, block, lds, stream, p, bx);
+        else if (p.wave_log)
+            hipLaunchKernelGGL((render_seg_kernel<MODE, false, false, true>), sgrid, block, lds, stream, p, bx);
         else
-            hipLaunchKernelGGL((render_seg_kernel<MODE, false, false>), sgrid, block, lds, stream, p, bx);
+            hipLaunchKernelGGL((render_seg_kernel<MODE, false, false, false>), sgrid, block, lds, stream, p, bx);
         return hipGetLastError();
     }
     if (COUNT)

@@ -46,6 +46,55 @@ bisect)
         one r05$rep build/ab/r05tree && one 8096f73$rep build/ab/t_8096f73 && one c48f03c$rep build/ab/t_c48f03c &&
         one e8037cc$rep build/ab/t_e8037cc && one head$rep . || exit $?
     done ;;
+logab)
+    # C4 and C3 flyover: this tree against itself without the segmented kernel's wave-log stamps
+    # (SVO_SEG_LOG=0, build/ab/nolog, nolog7 = also unbounded VGPRs) and the last tree before them
+    one() { local name=$1 dir=$2 lib=$3; shift 3
+            (cd "$dir" && SVO_RT_LIB=$lib timeout -k 10 150 python -u bench.py --no-extras --cpu-seconds 0 "$@") \
+                > "$out/lg_$name.json" 2> "$out/lg_$name.err"; }
+    r6=$PWD; l6=$r6/raytracingtest_amd/libsvo_rt.so; ln=$r6/build/ab/nolog/libsvo_rt.so; ln7=$r6/build/ab/nolog7/libsvo_rt.so
+    t8=$r6/build/ab/t_8096f73; l8=$t8/raytracingtest_amd/libsvo_rt.so
+    for rep in a b; do
+        for v in "head $r6 $l6" "nolog $r6 $ln" "nolog7 $r6 $ln7" "t8096 $t8 $l8"; do
+            set -- $v
+            one c4_$1$rep $2 $3 --config C4 --steps 300 --warmup 20 && one fly_$1$rep $2 $3 || exit $?
+        done
+    done
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null &&
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d "$out/c4prof" -o c4 -- \
+        python3 bench.py --no-extras --cpu-seconds 0 --config C4 --steps 100 --warmup 20 > "$out/c4prof.txt" 2>&1 ;;
+fixab)
+    # the template-flag wave log (this tree) against the last tree before the stamps and round 5's,
+    # on the configs that showed the stamps' cost
+    one() { local name=$1 dir=$2; shift 2
+            (cd "$dir" && timeout -k 10 200 python -u bench.py --no-extras --cpu-seconds 0 "$@") \
+                > "$out/fx_$name.json" 2> "$out/fx_$name.err"; }
+    for rep in a b; do
+        for v in "head ." "t8096 build/ab/t_8096f73" "r05 build/ab/r05tree"; do
+            set -- $v
+            one c4_$1$rep $2 --config C4 --steps 300 --warmup 20 && one fly_$1$rep $2 && one ov_$1$rep $2 --camera overview &&
+            one main_$1$rep $2 --camera main || exit $?
+        done
+        one c5_head$rep . --config C5 --steps 300 --warmup 20 && one c5_r05$rep build/ab/r05tree --config C5 --steps 300 --warmup 20 || exit $?
+    done ;;
+sgprab)
+    # the segmented kernel's node-pool pointer: reloaded from the kernel arguments every trip (head),
+    # pinned in SGPRs (pin), a larger SGPR budget (sgpr80), both (pin80); interleaved
+    one() { local name=$1 lib=$2; shift 2
+            SVO_RT_LIB=$lib timeout -k 10 200 python -u bench.py --no-extras --cpu-seconds 0 "$@" \
+                > "$out/sg_$name.json" 2> "$out/sg_$name.err"; }
+    for rep in a b; do
+        for v in head:raytracingtest_amd pin:build/ab/pin sgpr80:build/ab/sgpr80 pin80:build/ab/pin80; do
+            n=${v%%:*}; l=$PWD/${v#*:}/libsvo_rt.so
+            one fly_$n$rep $l && one main_$n$rep $l --camera main && one c4_$n$rep $l --config C4 --steps 300 --warmup 20 || exit $?
+        done
+    done ;;
+sq)
+    # SQ issue / wait counters of the segmented kernel (C3 flyover), the segmented parity tests, one
+    # wave-logged band (the LOG instantiation)
+    timeout -k 10 400 bash tools/pmc_sq.sh "$out/pmc_sq" render_seg_kernel > "$out/pmc_sq.txt" 2>&1 &&
+    timeout -k 10 300 python -u -m pytest tests/test_gpu_seg.py -x -q --timeout 120 --timeout-method thread > "$out/seg_tests.txt" 2>&1 &&
+    timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
