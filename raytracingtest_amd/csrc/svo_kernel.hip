@@ -2245,7 +2245,10 @@ hipError_t launch_assemble(const AssembleParams &a, hipStream_t stream) {
 // a workgroup's boxes cover a compact patch of the screen: their tiles are min-ed in an LDS window
 // first and each touched tile costs one global atomic per workgroup (device-scope atomics from
 // every XCD to one address serialise: one atomic per box-tile pair took 72 us per C3 frame).
-constexpr int SPLAT_THREADS = 512, SPLAT_WIN = 8192;
+#ifndef SVO_SPLAT_THREADS
+#define SVO_SPLAT_THREADS 512
+#endif
+constexpr int SPLAT_THREADS = SVO_SPLAT_THREADS, SPLAT_WIN = 8192;
 
 // no read first: a returning load before each atomic put a full memory round trip into every
 // iteration of the flush loop (24 us per C3 frame); the atomic alone returns nothing to wait for

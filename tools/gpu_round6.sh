@@ -95,6 +95,28 @@ sq)
     timeout -k 10 400 bash tools/pmc_sq.sh "$out/pmc_sq" render_seg_kernel > "$out/pmc_sq.txt" 2>&1 &&
     timeout -k 10 300 python -u -m pytest tests/test_gpu_seg.py -x -q --timeout 120 --timeout-method thread > "$out/seg_tests.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 ;;
+splatab)
+    # beam splat workgroup size (SVO_SPLAT_THREADS 512 / 256 / 128): the pan loop's frame and the
+    # splat kernel's own time (rocprofv3 kernel trace of the same loop)
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+    for rep in a b; do
+        for v in 512:raytracingtest_amd 256:build/ab/splat256 128:build/ab/splat128; do
+            n=${v%%:*}; l=$PWD/${v#*:}/libsvo_rt.so
+            SVO_RT_LIB=$l timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main > "$out/sp_$n$rep.txt" 2>&1 || exit $?
+        done
+    done
+    for v in 512:raytracingtest_amd 256:build/ab/splat256 128:build/ab/splat128; do
+        n=${v%%:*}; l=$PWD/${v#*:}/libsvo_rt.so
+        SVO_RT_LIB=$l timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d "$out/sp_prof_$n" -o sp -- \
+            python3 tools/dropin_loop.py --poses flyover --frames 200 > "$out/sp_prof_$n.txt" 2>&1 || exit $?
+    done ;;
+backab)
+    # splat depth (svo_config.beam_back 2 = default, 3, 4): held / jittered / pan frames
+    for rep in a b; do
+        for v in 2 3 4; do
+            timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main --set beam_back=$v > "$out/bb_$v$rep.txt" 2>&1 || exit $?
+        done
+    done ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
