@@ -159,3 +159,22 @@ def test_segmented_band_and_hit_masks(torch, oracle_mod, mode, k):
             assert np.array_equal(masks.cpu().numpy().view(np.uint64), want_masks), "hit masks differ"
     finally:
         m.close()
+
+
+@pytest.mark.parametrize("k", [4, 8])
+def test_wave_logged_segmented_launch_matches_oracle(torch, oracle_mod, text_svo, tmp_path, monkeypatch, k):
+    """The wave-logged instantiation of the segmented kernel (render_seg_kernel<..., LOG = true>,
+    launched only for a context created with SVO_WAVE_LOG): the same records as the oracle, and one
+    log record per workgroup with entry and trace stamps (tools/band_floor.py's input)."""
+    log = tmp_path / "wave_log.bin"
+    monkeypatch.setenv("SVO_WAVE_LOG", str(log))   # read when the context is created
+    # the log file holds the last launch; an order (and with it the segmented kernel) is in use from
+    # the launch after next (the order builds on a side stream)
+    _frames(torch, oracle_mod, text_svo, [main_camera()], 256, 256, 0, n_frames=4, config={"seg_all": k})
+    monkeypatch.delenv("SVO_WAVE_LOG")
+    rec = np.fromfile(log, np.uint32).reshape(-1, 12)
+    entry = rec[:, 2]
+    traced = entry != 0xFFFFFFFF
+    assert traced.sum() == (256 // 8) * (256 // 8) * k   # every tile's K parts, one workgroup each
+    assert ((entry[traced] >> 28) > 0).all()              # every entry a part (seg_all)
+    assert (rec[traced, 8] > 0).all() and (rec[traced, 0] > 0).all() and (rec[traced, 1] >= rec[traced, 0]).all()
