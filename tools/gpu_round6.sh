@@ -117,6 +117,12 @@ backab)
             timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main --set beam_back=$v > "$out/bb_$v$rep.txt" 2>&1 || exit $?
         done
     done ;;
+progtrace)
+    # the shim's per-frame call alone (held fixed / jittered / pan), then under a kernel + copy trace
+    timeout -k 10 150 python -u tools/progressive_trace.py > "$out/pt_plain.txt" 2>&1 &&
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null &&
+    timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace -f csv -d "$out/pt" -o pt -- \
+        python3 tools/progressive_trace.py > "$out/pt_prof.txt" 2>&1 ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
