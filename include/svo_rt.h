@@ -117,7 +117,7 @@ typedef struct svo_frame {
  * most `size` bytes.  svo_get_config(NULL, cfg) gives the defaults below.  Hex tables: one
  * nibble per cost class (lowest = heaviest: >= 7/8, 3/4, 1/2, 1/4, 1/8 of the heaviest tile,
  * rest), each 0 (whole tiles), 4 or 8 (t-segments per ray). */
-#define SVO_CONFIG_VERSION 1
+#define SVO_CONFIG_VERSION 2
 typedef struct svo_config {
     uint32_t size;               /* sizeof(svo_config) as compiled by the caller */
     uint32_t version;            /* SVO_CONFIG_VERSION (written by svo_get_config) */
@@ -159,6 +159,9 @@ typedef struct svo_config {
     /* multi-device contexts (svo_create_multi) */
     int32_t  sparse_payload;     /* 1: display-only frames travel as sparse hit payloads */
     int32_t  peer_copy;          /* 1: every member's payload copied instead of pulled over xGMI (tests) */
+    /* version 2 */
+    int32_t  beam_back_held;     /* a held view (the second launch at a view on a stream and later) re-splats
+                                    once with boxes this many levels above the leaves (0); -1: beam_back */
 } svo_config;
 int svo_get_config(svo_ctx *ctx, svo_config *cfg);
 int svo_set_config(svo_ctx *ctx, const svo_config *cfg);

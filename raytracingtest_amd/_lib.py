@@ -88,7 +88,7 @@ class SvoFrame(ctypes.Structure):
 
 
 # svo_config (include/svo_rt.h, ABI 10): the context's render policy, versioned by size
-CONFIG_VERSION = 1
+CONFIG_VERSION = 2   # 2: beam_back_held appended
 _i32, _u32, _f32 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_float
 CONFIG_FIELDS = [
     ("tile_order", _i32), ("xcd_strips", _i32), ("issue_priority", _i32), ("order_every", _i32),
@@ -100,7 +100,8 @@ CONFIG_FIELDS = [
     ("beam", _i32), ("beam_back", _i32),
     ("shadow_form", _i32), ("shadow_order", _i32),
     ("readback", _i32), ("host_copy_threads", _i32),
-    ("sparse_payload", _i32), ("peer_copy", _i32)]
+    ("sparse_payload", _i32), ("peer_copy", _i32),
+    ("beam_back_held", _i32)]   # version 2
 SHADOW_FUSED, SHADOW_TILES, SHADOW_LIST = 0, 1, 2   # svo_config.shadow_form
 
 

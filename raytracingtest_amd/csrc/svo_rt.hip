@@ -68,6 +68,16 @@ struct Upload {
     // host arrays at upload (null: none; a pool of several uploads is walked on the device copy)
     std::shared_ptr<const std::vector<uint2>> boxes;
     int boxes_back;      // the config's beam_back it was built with
+    std::shared_ptr<const std::vector<uint2>> boxes_held;   // ... and the held view's (beam_back_held)
+    int boxes_held_back;
+};
+
+// The device copy of a splat list (a context holds two: a moving camera's and a held view's)
+struct DevBoxes {
+    uint2 *d = nullptr;
+    size_t cap = 0;
+    uint32_t n = 0;
+    uint64_t id = 0;   // made from the list with this id (0: none)
 };
 
 enum { STAGE_KERNEL = 0, STAGE_ASSEMBLE = 1, N_STAGES = 2 };
@@ -127,6 +137,7 @@ struct Sched {
     unsigned long long ts_view = ~0ull; // ... splatted for this view, splat list and frame size
     uint64_t ts_boxes = 0;
     int ts_w = -1, ts_h = -1;
+    bool held_splat = false;           // this launch re-splatted a held view finer: its costs are new
     Geo order_key;                   // the newest build's key (width -1: none)
     Geo shadow_key;
     unsigned long long launches = 0, shadow_launches = 0;
@@ -251,6 +262,9 @@ struct svo_ctx {
     std::shared_ptr<const std::vector<uint2>> pool_boxes;
     uint64_t pool_boxes_id = 0;
     int pool_boxes_back = -1;
+    // ... and the finer one a held view re-splats with (beam_back_held; the same list when equal)
+    std::shared_ptr<const std::vector<uint2>> pool_boxes_held;
+    uint64_t pool_boxes_held_id = 0;
     // diagnostics (the library's only environment switches, read once at svo_create):
     // SVO_DEBUG bit 0 the loop-form / class-table decision trace, bit 1 the order each launch
     // takes; SVO_WAVE_LOG=<file> the per-wave record; SVO_BEAM_DIAG the splat's timing variants
@@ -321,12 +335,10 @@ struct svo_ctx {
     int seg_all = 0;                 // env SVO_SEG_ALL=4|8 (tests; 1 = 4): every tile segmented with that K
     uint32_t seg_scramble = 0;       // env SVO_SEG_SCRAMBLE=<seed> (tests): arbitrary segment starts
     uint32_t seg_launches = 0;
-    int beam = 1;                    // env SVO_BEAM=0: no beam starts
-    int beam_back = 2;               // env SVO_BEAM_BACK: splat the boxes this many levels above the leaves
-    uint2 *d_boxes = nullptr;        // the device copy of the root upload's splat list ...
-    size_t boxes_cap = 0;
-    uint32_t n_boxes = 0;
-    uint64_t boxes_id = 0;           // ... made from the list with this id (pool_boxes_id; 0: none)
+    int beam = 1;                    // svo_config.beam: beam starts
+    int beam_back = 2;               // svo_config.beam_back: a new view's splat, this many levels above the leaves
+    int beam_back_held = 0;          // svo_config.beam_back_held: a held view's (-1: beam_back)
+    DevBoxes dev_boxes[2];           // device copies of pool_boxes / pool_boxes_held
     unsigned long long *count_ts = nullptr;   // beam starts of an instrumented launch (SVO_OPT_COUNT_BEAM)
     size_t count_ts_cap = 0;
     uint32_t count_ts_gen = 0;
@@ -580,6 +592,9 @@ std::shared_ptr<const std::vector<uint2>> build_beam_boxes(const uint32_t *lo, c
     return out;
 }
 
+// The splat depth of a held view (svo_config.beam_back_held; -1: a new view's)
+int held_back(const svo_ctx *ctx) { return ctx->beam_back_held < 0 ? ctx->beam_back : ctx->beam_back_held; }
+
 int validate_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, size_t n, size_t base, Upload *out) {
     std::string err;
     int depth = 0;
@@ -589,10 +604,13 @@ int validate_upload(svo_ctx *ctx, const uint32_t *lo, const uint32_t *first, siz
     // capacity is legal; the pool is zero-filled at svo_create, so a link into a
     // region not uploaded yet reads empty descriptors
     if (walk_depth(lo, first, n, base, ctx->capacity, &depth, &ext, &tree, &err) != 0) return fail(SVO_ERR_FORMAT, err);
-    *out = Upload{base, n, depth, ext, tree, nullptr, -1};
-    if (base == 0 && tree && !ext && ctx->beam) {   // the common case: the splat list from the host arrays
+    *out = Upload{base, n, depth, ext, tree, nullptr, -1, nullptr, -1};
+    if (base == 0 && tree && !ext && ctx->beam) {   // the common case: the splat lists from the host arrays
+        const int hb = held_back(ctx);
         out->boxes = build_beam_boxes(lo, first, n, depth, ctx->beam_back);
         out->boxes_back = ctx->beam_back;
+        out->boxes_held = hb == ctx->beam_back ? out->boxes : build_beam_boxes(lo, first, n, depth, hb);
+        out->boxes_held_back = hb;
     }
     return SVO_OK;
 }
@@ -616,13 +634,17 @@ uint64_t next_boxes_id() {
 int recompute_pool(svo_ctx *ctx) {
     ctx->depth_exact = false;
     ctx->depth = 22;
-    std::shared_ptr<const std::vector<uint2>> boxes;
+    std::shared_ptr<const std::vector<uint2>> boxes, held;
+    const int hb = held_back(ctx);
     const bool simple = ctx->uploads.size() == 1 && ctx->uploads[0].offset == 0 && !ctx->uploads[0].external &&
                         ctx->uploads[0].tree && ctx->uploads[0].depth <= 22;
     if (simple) {
         ctx->depth_exact = true;
         ctx->depth = ctx->uploads[0].depth;
-        if (ctx->beam && ctx->uploads[0].boxes_back == ctx->beam_back) boxes = ctx->uploads[0].boxes;
+        if (ctx->beam && ctx->uploads[0].boxes_back == ctx->beam_back && ctx->uploads[0].boxes_held_back == hb) {
+            boxes = ctx->uploads[0].boxes;
+            held = ctx->uploads[0].boxes_held;
+        }
     }
     const bool have = boxes || !ctx->beam;
     if ((!simple || !have) && ctx->n_nodes > 0 && ctx->n_nodes < 0xFFFFFFFFull) {
@@ -674,11 +696,18 @@ int recompute_pool(svo_ctx *ctx) {
                 ctx->depth = dep[0];
             }
         }
-        if (ctx->depth_exact && ctx->beam) boxes = build_beam_boxes(lo.data(), first.data(), n, ctx->depth, ctx->beam_back);
+        if (ctx->depth_exact && ctx->beam) {
+            boxes = build_beam_boxes(lo.data(), first.data(), n, ctx->depth, ctx->beam_back);
+            held = hb == ctx->beam_back ? boxes : build_beam_boxes(lo.data(), first.data(), n, ctx->depth, hb);
+        }
     }
     if (boxes != ctx->pool_boxes) {
         ctx->pool_boxes = boxes;
         ctx->pool_boxes_id = boxes ? next_boxes_id() : 0;
+    }
+    if (held != ctx->pool_boxes_held) {
+        ctx->pool_boxes_held = held;
+        ctx->pool_boxes_held_id = !held ? 0 : held == boxes ? ctx->pool_boxes_id : next_boxes_id();
     }
     ctx->pool_boxes_back = ctx->beam_back;
     return SVO_OK;
@@ -1290,7 +1319,6 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // an instrumented launch with the beam: SVO_OPT_COUNT_BEAM's fetch count, or svo_beam_starts
     const bool count_beam = (p.out.fetches && (ctx->options & SVO_OPT_COUNT_BEAM)) || p.out.starts;
     if (ctx->beam && (q || count_beam) && !p.guard && (!instr || count_beam) && ctx->depth_exact && !p.lat) {
-        const std::shared_ptr<const std::vector<uint2>> &boxes = ctx->pool_boxes;
         auto in01 = [](float v) { return v >= 0.0f && v <= 1.0f; };
         bool offs = in01(p.cam.px_off[0]) && in01(p.cam.px_off[1]);
         if (p.samples) {
@@ -1299,33 +1327,42 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
         }
         svo::BeamParams bp;
         std::memset(&bp, 0, sizeof bp);
+        const int tx = (width + 7) / 8, ty = (height + 7) / 8, sx = (width + 63) / 64, sy = (height + 63) / 64;
+        const size_t need = (size_t)tx * ty + (size_t)sx * sy + 1;
+        // the stream's own buffer; an instrumented launch (no scheduling state) the shared scratch
+        unsigned long long *&buf = q ? q->tile_start : ctx->count_ts;
+        size_t &cap = q ? q->ts_cap : ctx->count_ts_cap;
+        uint32_t &gen = q ? q->ts_gen : ctx->count_ts_gen;
+        // A new view splats the moving camera's list; the view's next launch on this stream (a held
+        // view: the reference's accumulating camera, the drop-in's jittered frames) re-splats once with
+        // the finer held list and every later one reuses that.  An instrumented launch (the fetch count
+        // of the walk the render runs, svo_beam_starts) takes the held list.
+        const bool same_view = q && q->ts_view == ctx->view_gen && q->ts_w == width && q->ts_h == height &&
+                               cap >= need && gen != 0;
+        const int li = !q || same_view ? 1 : 0;
+        const std::shared_ptr<const std::vector<uint2>> &boxes = li ? ctx->pool_boxes_held : ctx->pool_boxes;
+        const uint64_t bid = li ? ctx->pool_boxes_held_id : ctx->pool_boxes_id;
+        DevBoxes &db = ctx->dev_boxes[li];
         if (boxes && !boxes->empty() && offs && beam_camera(p.cam, width, height, &bp)) {
-            if (ctx->boxes_id != ctx->pool_boxes_id) {   // the device copy of this pool's splat list
+            if (db.id != bid) {   // the device copy of this splat list
                 const size_t nb = boxes->size();
                 HIP_TRY(hipDeviceSynchronize());   // launches on any stream may still read the old one
-                if (ctx->boxes_cap < nb) {
-                    if (ctx->d_boxes) hipFree(ctx->d_boxes);
-                    ctx->d_boxes = nullptr;
-                    ctx->boxes_cap = 0;
-                    HIP_TRY(hipMalloc(&ctx->d_boxes, nb * sizeof(uint2)));
-                    ctx->boxes_cap = nb;
+                if (db.cap < nb) {
+                    if (db.d) hipFree(db.d);
+                    db.d = nullptr;
+                    db.cap = 0;
+                    HIP_TRY(hipMalloc(&db.d, nb * sizeof(uint2)));
+                    db.cap = nb;
                 }
-                HIP_TRY(hipMemcpy(ctx->d_boxes, boxes->data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
-                ctx->n_boxes = (uint32_t)nb;
-                ctx->boxes_id = ctx->pool_boxes_id;
+                HIP_TRY(hipMemcpy(db.d, boxes->data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
+                db.n = (uint32_t)nb;
+                db.id = bid;
             }
-            const int tx = (width + 7) / 8, ty = (height + 7) / 8, sx = (width + 63) / 64, sy = (height + 63) / 64;
-            const size_t need = (size_t)tx * ty + (size_t)sx * sy + 1;
-            // the stream's own buffer; an instrumented launch (no scheduling state) the shared scratch
-            unsigned long long *&buf = q ? q->tile_start : ctx->count_ts;
-            size_t &cap = q ? q->ts_cap : ctx->count_ts_cap;
-            uint32_t &gen = q ? q->ts_gen : ctx->count_ts_gen;
             if (!q) {
                 rc = order_scratch(ctx, s);
                 if (rc) return rc;
             }
-            const bool reuse = q && q->ts_view == ctx->view_gen && q->ts_boxes == ctx->pool_boxes_id && q->ts_w == width &&
-                               q->ts_h == height && cap >= need && gen != 0;
+            const bool reuse = same_view && q->ts_boxes == bid;
             if (!reuse && (cap < need || gen == 0xFFFFFFFEu)) {   // (re)filled with all-ones keys: generation 0, stale
                 HIP_TRY(hipDeviceSynchronize());   // a pending launch may still read the old buffer
                 if (cap < need) {
@@ -1339,8 +1376,8 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 gen = 0;
             }
             if (!reuse) ++gen;
-            bp.boxes = ctx->d_boxes;
-            bp.n_boxes = ctx->n_boxes;
+            bp.boxes = db.d;
+            bp.n_boxes = db.n;
             bp.tile_start = buf;
             bp.gen = gen;
             bp.diag = ctx->beam_diag;   // timing diagnostics only
@@ -1356,8 +1393,9 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                 hipError_t eb = svo::launch_beam_splat(bp, s);
                 if (eb != hipSuccess) return fail(SVO_ERR_HIP, std::string("beam splat launch: ") + hipGetErrorString(eb));
                 if (q) {
+                    q->held_splat = li == 1;
                     q->ts_view = ctx->view_gen;
-                    q->ts_boxes = ctx->pool_boxes_id;
+                    q->ts_boxes = bid;
                     q->ts_w = width;
                     q->ts_h = height;
                 }
@@ -1402,8 +1440,11 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
                                                || used_kpack != okey.kpack);
         if (relayout) q->relayout_pending = true;
         const bool own_layout = !relayout && q->relayout_pending;
+        // (a held view's finer re-splat shortens its rays: the order is rebuilt from that launch's costs)
         refresh = q->order_key != okey || (n % ctx->order_every == 0 && drift) || q->built_mode != mode_now || own_layout ||
+                  q->held_splat ||
                   (q->built_view != ctx->view_gen && (!moving || n - q->last_build >= (unsigned long long)ctx->move_every));
+        q->held_splat = false;
         if (own_layout) q->relayout_pending = false;
         if (refresh) q->last_build = n;
         moving_build = moving;
@@ -1744,7 +1785,8 @@ int destroy_single(svo_ctx *ctx) {
     for (auto &ev : ctx->timing_free) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     if (ctx->switch_event) hipEventDestroy(ctx->switch_event);
     if (ctx->d_wave_log) hipFree(ctx->d_wave_log);
-    if (ctx->d_boxes) hipFree(ctx->d_boxes);
+    for (DevBoxes &db : ctx->dev_boxes)
+        if (db.d) hipFree(db.d);
     if (ctx->count_ts) hipFree(ctx->count_ts);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1781,6 +1823,7 @@ void config_of(const svo_ctx *c, svo_config *o) {
     k.seg_scramble = c->seg_scramble;
     k.beam = c->beam;
     k.beam_back = c->beam_back;
+    k.beam_back_held = c->beam_back_held;
     k.shadow_form = c->shadow_compact ? 2 : c->fused_shadows ? 0 : 1;
     k.shadow_order = c->shadow_order_enabled;
     k.readback = c->pin_push;
@@ -1815,14 +1858,15 @@ int check_config(const svo_config &k) {
                     : k.beam_back < 0 || k.beam_back > 22 ? "beam_back" : k.shadow_form < 0 || k.shadow_form > 2 ? "shadow_form"
                     : !bit(k.shadow_order) ? "shadow_order" : k.readback < 0 || k.readback > 2 ? "readback"
                     : k.host_copy_threads < 0 || k.host_copy_threads > 16 ? "host_copy_threads"
-                    : !bit(k.sparse_payload) ? "sparse_payload" : !bit(k.peer_copy) ? "peer_copy" : nullptr;
+                    : !bit(k.sparse_payload) ? "sparse_payload" : !bit(k.peer_copy) ? "peer_copy"
+                    : k.beam_back_held < -1 || k.beam_back_held > 22 ? "beam_back_held" : nullptr;
     if (bad) return fail(SVO_ERR_ARG, std::string("svo_config.") + bad + " out of range");
     return SVO_OK;
 }
 
 // One device's context takes a validated config.  Nothing here changes a result; what holds state
 // built under the old value is rebuilt: the pinned readback slots (their allocation flags follow
-// `readback`), the host copy threads, the pool's splat list (beam, beam_back); and every stream's
+// `readback`), the host copy threads, the pool's splat lists (beam, beam_back, beam_back_held); and every stream's
 // loop-form / class-table decision is dropped, so the next order build decides under the new rule.
 int apply_config(svo_ctx *c, const svo_config &k) {
     c->tile_order = k.tile_order;
@@ -1866,9 +1910,10 @@ int apply_config(svo_ctx *c, const svo_config &k) {
         c->copy_pool.reset();   // idle between calls (svo_render waits for it)
         c->host_copy_threads = k.host_copy_threads;
     }
-    const bool boxes = c->beam != k.beam || c->beam_back != k.beam_back;
+    const bool boxes = c->beam != k.beam || c->beam_back != k.beam_back || c->beam_back_held != k.beam_back_held;
     c->beam = k.beam;
     c->beam_back = k.beam_back;
+    c->beam_back_held = k.beam_back_held;
     if (boxes && c->n_nodes > 0) {
         const int rc = recompute_pool(c);
         if (rc) return rc;

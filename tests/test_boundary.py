@@ -161,11 +161,12 @@ CONFIG_DEFAULTS = {
     "relayout": 1, "fetch_all": -1, "loop_form": -1, "lat_ratio": 0.3, "segments": 1, "seg_table_latency": 0x444,
     "seg_table_issue": 0x4, "seg_table_thin": 0x888, "seg_ratio": 0.28, "seg_thin_ratio": 0.083, "seg_cap": 96,
     "seg_min_chain": 160, "seg_move": 2, "seg_jitter": 2, "seg_all": 0, "seg_scramble": 0, "beam": 1, "beam_back": 2,
-    "shadow_form": 0, "shadow_order": 1, "readback": 0, "host_copy_threads": 0, "sparse_payload": 0, "peer_copy": 0}
+    "shadow_form": 0, "shadow_order": 1, "readback": 0, "host_copy_threads": 0, "sparse_payload": 0, "peer_copy": 0,
+    "beam_back_held": 0}
 
 
 def test_config_struct_size_version_and_layout(tmp_path):
-    """svo_config (ABI 10): the ctypes mirror has the header's size, version and every field at the
+    """svo_config (ABI 10, config version 2): the ctypes mirror has the header's size, version and every field at the
     header's offset (the C# shim's StructLayout(Sequential) follows the same order)."""
     from raytracingtest_amd import _lib
     fields = [n for n, _ in _lib.CONFIG_FIELDS]
@@ -178,8 +179,8 @@ def test_config_struct_size_version_and_layout(tmp_path):
     subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o",
                     str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
-    assert int(out[0]) == ctypes.sizeof(_lib.SvoConfig) == 128
-    assert int(out[1]) == _lib.CONFIG_VERSION == 1
+    assert int(out[0]) == ctypes.sizeof(_lib.SvoConfig) == 132
+    assert int(out[1]) == _lib.CONFIG_VERSION == 2
     for f, off in zip(fields, out[2:]):
         assert int(off) == getattr(_lib.SvoConfig, f).offset, f
     # every field is documented in INTEGRATION.md's config table and declared in the header
@@ -204,13 +205,18 @@ def test_config_defaults_and_size_versioning_without_gpu(native):
     assert native.svo_get_config(None, ctypes.byref(c)) == -1
     assert native.svo_set_config(None, ctypes.byref(c)) == -1
     # an older caller's struct: only the first 16 bytes (size, version, tile_order, xcd_strips)
-    buf = (ctypes.c_uint8 * 128)(*([0xEE] * 128))
+    buf = (ctypes.c_uint8 * 132)(*([0xEE] * 132))
     hdr = ctypes.cast(buf, ctypes.POINTER(_lib.SvoConfig))
     hdr.contents.size = 16
     assert native.svo_get_config(None, hdr) == 0
-    assert hdr.contents.size == 16 and hdr.contents.version == 1
+    assert hdr.contents.size == 16 and hdr.contents.version == 2
     assert hdr.contents.tile_order == 1 and hdr.contents.xcd_strips == 1
     assert all(b == 0xEE for b in bytes(buf)[16:]), "wrote past the caller's size"
+    # a version-1 caller (128 bytes, before beam_back_held): filled up to its size, the rest untouched
+    hdr.contents.size = 128
+    assert native.svo_get_config(None, hdr) == 0
+    assert hdr.contents.size == 128 and hdr.contents.peer_copy == 0
+    assert all(b == 0xEE for b in bytes(buf)[128:])
 
 
 def test_library_reads_no_policy_from_the_environment():

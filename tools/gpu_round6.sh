@@ -111,9 +111,9 @@ splatab)
             python3 tools/dropin_loop.py --poses flyover --frames 200 > "$out/sp_prof_$n.txt" 2>&1 || exit $?
     done ;;
 backab)
-    # splat depth (svo_config.beam_back 2 = default, 3, 4): held / jittered / pan frames
+    # splat depth (svo_config.beam_back 2 = default, 3, 4; BACKS overrides): held / jittered / pan frames
     for rep in a b; do
-        for v in 2 3 4; do
+        for v in ${BACKS:-2 3 4}; do
             timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main --set beam_back=$v > "$out/bb_$v$rep.txt" 2>&1 || exit $?
         done
     done ;;
@@ -123,6 +123,23 @@ progtrace)
     cd /tmp && export TMPDIR=/tmp && cd - > /dev/null &&
     timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace -f csv -d "$out/pt" -o pt -- \
         python3 tools/progressive_trace.py > "$out/pt_prof.txt" 2>&1 ;;
+heldab)
+    # a held view's finer re-splat (beam_back_held 0, the default) against none (-1): parity of the
+    # beam / segment / decision suites first, then the drop-in loops and the bench line, interleaved
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_beam.py tests/test_gpu_seg.py -x -v --timeout 200 \
+        --timeout-method thread > "$out/held_tests.txt" 2>&1 &&
+    timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread \
+        -k "class_table or loop_form or switches" > "$out/held_tests2.txt" 2>&1 || exit $?
+    for rep in a b; do
+        for v in 0 -1; do
+            timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main --set beam_back_held=$v \
+                > "$out/hd_$v$rep.txt" 2>&1 || exit $?
+            timeout -k 10 150 python -u bench.py --no-extras --cpu-seconds 0 --set beam_back_held=$v \
+                > "$out/hb_fly_$v$rep.json" 2> "$out/hb_$v$rep.err" || exit $?
+            timeout -k 10 150 python -u bench.py --no-extras --cpu-seconds 0 --camera main --set beam_back_held=$v \
+                > "$out/hb_main_$v$rep.json" 2>> "$out/hb_$v$rep.err" || exit $?
+        done
+    done ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&

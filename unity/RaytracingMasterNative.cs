@@ -56,6 +56,7 @@ public static class SvoNative {
         public int segCap, segMinChain, segMove, segJitter, segAll;
         public uint segScramble;
         public int beam, beamBack, shadowForm, shadowOrder, readback, hostCopyThreads, sparsePayload, peerCopy;
+        public int beamBackHeld;   // config version 2
     }
     [DllImport(Lib)] public static extern int svo_get_config(IntPtr ctx, ref SvoConfig cfg);
     [DllImport(Lib)] public static extern int svo_set_config(IntPtr ctx, ref SvoConfig cfg);
@@ -104,7 +105,8 @@ public class RaytracingMasterNative : MonoBehaviour {
     // library's (svo_get_config(NULL)).  None changes the image -- only where the time goes.
     [Header("Render policy (svo_config)")]
     public bool beamStarts = true;               // beam: rays start at their tile's lower bound of the hit t
-    [Range(0, 8)] public int beamBack = 2;       // splat boxes this many levels above the leaves
+    [Range(0, 8)] public int beamBack = 2;       // a new view's splat: boxes this many levels above the leaves
+    [Range(-1, 8)] public int beamBackHeld = 0;  // a held view's finer re-splat (-1: beamBack)
     public bool segmentedRays = true;            // segments: heavy tiles traced as exact t-segments
     public bool costOrderedDispatch = true;      // tile_order: heaviest tiles dispatched first
     [Range(1, 32)] public int moveEvery = 4;     // while the camera moves, rebuild the order every k-th frame
@@ -157,6 +159,7 @@ public class RaytracingMasterNative : MonoBehaviour {
         SvoNative.Check(SvoNative.svo_get_config(_ctx, ref cfg), "svo_get_config");
         cfg.beam = beamStarts ? 1 : 0;
         cfg.beamBack = beamBack;
+        cfg.beamBackHeld = beamBackHeld;
         cfg.segments = segmentedRays ? 1 : 0;
         cfg.tileOrder = costOrderedDispatch ? 1 : 0;
         cfg.moveEvery = moveEvery;
