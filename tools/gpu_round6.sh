@@ -140,6 +140,18 @@ heldab)
                 > "$out/hb_main_$v$rep.json" 2>> "$out/hb_$v$rep.err" || exit $?
         done
     done ;;
+tableab)
+    # the class tables under the held view's fine starts (bench line, flyover and Main.unity pose)
+    one() { local name=$1; shift
+            timeout -k 10 150 python -u bench.py --no-extras --cpu-seconds 0 "$@" > "$out/tb_$name.json" 2>> "$out/tb.err"; }
+    for rep in a b; do
+        for v in ${TABLES:-"default:" "noseg:--set segments=0" "iss44:--set seg_table_issue=0x44" "iss8:--set seg_table_issue=0x8" "cap192:--set seg_cap=192"}; do
+            n=${v%%:*}; a=${v#*:}; a=${a//+/ }   # '+' stands for a space inside one TABLES entry
+            for pose in ${POSES:-flyover main}; do
+                one ${pose:0:4}_$n$rep --camera $pose $a || exit $?
+            done
+        done
+    done ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
