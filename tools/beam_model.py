@@ -37,19 +37,22 @@ def bind(L):
     return L
 
 
-def boxes_at(nodes, depth):
+def boxes_at(nodes, depth, leaves=False):
     """Lower corners (SVO space) of the non-leaf nodes at `depth` (svo_rt.hip build_beam_boxes; this
-    pool has its leaves at the deepest level only)."""
+    pool has its leaves at the deepest level only); leaves=True: every valid child at the last level
+    (the voxels themselves when depth is the pool's, beam_back 0)."""
     lo = (nodes & np.uint64(0xFFFFFFFF)).astype(np.uint32)
     first = (nodes >> np.uint64(32)).astype(np.uint32)
     pc = np.array([bin(v).count("1") for v in range(256)])
     cur, pos, size = np.array([0]), np.zeros((1, 3)), 1.0
-    for _ in range(depth):
+    for d in range(depth):
         m, v = lo[cur] & 0xFF, (lo[cur] >> 8) & 0xFF
         nxt, npos = [], []
         half = size / 2
         for c in range(8):   # bit c of the masks: upper half on axis k iff bit k of c
             inner = ((m >> c) & 1).astype(bool) & ((v >> c) & 1).astype(bool)
+            if leaves and d == depth - 1:   # the last level: every valid child, leaf or not
+                inner = ((v >> c) & 1).astype(bool)
             ptr = first[cur].astype(np.int64) + pc[m & ((1 << c) - 1)]
             nxt.append(ptr[inner])
             npos.append(pos[inner] + np.array([c & 1, (c >> 1) & 1, (c >> 2) & 1]) * half)
@@ -57,8 +60,9 @@ def boxes_at(nodes, depth):
     return pos + 1.0, size
 
 
-def splat(cam, P, size, W, H):
-    """The kernel's per-tile bounds (tile, 64x64 super tile, global), as a per-pixel image."""
+def splat(cam, P, size, W, H, cell=8):
+    """The kernel's per-tile bounds (tile, 64x64 super tile, global), as a per-pixel image; `cell`:
+    the finest cell's size in pixels (the kernel's 8; smaller: what finer cells would give)."""
     c2w = np.array(cam.c2w[:], f32)
     ip = np.array(cam.inv_proj[:], f32)
     A, B, C = (np.array([sum(float(c2w[k * 4 + r]) * float(ip[col * 4 + k]) for k in range(3)) for r in range(3)])
@@ -110,16 +114,17 @@ def splat(cam, P, size, W, H):
                 y0, y1 = np.where(cross, np.minimum(y0, fy), y0), np.where(cross, np.maximum(y1, fy), y1)
     x0, y0, x1, y1 = x0 - 0.05, y0 - 0.05, x1 + 0.05, y1 + 0.05
     keep &= (x1 >= 0) & (y1 >= 0) & (x0 <= W) & (y0 <= H)
-    tx_, ty_, sx_, sy_ = (W + 7) // 8, (H + 7) // 8, (W + 63) // 64, (H + 63) // 64
+    tx_, ty_, sx_, sy_ = (W + cell - 1) // cell, (H + cell - 1) // cell, (W + 63) // 64, (H + 63) // 64
+    per = 64 // cell   # cells per super tile side
     tiles, sup, gl = np.full(tx_ * ty_, np.inf, f32), np.full(sx_ * sy_, np.inf, f32), np.inf
     if glob.any():
         gl = min(gl, float(dist[glob].min()))
     k = keep & ~glob
     with np.errstate(all="ignore"):
-        tx0 = (np.maximum(x0, 0) * 0.125).astype(np.int64)
-        ty0 = (np.maximum(y0, 0) * 0.125).astype(np.int64)
-        tx1 = np.minimum((np.minimum(x1, W) * 0.125).astype(np.int64), tx_ - 1)
-        ty1 = np.minimum((np.minimum(y1, H) * 0.125).astype(np.int64), ty_ - 1)
+        tx0 = (np.maximum(x0, 0) / cell).astype(np.int64)
+        ty0 = (np.maximum(y0, 0) / cell).astype(np.int64)
+        tx1 = np.minimum((np.minimum(x1, W) / cell).astype(np.int64), tx_ - 1)
+        ty1 = np.minimum((np.minimum(y1, H) / cell).astype(np.int64), ty_ - 1)
     nt = (tx1 - tx0 + 1) * (ty1 - ty0 + 1)
     for i in np.flatnonzero(k & (nt <= 32)):
         for ty in range(ty0[i], ty1[i] + 1):
@@ -128,7 +133,7 @@ def splat(cam, P, size, W, H):
     stats = {"boxes_in_view": int(keep.sum()), "tile_writes": int(nt[k & (nt <= 32)].sum()), "super": 0,
              "global": int(glob.sum())}
     for i in np.flatnonzero(k & (nt > 32)):
-        sx0, sx1, sy0, sy1 = tx0[i] >> 3, tx1[i] >> 3, ty0[i] >> 3, ty1[i] >> 3
+        sx0, sx1, sy0, sy1 = tx0[i] // per, tx1[i] // per, ty0[i] // per, ty1[i] // per
         if (sx1 - sx0 + 1) * (sy1 - sy0 + 1) <= 32:
             stats["super"] += 1
             for sy in range(sy0, sy1 + 1):
@@ -138,7 +143,7 @@ def splat(cam, P, size, W, H):
             stats["global"] += 1
             gl = min(gl, float(dist[i]))
     ys, xs = np.mgrid[0:H, 0:W]
-    img = np.minimum(np.minimum(tiles[(ys >> 3) * tx_ + (xs >> 3)], sup[(ys >> 6) * sx_ + (xs >> 6)]), f32(gl))
+    img = np.minimum(np.minimum(tiles[(ys // cell) * tx_ + (xs // cell)], sup[(ys >> 6) * sx_ + (xs >> 6)]), f32(gl))
     return img.astype(f32), stats
 
 
@@ -166,13 +171,16 @@ def main():
     ap.add_argument("--cameras", default="flyover,main")
     ap.add_argument("--cuts", default="13,15,17", help="cone model: terminal scales (13 = the leaves of C3)")
     ap.add_argument("--splat-depth", type=int, default=8)
+    ap.add_argument("--leaves", action="store_true", help="the splat's last level takes every valid child (voxels)")
+    ap.add_argument("--cells", default="8", help="comma list of finest-cell sizes in pixels (the kernel: 8)")
+    ap.add_argument("--offsets", default="0.5,0,1", help="pixel offsets checked (the first also traced)")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     a = ap.parse_args()
     W, H = 1920, 1080
     z = np.load(a.npz)
     svo = orc.OracleSVO(nodes=z["nodes"], attachments=z["attachments"])
     L = bind(sm.lib())
-    P, size = boxes_at(z["nodes"].astype(np.uint64), a.splat_depth)
+    P, size = boxes_at(z["nodes"].astype(np.uint64), a.splat_depth, a.leaves)
     print(f"C3 pool {len(z['nodes'])} nodes; splat depth {a.splat_depth}: {len(P)} boxes", flush=True)
     for name in a.cameras.split(","):
         c2w, ipm = (sm.pan_camera(1) if name == "flyover" else CAMERAS[name]()).uniforms(W, H)
@@ -189,7 +197,7 @@ def main():
                     f"({bb.sum() / cont.sum():.3f}); wave trips {int(cont.max(1).sum())} -> {int(bb.max(1).sum())} "
                     f"({bb.max(1).sum() / cont.max(1).sum():.3f}); heaviest wave {int(cont.max())} -> {int(bb.max())}")
 
-        for cut in (int(c) for c in a.cuts.split(",")):
+        for cut in (int(c) for c in a.cuts.split(",") if c):
             ty, tx = H // 8, W // 8
             tb, pops = np.zeros(ty * tx, f32), np.zeros(ty * tx, np.uint32)
             L.segm_beam(ctypes.byref(svo.s), ctypes.byref(cam), W, H, 8, cut, a.threads, tb.ctypes.data,
@@ -199,16 +207,17 @@ def main():
             start = np.ascontiguousarray(np.where(np.isfinite(img), img * f32(1 - 2 ** -14), img).reshape(-1))
             print(f"{name} cone, terminal scale {cut}: search pops/tile mean {pops.mean():.1f} max {pops.max()}; "
                   + run(start), flush=True)
-        for off in ((0.5, 0.5), (0.0, 0.0), (1.0, 1.0)):
+        offs = [(float(o), float(o)) for o in a.offsets.split(",")]
+        for cell, off in ((int(c), o) for c in a.cells.split(",") for o in offs):
             cam = orc.make_camera(c2w, ipm, off, main_light())
-            img, st = splat(cam, P, size, W, H)
+            img, st = splat(cam, P, size, W, H, cell)
             hits, _, _ = orc.render(svo, cam, W, H, orc.STACK_HLSL, want_rgba=False, want_fetches=False)
             start, zero = kernel_start(cam, img, W, H, off)
             th = (hits["t"] / f32(2048)).reshape(H, W)
             hit = ((hits["flags"] & 1).reshape(H, W) != 0) & ~zero
             bad = int(np.count_nonzero(hit & (start.reshape(H, W) > th)))
-            print(f"{name} splat, offset {off}: {st}; hit rays {int(hit.sum())}, start > oracle t for {bad}"
-                  + ("; " + run(start) if off == (0.5, 0.5) else ""), flush=True)
+            print(f"{name} splat, cell {cell}, offset {off}: {st}; hit rays {int(hit.sum())}, start > oracle t for {bad}"
+                  + ("; " + run(start) if off == offs[0] else ""), flush=True)
 
 
 if __name__ == "__main__":
