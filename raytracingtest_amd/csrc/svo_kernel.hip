@@ -1399,7 +1399,7 @@ void render_samples_kernel(LaunchParams p, int tiles_x) {
 }
 
 // ------------------------------------------------------------- shadow pass
-// Two-pass form (env SVO_FUSED_SHADOWS=0): one shadow ray per primary hit, read
+// Two-pass form (svo_config.shadow_form 1): one shadow ray per primary hit, read
 // back from the primary pass's records (svo_hit or compact); an occluded pixel
 // gets flag bit 3 and a black Result (R:109-111) in every output.  Same 8x8
 // tiles as the primary pass, cost-ordered by its own recorded trip counts.
@@ -1469,7 +1469,7 @@ __global__ __launch_bounds__(TILE) void shadow_tile_kernel(LaunchParams p, int t
     }
 }
 
-// Compacted form (env SVO_SHADOW_COMPACT=1): the primary pass's
+// Compacted form (svo_config.shadow_form 2): the primary pass's
 // hit masks are scanned and its hit pixels packed into a dense list in tile order
 // (pack_hits_kernel<INDEX>, the sparse payload's ballot + prefix sum), and one wave
 // traces 64 consecutive list entries.  The grid covers every pixel; waves past the
@@ -1975,7 +1975,7 @@ hipError_t launch_accumulate(float4 *dst, const float4 *src, size_t n_px, uint32
     return hipGetLastError();
 }
 
-// svo_render_progressive_async (env SVO_PIN_PUSH=1): the packed display words pushed into the
+// svo_render_progressive_async (svo_config.readback 1): the packed display words pushed into the
 // plugin's mapped pinned host buffer by a kernel (PCIe writes from every workgroup) instead of
 // one DMA copy; 16 B per lane, grid-stride, non-temporal stores.
 __global__ __launch_bounds__(256) void push_host_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,

@@ -164,7 +164,7 @@ struct Sched {
     bool relayout_pending = false;       // a launch ran in an order of another class layout (see launch)
     int lat_cache = 0;                   // the decision of the last completed build ...
     bool lat_short = false;              // ... and whether its heaviest tile's chain was short
-    bool lat_thin = false;               // ... and whether its work was thin against that chain (SVO_SEG_THIN)
+    bool lat_thin = false;               // ... and whether its work was thin against that chain (svo_config.seg_table_thin)
     Geo lat_key;                         // ... made at this geometry / view / mode (width -1: none)
     unsigned long long lat_view = 0;
     int lat_mode = -1;
@@ -307,7 +307,7 @@ struct svo_ctx {
     unsigned long long pin_frames = 0;   // frames enqueued since the slots were (re)allocated
     int num_cus = 256;
     size_t lds_per_block = 160 * 1024;   // hipDeviceProp.sharedMemPerBlock
-    int xcd_remap = 2;               // env SVO_XCD_REMAP: 2 interleaved column strips (default), 0 raster
+    int xcd_remap = 2;               // svo_config.xcd_strips: 2 interleaved column strips (default), 0 raster
     uint32_t options = 0;            // svo_set_options
     // SVO_OPT_KERNEL_TIMING: event pairs around the primary kernel / the assemble kernel
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timing_events[N_STAGES];   // recorded, not yet read
@@ -315,25 +315,25 @@ struct svo_ctx {
     uint32_t *d_wave_log = nullptr;  // diagnostics: env SVO_WAVE_LOG=<file>
     size_t wave_log_cap = 0;
     // cost-ordered tile dispatch (svo_rt.hip Sched): switches and per-stream state
-    int tile_order = 1;              // env SVO_TILE_ORDER=0 disables
-    int prio = 1;                    // env SVO_PRIO=0: no issue priority by cost class
-    int shadow_order_enabled = 1;    // env SVO_SHADOW_ORDER=0: shadow tiles in plain strip order
-    int fetch_all = -1;              // env SVO_FETCH_ALL=0|1 (default: by pool size, see launch)
-    int fused_shadows = 1;           // env SVO_FUSED_SHADOWS=0: shadow rays as a second launch
-    int shadow_compact = 0;          // env SVO_SHADOW_COMPACT=1: that launch over the compacted hit list
-    int lat_mode = -1;               // env SVO_LAT: 0 never, 1 always, unset: by the last launch's costs (see launch)
-    int seg_mode = 1;                // env SVO_SEG=0: never trace heavy tiles as segmented rays (see launch)
-    int seg_kpack_lat = 0x444;       // env SVO_SEG_LAT=<hex>: the K of each cost class (nibble c: class c, >= 7/8,
+    int tile_order = 1;              // svo_config.tile_order (0: strip order)
+    int prio = 1;                    // svo_config.issue_priority 0: no issue priority by cost class
+    int shadow_order_enabled = 1;    // svo_config.shadow_order 0: shadow tiles in plain strip order
+    int fetch_all = -1;              // svo_config.fetch_all 0|1 (default: by pool size, see launch)
+    int fused_shadows = 1;           // svo_config.shadow_form 1: shadow rays as a second launch
+    int shadow_compact = 0;          // svo_config.shadow_form 2: that launch over the compacted hit list
+    int lat_mode = -1;               // svo_config.loop_form: 0 never, 1 always, unset: by the last launch's costs (see launch)
+    int seg_mode = 1;                // svo_config.segments 0: never trace heavy tiles as segmented rays (see launch)
+    int seg_kpack_lat = 0x444;       // svo_config.seg_table_latency: the K of each cost class (nibble c: class c, >= 7/8,
                                      // 3/4, 1/2, 1/4, 1/8 of the max, rest; 0 none, 4 or 8) in a latency-bound launch
-    int seg_kpack_issue = 0x4;       // env SVO_SEG_ISSUE=<hex>: the same in an issue-bound launch
-    int seg_kpack_thin = 0x888;      // env SVO_SEG_THIN=<hex>: ... and in a latency-bound launch whose summed trips
-    float thin_ratio = 0.083f;       // are below SVO_SEG_THIN_RATIO x slots x its heaviest tile's: C3 8-way bands
+    int seg_kpack_issue = 0x4;       // svo_config.seg_table_issue: the same in an issue-bound launch
+    int seg_kpack_thin = 0x888;      // svo_config.seg_table_thin: ... and in a latency-bound launch whose summed trips
+    float thin_ratio = 0.083f;       // are below svo_config.seg_thin_ratio x slots x its heaviest tile's: C3 8-way bands
                                      // (flyover 0.045, Main.unity 0.079) and the overview frame (0.063) run faster
                                      // with every heavy class in eighths, the flyover 4-way band (0.087) with 444
                                      // (profiles/r05_thin_ab.json)
-    int seg_cap = 96;                // env SVO_SEG_CAP: at most this many segmented tiles per XCD
-    int seg_all = 0;                 // env SVO_SEG_ALL=4|8 (tests; 1 = 4): every tile segmented with that K
-    uint32_t seg_scramble = 0;       // env SVO_SEG_SCRAMBLE=<seed> (tests): arbitrary segment starts
+    int seg_cap = 96;                // svo_config.seg_cap: at most this many segmented tiles per XCD
+    int seg_all = 0;                 // svo_config.seg_all 4|8 (tests): every tile segmented with that K
+    uint32_t seg_scramble = 0;       // svo_config.seg_scramble (tests): arbitrary segment starts
     uint32_t seg_launches = 0;
     int beam = 1;                    // svo_config.beam: beam starts
     int beam_back = 2;               // svo_config.beam_back: a new view's splat, this many levels above the leaves
@@ -349,17 +349,17 @@ struct svo_ctx {
     // record end early; trace_seg): C3 one-sample route 94.6 against 97.9 us (overview 84.3 / 88.8),
     // a slow pan 91.2 / 93.0 us (profiles/r05_stale_starts.txt).  1: the stored starts, 0 (jittered
     // launches only): no segments
-    int seg_move = 2;                // env SVO_SEG_MOVE: a launch at a new view
-    int seg_jitter = 2;              // env SVO_SEG_JITTER: a jittered launch (the one-sample samples route)
-    int spread = 1;                  // env SVO_SPREAD=0: a moving camera's order classes tiles by their own costs only
+    int seg_move = 2;                // svo_config.seg_move: a launch at a new view
+    int seg_jitter = 2;              // svo_config.seg_jitter: a jittered launch (the one-sample samples route)
+    int spread = 1;                  // svo_config.move_spread 0: a moving camera's order classes tiles by their own costs only
     int relayout = 1;                // svo_config.relayout 0: keep an order built from costs of another class layout
-    int seg_min_chain = 160;         // env SVO_SEG_MIN_CHAIN: a latency-bound launch whose heaviest tile costs fewer
+    int seg_min_chain = 160;         // svo_config.seg_min_chain: a latency-bound launch whose heaviest tile costs fewer
                                      // trips takes the latency form, unsegmented, without beam starts
     float seg_ratio = 0.28f;         // svo_config.seg_ratio: ... and the same with beam starts (class table only)
-    int move_every = 4;              // env SVO_MOVE_EVERY: while the camera moves every launch, rebuild the
+    int move_every = 4;              // svo_config.move_every: while the camera moves every launch, rebuild the
                                      // order only every k-th launch (see launch; 1 = at every new view).
                                      // C3 pan: 118.8 us per frame at 1, 110.7 at 4, 111.9 at 8
-    int order_every = 32;            // env SVO_ORDER_EVERY: rebuild the order every k-th launch (and after
+    int order_every = 32;            // svo_config.order_every: rebuild the order every k-th launch (and after
                                      // every camera move or change of render mode)
     unsigned long long view_gen = 0; // bumped when svo_set_camera changes the matrices
     unsigned long long cost_gen = 0; // bumped by whatever else changes the tiles' costs: a new pixel
@@ -1173,7 +1173,7 @@ int launch(svo_ctx *ctx, int width, int height, int stack_mode, const svo_band *
     // tile costs include its shadow trips.  The wait can block the host for up to a frame,
     // once per new view (svo_rt.h, svo_render_device).
     // The same statistics decide whether the heaviest tiles are traced as segmented rays
-    // (SVO_SEG unset: exactly when the launch is latency-bound, i.e. its heaviest chain and not
+    // (segments on: exactly when the launch is latency-bound, i.e. its heaviest chain and not
     // its issued work bounds it -- a strong split's band).
     const int mode_now = p.shadows | (stack_mode << 2);
     // whether this launch's primary rays get beam starts (the test of the beam block below, less the

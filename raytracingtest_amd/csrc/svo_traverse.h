@@ -92,7 +92,7 @@ struct LaunchParams {
     // and records its wave trip count in tile_cost.
     const uint32_t *tile_order;   // n_tiles entries + 36 class boundaries
     uint16_t *tile_cost;
-    int prio;                     // s_setprio by cost class (env SVO_PRIO)
+    int prio;                     // s_setprio by cost class (svo_config.issue_priority)
     int guard;                    // lean loop: stack-overflow test and HLSL parent round trip needed
     int fetch_all;                // lean loop (!guard): every lane loads its node every trip
     int lat;                      // latency form of the loop (trace_lat; !guard, primary rays only)
@@ -120,7 +120,7 @@ struct LaunchParams {
     int seg, seg_kmax;
     float4 *seg_hint;
     uint16_t *part_cost;
-    uint32_t seg_scramble;     // tests (env SVO_SEG_SCRAMBLE): != 0 replaces every start by a hash of
+    uint32_t seg_scramble;     // tests (svo_config.seg_scramble): != 0 replaces every start by a hash of
                                // (pixel, this value) -- unordered, NaN, +-inf, outside the cube
     // Beam starts (null: none).  tile_start[ty * ts_tiles_x + tx] for the 8x8 tile
     // (tx, ty) of the FULL frame (global rows), tile_start[ts_super_off + sy * ts_super_x + sx] for

@@ -100,11 +100,12 @@ splatab)
     # splat kernel's own time (rocprofv3 kernel trace of the same loop)
     cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
     for rep in a b; do
-        for v in 512:raytracingtest_amd 256:build/ab/splat256 128:build/ab/splat128; do
+        for v in ${SPLATS:-512:raytracingtest_amd 256:build/ab/splat256 128:build/ab/splat128}; do
             n=${v%%:*}; l=$PWD/${v#*:}/libsvo_rt.so
             SVO_RT_LIB=$l timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main > "$out/sp_$n$rep.txt" 2>&1 || exit $?
         done
     done
+    [ -n "$SPLATS" ] && exit 0
     for v in 512:raytracingtest_amd 256:build/ab/splat256 128:build/ab/splat128; do
         n=${v%%:*}; l=$PWD/${v#*:}/libsvo_rt.so
         SVO_RT_LIB=$l timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d "$out/sp_prof_$n" -o sp -- \
