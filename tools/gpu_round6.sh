@@ -153,6 +153,14 @@ tableab)
             done
         done
     done ;;
+splatcost)
+    # the splat kernel's own time per list depth (beam_back 2 / 1 / 0 for the moving camera) over the
+    # pan loop, from a kernel trace
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+    for v in 2 1 0; do
+        timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d "$out/sc_$v" -o sc -- \
+            python3 tools/progressive_trace.py --frames 100 --set beam_back=$v > "$out/sc_$v.txt" 2>&1 || exit $?
+    done ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
