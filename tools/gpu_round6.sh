@@ -161,6 +161,13 @@ splatcost)
         timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d "$out/sc_$v" -o sc -- \
             python3 tools/progressive_trace.py --frames 100 --set beam_back=$v > "$out/sc_$v.txt" 2>&1 || exit $?
     done ;;
+jitab)
+    # the jittered launch's segment starts under the held view's fine splat (seg_jitter 2 default / 1 / 0)
+    for rep in a b; do
+        for v in 2 1 0; do
+            timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main --set seg_jitter=$v > "$out/jt_$v$rep.txt" 2>&1 || exit $?
+        done
+    done ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
