@@ -322,3 +322,43 @@ def test_beam_bound_random_camera_sweep(torch, oracle_mod, c3_svo):
             json.dump(summary, fh, indent=1)
     print(f"beam sweep: {summary['beam_rays']} beam-started hit rays over {summary['cameras']} cameras, "
           f"min slack {summary['min_slack_margins']:.3f} margins ({summary['min_slack_rel']:.3e} relative)")
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_held_view_resplat_is_finer_and_exact(torch, oracle_mod, c3_svo, mode):
+    """A held view re-splats once with its finer list (svo_config.beam_back_held):
+    the first launch at a view starts from the moving camera's depth-8 boxes, the next ones from
+    every voxel's box.  Every frame of the sequence equals the oracle's, and the walk the render runs
+    (SVO_OPT_COUNT_BEAM: the held list) fetches fewer descriptors than with the held list off (-1),
+    every start staying at or below its ray's hit t."""
+    w, h = 480, 270
+    cams = [CAMERAS["flyover"](), CAMERAS["main"]()]
+    fetches = {}
+    for held in (0, -1):
+        m = RaytracingMaster(device=0, capacity_nodes=len(c3_svo), config={"beam_back_held": held})
+        try:
+            m.SetSVOBuffer(c3_svo)
+            assert m.get_config()["beam_back_held"] == held
+            total = 0
+            for cam in cams:
+                m.UpdateShaderParameters(cam, w, h)
+                ref_hits, ref_rgba, _, _ = _oracle(oracle_mod, c3_svo, cam, w, h, mode)
+                for _ in range(3):   # a new view (coarse), then held (the fine re-splat, then reuse)
+                    b = _render(torch, m, w, h, mode, keys=("hits", "rgba"))
+                    _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
+                m.set_count_beam(True)
+                f = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+                m.count_fetches_device(w, h, f.data_ptr(), stack_mode=mode)
+                m.set_count_beam(False)
+                starts = torch.empty(w * h, dtype=torch.float32, device="cuda")
+                m.beam_starts_device(w, h, starts.data_ptr())
+                m.synchronize()
+                total += int(f.sum().item())
+                hit = (ref_hits["flags"] & 1) != 0
+                t = ref_hits["t"].astype(np.float64) / 2048.0   # bestHit.distance = 2048 t_min, exact
+                s = starts.cpu().numpy().astype(np.float64)
+                assert not np.any(hit & np.isfinite(s) & (s > t)), "a start past its ray's hit"
+            fetches[held] = total
+        finally:
+            m.close()
+    assert fetches[0] < fetches[-1], fetches
