@@ -168,6 +168,20 @@ jitab)
             timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main --set seg_jitter=$v > "$out/jt_$v$rep.txt" 2>&1 || exit $?
         done
     done ;;
+longab)
+    # the long splat list's boxes per thread (SVO_SPLAT_LONG_PER 4 = this tree, 1, 8) on the pan with the
+    # moving list at one and zero levels back, and the beam suite on this tree first
+    timeout -k 10 400 python -u -m pytest tests/test_gpu_beam.py -x -q --timeout 200 --timeout-method thread \
+        > "$out/beam_tests.txt" 2>&1 || exit $?
+    for rep in a b; do
+        for v in 4:raytracingtest_amd 1:build/ab/long1 8:build/ab/long8; do
+            n=${v%%:*}; l=$PWD/${v#*:}/libsvo_rt.so
+            for bb in 1 0; do
+                SVO_RT_LIB=$l timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main --set beam_back=$bb \
+                    > "$out/lp_${n}_bb$bb$rep.txt" 2>&1 || exit $?
+            done
+        done
+    done ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
