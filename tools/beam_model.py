@@ -78,17 +78,18 @@ def splat(cam, P, size, W, H, cell=8):
         planes.append((n / np.linalg.norm(n)).astype(f32))
     org = (c2w[12:15] * f32(1 / 32) + f32(1.5)).astype(f32)
     lo = P.astype(f32)
-    sz = f32(size)
+    sz = np.broadcast_to(np.asarray(size, f32), (len(P),)).astype(f32)   # per box (a mixed list) or one
     rel = lo - org
-    m = np.maximum(np.maximum(rel, -(rel + sz)), 0)
+    m = np.maximum(np.maximum(rel, -(rel + sz[:, None])), 0)
     dist = np.sqrt((m * m).sum(1)).astype(f32)
     span = np.abs(rel).sum(1) + 3 * sz
     keep = np.ones(len(P), bool)
     for n in planes:
         keep &= ~((rel @ n + sz * np.maximum(n, 0).sum()) < -1e-5 * span)
     q0 = rel @ Minv.T
-    g = (Minv * sz).T
-    q = np.stack([q0 + (c & 1) * g[0] + ((c >> 1) & 1) * g[1] + ((c >> 2) & 1) * g[2] for c in range(8)], 1)
+    g = Minv.T   # row k: the step along axis k in q
+    q = np.stack([q0 + sz[:, None] * ((c & 1) * g[0] + ((c >> 1) & 1) * g[1] + ((c >> 2) & 1) * g[2])
+                  for c in range(8)], 1)
     qz = q[..., 2]
     zmax = qz.max(1)
     keep &= zmax > 0
