@@ -1300,3 +1300,30 @@ def test_moving_camera_frames_match_oracle(torch, oracle_mod, move_every):
             _check(b, oracle_mod, ref_hits, ref_rgba, keys=("hits", "rgba"))
     finally:
         m.close()
+
+
+def test_config_version1_struct_keeps_later_fields(torch):
+    """svo_config is versioned by size: a version-1 caller's 128-byte struct (before beam_back_held)
+    sets every field it holds and leaves the context's beam_back_held as it was; a struct larger than
+    the library's is refused."""
+    import ctypes
+    from raytracingtest_amd import _lib
+    m = RaytracingMaster(device=0, capacity_nodes=1 << 10, config={"beam_back_held": 3})
+    try:
+        L = _lib.lib()
+        c = _lib.SvoConfig()
+        c.size = ctypes.sizeof(c)
+        assert L.svo_get_config(m._ctx, ctypes.byref(c)) == 0 and c.beam_back_held == 3 and c.version == 2
+        c.size = 128            # a version-1 caller
+        c.move_every = 7
+        c.beam_back_held = 1    # past its size: not read
+        assert L.svo_set_config(m._ctx, ctypes.byref(c)) == 0
+        got = m.get_config()
+        assert got["move_every"] == 7 and got["beam_back_held"] == 3
+        big = (ctypes.c_uint8 * 256)()
+        hdr = ctypes.cast(big, ctypes.POINTER(_lib.SvoConfig))
+        hdr.contents.size = 256
+        assert L.svo_set_config(m._ctx, hdr) != 0
+        assert m.get_config() == got
+    finally:
+        m.close()
