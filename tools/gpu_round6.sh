@@ -182,6 +182,13 @@ longab)
             done
         done
     done ;;
+orderab)
+    # the periodic order rebuild while costs drift (order_every 32 default / 16 / 8 / 4) on the drop-in loops
+    for rep in a b; do
+        for v in ${EVERY:-32 16 8 4}; do
+            timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main --set order_every=$v > "$out/oe_$v$rep.txt" 2>&1 || exit $?
+        done
+    done ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
