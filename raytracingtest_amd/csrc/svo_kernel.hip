@@ -797,7 +797,10 @@ __device__ __forceinline__ void trace_seg(const LaunchParams &p, FRay &r, uint2 
         const lmask lx = LM_OF(tx <= tc_max), ly = LM_OF(ty <= tc_max), lz = LM_OF(tz <= tc_max);
         const lmask in_span = LM_OF(r.t_min <= tv_max), below_h = LM_OF(tc_max < r.h);
         const lmask before = LM_OF(tc_max < t_start);    // SKIP test (NaN start: never)
-        const lmask arm_now = LM_OF(tc_max >= t_start);  // ARM / STOP tests on the ADVANCE's new t_min
+        // ARM / STOP tests on the ADVANCE's new t_min.  Without segments (a beam start: finite or -inf,
+        // never NaN; tc_max is never NaN, a min of three corner times of which at most two are NaN)
+        // arming is the complement of the SKIP test: one compare fewer per trip
+        const lmask arm_now = SEGS ? LM_OF(tc_max >= t_start) : ~before;
         const lmask stop_now = SEGS ? LM_OF(tc_max >= t_stop) : (lmask)0;
         const uint32_t cm = r.cd16 << sh;
         const lmask descend = act & LM_OF((int32_t)cm < 0) & in_span;

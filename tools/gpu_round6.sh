@@ -189,6 +189,17 @@ orderab)
             timeout -k 10 150 python -u tools/dropin_loop.py --poses flyover,main --set order_every=$v > "$out/oe_$v$rep.txt" 2>&1 || exit $?
         done
     done ;;
+armab)
+    # one compare fewer per trip in the beam loop (arm = not skip): parity first, then interleaved
+    timeout -k 10 500 python -u -m pytest tests/test_gpu_beam.py tests/test_gpu_seg.py tests/test_gpu_fullsize.py -x -q \
+        --timeout 300 --timeout-method thread > "$out/arm_tests.txt" 2>&1 || exit $?
+    for rep in a b c; do
+        for v in new:raytracingtest_amd base:build/ab/base; do
+            n=${v%%:*}; l=$PWD/${v#*:}/libsvo_rt.so
+            SVO_RT_LIB=$l timeout -k 10 150 python -u bench.py --no-extras --cpu-seconds 0 > "$out/am_fly_$n$rep.json" 2>> "$out/am.err" &&
+            SVO_RT_LIB=$l timeout -k 10 150 python -u bench.py --no-extras --cpu-seconds 0 --camera main > "$out/am_main_$n$rep.json" 2>> "$out/am.err" || exit $?
+        done
+    done ;;
 band)
     timeout -k 10 200 python -u tools/band_floor.py --gpus 8 --out "$out/band_floor_8.json" > "$out/band_floor_8.txt" 2>&1 &&
     timeout -k 10 200 python -u tools/band_floor.py --gpus 4 --out "$out/band_floor_4.json" > "$out/band_floor_4.txt" 2>&1 &&
